@@ -1,0 +1,44 @@
+// common.h — shared device helpers for the gfx950 kernels of the victim-query engine.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef short shortx8 __attribute__((ext_vector_type(8)));
+
+#define AE_HIDDEN 768
+#define AE_HEAD_DIM 64
+
+// 32x32 MFMA C/D layout (gfx950, dtype independent): register r of lane l holds
+// row = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), col = l & 31.
+__device__ __forceinline__ int mfma32_row(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  // exact-erf GELU (HF "gelu" = nn.functional.gelu, approximate='none')
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+}
+
+// bf16 round-to-nearest-even of an f32 (NaN-preserving cast lowered to v_cvt_pk_bf16_f32).
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(unsigned short, b);
+}
+
+// Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming.md §5, T1):
+// blocks b and b+8 share an XCD, so give each XCD a contiguous chunk of the tile order.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7, idx = orig >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}

@@ -1,0 +1,569 @@
+// engine.hip — host side of the C-ABI (include/alert_engine.h): weight residency, workspaces and
+// the launch sequence of one victim query batch.
+//
+// One ae_score call = the whole of Model.get_results' device work for a batch
+// (CodeXGLUE/Defect-detection/code/model.py:36-59): pad compaction -> embedding+LN ->
+// 12 x [QKV GEMM -> fused attention -> O GEMM(+res) -> LN -> FFN1 GEMM(+GELU) -> FFN2 GEMM(+res)
+// -> LN] -> task head.  The last layer only needs the CLS row of every sequence (the heads read
+// features[:, 0, :]), so after its K/V are produced its attention, O-projection, LayerNorms and
+// FFN run on the n CLS rows only.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/alert_engine.h"
+
+extern "C" {
+hipError_t ae_launch_gemm_f32(const float*, const float*, const float*, const float*, float*, int,
+                              int, int, int, int, int, int, const int*, hipStream_t);
+hipError_t ae_launch_attention_f32(const float*, float*, const int*, const int*, int, int, int,
+                                   const uint32_t*, int, hipStream_t);
+hipError_t ae_launch_compact(const int*, const int*, const int*, int, int, int, int*, int*, int*,
+                             hipStream_t);
+hipError_t ae_launch_embed_ln(const int*, const int*, const float*, const float*, const float*,
+                              const float*, const float*, float, int, int, float*, hipStream_t);
+hipError_t ae_launch_layernorm(const float*, const float*, const float*, float, int, float*,
+                               hipStream_t);
+hipError_t ae_launch_gather_cls(const float*, const float*, const int*, int, float*, float*,
+                                hipStream_t);
+hipError_t ae_launch_head(const float*, const float*, const float*, const float*, const float*,
+                          int, int, int, float*, hipStream_t);
+hipError_t ae_launch_splice(const int*, const int*, const int*, const int*, int, int, int, int,
+                            int, int*, int*, hipStream_t);
+hipError_t ae_launch_topk(const float*, int, int, int, float*, int*, hipStream_t);
+hipError_t ae_launch_cosine_rank(const float*, const float*, int, int, int, float, float*,
+                                 hipStream_t);
+hipError_t ae_launch_scatter_rows(const float*, const int*, const int*, int, int, int, float*,
+                                  hipStream_t);
+}
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPC(x)                                                                         \
+  do {                                                                                  \
+    hipError_t _e = (x);                                                                \
+    if (_e != hipSuccess)                                                               \
+      return fail(AE_EDEVICE, std::string(#x) + ": " + hipGetErrorString(_e));          \
+  } while (0)
+
+enum { EPI_BIAS = 0, EPI_BIAS_GELU = 1, EPI_BIAS_RESIDUAL = 2 };
+
+struct LayerW {
+  float *wqkv, *bqkv, *wo, *bo, *ln1g, *ln1b, *w1, *b1, *w2, *b2, *ln2g, *ln2b;
+  unsigned short *wqkv_h, *wo_h, *w1_h, *w2_h;  // bf16 copies (AE_PREC_BF16)
+};
+
+struct ProfRec {
+  hipEvent_t a, b;
+  double flop;
+};
+}  // namespace
+
+struct ae_engine {
+  ae_config cfg;
+  int device = 0;
+  std::vector<void*> allocs;
+  float *wemb = nullptr, *pemb = nullptr, *temb = nullptr, *eg = nullptr, *eb = nullptr;
+  std::vector<LayerW> layers;
+  float *hd_w = nullptr, *hd_b = nullptr, *ho_w = nullptr, *ho_b = nullptr;
+  // MLM head
+  float *lm_dw = nullptr, *lm_db = nullptr, *lm_lg = nullptr, *lm_lb = nullptr, *lm_bias = nullptr;
+  // workspaces
+  size_t cap_T = 0, cap_n = 0;
+  float *x = nullptr, *qkv = nullptr, *ctx = nullptr, *tmp = nullptr, *h1 = nullptr;
+  float *xc = nullptr, *cc = nullptr, *tc = nullptr, *hc = nullptr;
+  int *tok_ids = nullptr, *tok_pos = nullptr, *src_col = nullptr, *cu = nullptr, *one = nullptr;
+  float* logits = nullptr;
+  size_t cap_logits = 0;
+  int* pinned_cu = nullptr;
+  size_t cap_pinned = 0;
+  hipEvent_t pinned_ready = nullptr;
+  // profiling
+  int prof_kind = -1;
+  std::vector<ProfRec> prof;
+};
+
+namespace {
+int dev_alloc(ae_engine* e, void** p, size_t bytes) {
+  hipError_t r = hipMalloc(p, bytes ? bytes : 16);
+  if (r != hipSuccess) return fail(AE_ENOMEM, "hipMalloc " + std::to_string(bytes) + " B failed");
+  e->allocs.push_back(*p);
+  return AE_OK;
+}
+void dev_free(ae_engine* e, void* p) {
+  if (!p) return;
+  for (auto& a : e->allocs)
+    if (a == p) { a = nullptr; }
+  (void)hipFree(p);
+}
+
+struct WeightTable {
+  std::map<std::string, const ae_weight_view*> by_name;
+  const ae_weight_view* get(const std::string& n) const {
+    auto it = by_name.find(n);
+    return it == by_name.end() ? nullptr : it->second;
+  }
+};
+
+int upload(ae_engine* e, const WeightTable& wt, const std::string& name, int64_t numel,
+           float** dst) {
+  const ae_weight_view* v = wt.get(name);
+  if (!v) return fail(AE_ENOENT, "missing weight " + name);
+  if (v->numel != numel)
+    return fail(AE_EINVAL, "weight " + name + " has " + std::to_string(v->numel) +
+                               " elements, expected " + std::to_string(numel));
+  int rc = dev_alloc(e, (void**)dst, numel * sizeof(float));
+  if (rc) return rc;
+  HIPC(hipMemcpy(*dst, v->data, numel * sizeof(float), hipMemcpyHostToDevice));
+  return AE_OK;
+}
+
+unsigned short host_f2bf(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (unsigned short)(u >> 16);
+}
+
+int upload_bf16(ae_engine* e, const std::vector<float>& host, unsigned short** dst) {
+  std::vector<unsigned short> h(host.size());
+  for (size_t i = 0; i < host.size(); ++i) h[i] = host_f2bf(host[i]);
+  int rc = dev_alloc(e, (void**)dst, h.size() * 2);
+  if (rc) return rc;
+  HIPC(hipMemcpy(*dst, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+  return AE_OK;
+}
+
+int ensure_workspace(ae_engine* e, size_t T, size_t n) {
+  const size_t H = e->cfg.hidden, F = e->cfg.ffn;
+  if (T > e->cap_T) {
+    size_t nt = T + T / 4 + 128;
+    HIPC(hipDeviceSynchronize());
+    for (void* p : {(void*)e->x, (void*)e->qkv, (void*)e->ctx, (void*)e->tmp, (void*)e->h1,
+                    (void*)e->tok_ids, (void*)e->tok_pos, (void*)e->src_col})
+      dev_free(e, p);
+    int rc = 0;
+    if ((rc = dev_alloc(e, (void**)&e->x, nt * H * 4))) return rc;
+    if ((rc = dev_alloc(e, (void**)&e->qkv, nt * 3 * H * 4))) return rc;
+    if ((rc = dev_alloc(e, (void**)&e->ctx, nt * H * 4))) return rc;
+    if ((rc = dev_alloc(e, (void**)&e->tmp, nt * H * 4))) return rc;
+    if ((rc = dev_alloc(e, (void**)&e->h1, nt * F * 4))) return rc;
+    if ((rc = dev_alloc(e, (void**)&e->tok_ids, nt * 4))) return rc;
+    if ((rc = dev_alloc(e, (void**)&e->tok_pos, nt * 4))) return rc;
+    if ((rc = dev_alloc(e, (void**)&e->src_col, nt * 4))) return rc;
+    e->cap_T = nt;
+  }
+  if (n + 1 > e->cap_n) {
+    size_t nn = n + n / 4 + 64;
+    HIPC(hipDeviceSynchronize());
+    for (void* p : {(void*)e->xc, (void*)e->cc, (void*)e->tc, (void*)e->hc, (void*)e->cu})
+      dev_free(e, p);
+    int rc = 0;
+    if ((rc = dev_alloc(e, (void**)&e->xc, nn * H * 4))) return rc;
+    if ((rc = dev_alloc(e, (void**)&e->cc, nn * H * 4))) return rc;
+    if ((rc = dev_alloc(e, (void**)&e->tc, nn * H * 4))) return rc;
+    if ((rc = dev_alloc(e, (void**)&e->hc, nn * F * 4))) return rc;
+    if ((rc = dev_alloc(e, (void**)&e->cu, (nn + 1) * 4))) return rc;
+    e->cap_n = nn;
+    if (e->pinned_cu) (void)hipHostFree(e->pinned_cu);
+    HIPC(hipHostMalloc((void**)&e->pinned_cu, (nn + 1) * 4, hipHostMallocDefault));
+    e->cap_pinned = nn + 1;
+  }
+  return AE_OK;
+}
+
+// Upload cu_seqlens computed on the host; returns T.
+int upload_cu(ae_engine* e, const int32_t* lens, int n, int L, hipStream_t st, int64_t* T_out) {
+  // the previous upload must have left the pinned buffer
+  HIPC(hipEventSynchronize(e->pinned_ready));
+  int64_t T = 0;
+  e->pinned_cu[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    if (lens[i] < 1 || lens[i] > L)
+      return fail(AE_EINVAL, "lens[" + std::to_string(i) + "]=" + std::to_string(lens[i]) +
+                                 " outside [1, L]");
+    T += lens[i];
+    e->pinned_cu[i + 1] = (int)T;
+  }
+  HIPC(hipMemcpyAsync(e->cu, e->pinned_cu, (size_t)(n + 1) * 4, hipMemcpyHostToDevice, st));
+  HIPC(hipEventRecord(e->pinned_ready, st));
+  *T_out = T;
+  return AE_OK;
+}
+
+// Profiled launch wrapper
+struct Prof {
+  ae_engine* e;
+  hipStream_t st;
+  bool on;
+  ProfRec rec;
+  Prof(ae_engine* e_, hipStream_t s, bool enabled, double flop) : e(e_), st(s), on(enabled) {
+    if (on) {
+      rec.flop = flop;
+      (void)hipEventCreate(&rec.a);
+      (void)hipEventCreate(&rec.b);
+      (void)hipEventRecord(rec.a, st);
+    }
+  }
+  ~Prof() {
+    if (on) {
+      (void)hipEventRecord(rec.b, st);
+      e->prof.push_back(rec);
+    }
+  }
+};
+
+int gemm(ae_engine* e, const float* A, const float* W, const unsigned short* Wh, const float* bias,
+         const float* R, float* C, int M, int N, int K, int epi, hipStream_t st, bool is_ffn1) {
+  const bool prof = (e->prof_kind == AE_KIND_GEMM_ANY) || (e->prof_kind == AE_KIND_GEMM_FFN1 && is_ffn1);
+  Prof p(e, st, prof, 2.0 * M * N * K);
+  (void)Wh;
+  HIPC(ae_launch_gemm_f32(A, W, bias, R, C, M, N, K, K, K, N, epi, nullptr, st));
+  return AE_OK;
+}
+
+// Runs the encoder over compacted tokens; on return the last-layer CLS rows are in e->xc
+// (cls_only) or all rows in e->x.
+int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint32_t* mask_bits,
+                int n, int L, int64_t T, int max_len, bool cls_only, hipStream_t st) {
+  const int H = e->cfg.hidden, F = e->cfg.ffn, NL = e->cfg.layers, heads = e->cfg.heads;
+  const float eps = e->cfg.ln_eps;
+  HIPC(ae_launch_compact(ids, pos, e->cu, n, L, e->cfg.pad_id, e->tok_ids, e->tok_pos, e->src_col,
+                         st));
+  HIPC(ae_launch_embed_ln(e->tok_ids, e->tok_pos, e->wemb, e->pemb, e->temb, e->eg, e->eb, eps,
+                          (int)T, e->cfg.max_pos, e->x, st));
+  for (int li = 0; li < NL; ++li) {
+    const LayerW& w = e->layers[li];
+    const bool last_cls = cls_only && li == NL - 1;
+    int rc;
+    if ((rc = gemm(e, e->x, w.wqkv, w.wqkv_h, w.bqkv, nullptr, e->qkv, (int)T, 3 * H, H, EPI_BIAS,
+                   st, false)))
+      return rc;
+    {
+      const double flop = 0.0;  // attention FLOP are accounted by the caller
+      Prof p(e, st, e->prof_kind == AE_KIND_ATTENTION, flop);
+      HIPC(ae_launch_attention_f32(e->qkv, e->ctx, e->cu, last_cls ? e->one : nullptr,
+                                   last_cls ? 1 : max_len, n, heads, mask_bits, L, st));
+    }
+    if (!last_cls) {
+      if ((rc = gemm(e, e->ctx, w.wo, w.wo_h, w.bo, e->x, e->tmp, (int)T, H, H, EPI_BIAS_RESIDUAL,
+                     st, false)))
+        return rc;
+      HIPC(ae_launch_layernorm(e->tmp, w.ln1g, w.ln1b, eps, (int)T, e->x, st));
+      if ((rc = gemm(e, e->x, w.w1, w.w1_h, w.b1, nullptr, e->h1, (int)T, F, H, EPI_BIAS_GELU, st,
+                     true)))
+        return rc;
+      if ((rc = gemm(e, e->h1, w.w2, w.w2_h, w.b2, e->x, e->tmp, (int)T, H, F, EPI_BIAS_RESIDUAL,
+                     st, false)))
+        return rc;
+      HIPC(ae_launch_layernorm(e->tmp, w.ln2g, w.ln2b, eps, (int)T, e->x, st));
+    } else {
+      HIPC(ae_launch_gather_cls(e->ctx, e->x, e->cu, n, e->cc, e->xc, st));
+      if ((rc = gemm(e, e->cc, w.wo, w.wo_h, w.bo, e->xc, e->tc, n, H, H, EPI_BIAS_RESIDUAL, st,
+                     false)))
+        return rc;
+      HIPC(ae_launch_layernorm(e->tc, w.ln1g, w.ln1b, eps, n, e->xc, st));
+      if ((rc = gemm(e, e->xc, w.w1, w.w1_h, w.b1, nullptr, e->hc, n, F, H, EPI_BIAS_GELU, st,
+                     false)))
+        return rc;
+      if ((rc = gemm(e, e->hc, w.w2, w.w2_h, w.b2, e->xc, e->tc, n, H, F, EPI_BIAS_RESIDUAL, st,
+                     false)))
+        return rc;
+      HIPC(ae_launch_layernorm(e->tc, w.ln2g, w.ln2b, eps, n, e->xc, st));
+    }
+  }
+  return AE_OK;
+}
+
+int check_common(ae_engine* e, const int32_t* ids, const int32_t* lens, int n, int L) {
+  if (!e) return fail(AE_EINVAL, "null engine");
+  if (!ids || !lens) return fail(AE_EINVAL, "null ids/lens");
+  if (n < 0 || L < 2 || L > 4096) return fail(AE_EINVAL, "bad n/L");
+  return AE_OK;
+}
+}  // namespace
+
+extern "C" {
+
+const char* ae_last_error(void) { return g_err.c_str(); }
+const char* ae_version(void) { return "alert-mi355x 0.1 (gfx950)"; }
+
+int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_weights,
+              int32_t device, ae_engine** out) {
+  if (!cfg || !out || (!weights && n_weights)) return fail(AE_EINVAL, "null argument");
+  if (cfg->hidden != 768 || cfg->heads != 12)
+    return fail(AE_EINVAL, "kernels are specialised for hidden=768, heads=12");
+  if (cfg->ffn % 32 || cfg->layers < 1) return fail(AE_EINVAL, "bad ffn/layers");
+  if (cfg->num_labels < 1 || cfg->num_labels > 128) return fail(AE_EINVAL, "num_labels in [1,128]");
+  if (cfg->head_kind == AE_HEAD_SIGMOID1 && cfg->num_labels != 1)
+    return fail(AE_EINVAL, "sigmoid head needs num_labels=1");
+  if (cfg->head_kind == AE_HEAD_PAIR2 && cfg->num_labels != 2)
+    return fail(AE_EINVAL, "pair head needs num_labels=2");
+  if (cfg->precision != AE_PREC_FP32)
+    return fail(AE_EINVAL, "only AE_PREC_FP32 is built in this version");
+  HIPC(hipSetDevice(device));
+  ae_engine* e = new ae_engine();
+  e->cfg = *cfg;
+  e->device = device;
+  WeightTable wt;
+  for (int i = 0; i < n_weights; ++i) wt.by_name[weights[i].name] = &weights[i];
+  const int64_t H = cfg->hidden, F = cfg->ffn, V = cfg->vocab;
+  int rc = 0;
+#define UP(name, numel, dst)                                   \
+  if ((rc = upload(e, wt, name, numel, dst))) {                \
+    std::string m = g_err;                                     \
+    ae_destroy(e);                                             \
+    return fail(rc, m);                                        \
+  }
+  UP("embeddings.word_embeddings.weight", V * H, &e->wemb);
+  UP("embeddings.position_embeddings.weight", (int64_t)cfg->max_pos * H, &e->pemb);
+  UP("embeddings.token_type_embeddings.weight", (int64_t)cfg->type_vocab * H, &e->temb);
+  UP("embeddings.LayerNorm.weight", H, &e->eg);
+  UP("embeddings.LayerNorm.bias", H, &e->eb);
+  e->layers.resize(cfg->layers);
+  for (int l = 0; l < cfg->layers; ++l) {
+    LayerW& w = e->layers[l];
+    std::memset(&w, 0, sizeof(w));
+    const std::string p = "encoder.layer." + std::to_string(l) + ".";
+    // fused QKV: rows [q; k; v]
+    const ae_weight_view* q = wt.get(p + "attention.self.query.weight");
+    const ae_weight_view* k = wt.get(p + "attention.self.key.weight");
+    const ae_weight_view* v = wt.get(p + "attention.self.value.weight");
+    const ae_weight_view* qb = wt.get(p + "attention.self.query.bias");
+    const ae_weight_view* kb = wt.get(p + "attention.self.key.bias");
+    const ae_weight_view* vb = wt.get(p + "attention.self.value.bias");
+    if (!q || !k || !v || !qb || !kb || !vb) {
+      ae_destroy(e);
+      return fail(AE_ENOENT, "missing attention.self weights of layer " + std::to_string(l));
+    }
+    if (q->numel != H * H || k->numel != H * H || v->numel != H * H || qb->numel != H ||
+        kb->numel != H || vb->numel != H) {
+      ae_destroy(e);
+      return fail(AE_EINVAL, "bad attention.self shapes in layer " + std::to_string(l));
+    }
+    std::vector<float> hw(3 * H * H), hb(3 * H);
+    std::memcpy(hw.data(), q->data, H * H * 4);
+    std::memcpy(hw.data() + H * H, k->data, H * H * 4);
+    std::memcpy(hw.data() + 2 * H * H, v->data, H * H * 4);
+    std::memcpy(hb.data(), qb->data, H * 4);
+    std::memcpy(hb.data() + H, kb->data, H * 4);
+    std::memcpy(hb.data() + 2 * H, vb->data, H * 4);
+    if ((rc = dev_alloc(e, (void**)&w.wqkv, hw.size() * 4)) ||
+        (rc = dev_alloc(e, (void**)&w.bqkv, hb.size() * 4))) {
+      std::string m = g_err;
+      ae_destroy(e);
+      return fail(rc, m);
+    }
+    if (hipMemcpy(w.wqkv, hw.data(), hw.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(w.bqkv, hb.data(), hb.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+      ae_destroy(e);
+      return fail(AE_EDEVICE, "weight upload failed");
+    }
+    UP(p + "attention.output.dense.weight", H * H, &w.wo);
+    UP(p + "attention.output.dense.bias", H, &w.bo);
+    UP(p + "attention.output.LayerNorm.weight", H, &w.ln1g);
+    UP(p + "attention.output.LayerNorm.bias", H, &w.ln1b);
+    UP(p + "intermediate.dense.weight", F * H, &w.w1);
+    UP(p + "intermediate.dense.bias", F, &w.b1);
+    UP(p + "output.dense.weight", H * F, &w.w2);
+    UP(p + "output.dense.bias", H, &w.b2);
+    UP(p + "output.LayerNorm.weight", H, &w.ln2g);
+    UP(p + "output.LayerNorm.bias", H, &w.ln2b);
+    if (cfg->precision == AE_PREC_BF16) {
+      auto grab = [&](const std::string& n) {
+        const ae_weight_view* t = wt.get(n);
+        return std::vector<float>(t->data, t->data + t->numel);
+      };
+      if ((rc = upload_bf16(e, hw, &w.wqkv_h)) ||
+          (rc = upload_bf16(e, grab(p + "attention.output.dense.weight"), &w.wo_h)) ||
+          (rc = upload_bf16(e, grab(p + "intermediate.dense.weight"), &w.w1_h)) ||
+          (rc = upload_bf16(e, grab(p + "output.dense.weight"), &w.w2_h))) {
+        std::string m = g_err;
+        ae_destroy(e);
+        return fail(rc, m);
+      }
+    }
+  }
+  if (cfg->head_kind != AE_HEAD_NONE) {
+    const int64_t in_dim = cfg->head_kind == AE_HEAD_PAIR2 ? 2 * H : H;
+    UP("classifier.dense.weight", H * in_dim, &e->hd_w);
+    UP("classifier.dense.bias", H, &e->hd_b);
+    UP("classifier.out_proj.weight", (int64_t)cfg->num_labels * H, &e->ho_w);
+    UP("classifier.out_proj.bias", cfg->num_labels, &e->ho_b);
+  }
+  if (cfg->with_mlm) {
+    UP("lm_head.dense.weight", H * H, &e->lm_dw);
+    UP("lm_head.dense.bias", H, &e->lm_db);
+    UP("lm_head.layer_norm.weight", H, &e->lm_lg);
+    UP("lm_head.layer_norm.bias", H, &e->lm_lb);
+    UP("lm_head.bias", V, &e->lm_bias);  // decoder weight is tied to word_embeddings
+  }
+#undef UP
+  if ((rc = dev_alloc(e, (void**)&e->one, 16))) {
+    ae_destroy(e);
+    return fail(rc, "alloc");
+  }
+  const int one_host[4] = {1, 1, 1, 1};
+  HIPC(hipMemcpy(e->one, one_host, 16, hipMemcpyHostToDevice));
+  HIPC(hipEventCreateWithFlags(&e->pinned_ready, hipEventDisableTiming));
+  HIPC(hipEventRecord(e->pinned_ready, nullptr));
+  HIPC(hipDeviceSynchronize());
+  *out = e;
+  return AE_OK;
+}
+
+int ae_destroy(ae_engine* e) {
+  if (!e) return AE_OK;
+  (void)hipSetDevice(e->device);
+  (void)hipDeviceSynchronize();
+  for (void* p : e->allocs)
+    if (p) (void)hipFree(p);
+  if (e->pinned_cu) (void)hipHostFree(e->pinned_cu);
+  if (e->pinned_ready) (void)hipEventDestroy(e->pinned_ready);
+  for (auto& r : e->prof) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  delete e;
+  return AE_OK;
+}
+
+int ae_score(ae_engine* e, const int32_t* ids, const int32_t* lens, const int32_t* pos,
+             const uint32_t* mask_bits, int32_t n, int32_t L, float* probs_out, void* stream) {
+  int rc = check_common(e, ids, lens, n, L);
+  if (rc) return rc;
+  if (e->cfg.head_kind == AE_HEAD_NONE) return fail(AE_EINVAL, "engine has no task head");
+  if (e->cfg.head_kind == AE_HEAD_PAIR2 && (n & 1)) return fail(AE_EINVAL, "pair head needs even n");
+  if (mask_bits && (L % 32)) return fail(AE_EINVAL, "mask_bits needs L % 32 == 0");
+  if (!probs_out) return fail(AE_EINVAL, "null probs_out");
+  if (n == 0) return AE_OK;
+  HIPC(hipSetDevice(e->device));
+  hipStream_t st = (hipStream_t)stream;
+  if ((rc = ensure_workspace(e, (size_t)n * L, n))) return rc;
+  int64_t T = 0;
+  if ((rc = upload_cu(e, lens, n, L, st, &T))) return rc;
+  int max_len = 0;
+  for (int i = 0; i < n; ++i) max_len = lens[i] > max_len ? lens[i] : max_len;
+  if ((rc = run_encoder(e, ids, pos, mask_bits, n, L, T, max_len, true, st))) return rc;
+  const int kind = e->cfg.head_kind == AE_HEAD_SIGMOID1 ? 0 : (e->cfg.head_kind == AE_HEAD_PAIR2 ? 2 : 1);
+  const int n_out = kind == 2 ? n / 2 : n;
+  HIPC(ae_launch_head(e->xc, e->hd_w, e->hd_b, e->ho_w, e->ho_b, kind, e->cfg.num_labels, n_out,
+                      probs_out, st));
+  return AE_OK;
+}
+
+int ae_encode(ae_engine* e, const int32_t* ids, const int32_t* lens, int32_t n, int32_t L,
+              float* hidden_out, void* stream) {
+  int rc = check_common(e, ids, lens, n, L);
+  if (rc) return rc;
+  if (!hidden_out) return fail(AE_EINVAL, "null hidden_out");
+  if (n == 0) return AE_OK;
+  HIPC(hipSetDevice(e->device));
+  hipStream_t st = (hipStream_t)stream;
+  if ((rc = ensure_workspace(e, (size_t)n * L, n))) return rc;
+  int64_t T = 0;
+  if ((rc = upload_cu(e, lens, n, L, st, &T))) return rc;
+  int max_len = 0;
+  for (int i = 0; i < n; ++i) max_len = lens[i] > max_len ? lens[i] : max_len;
+  if ((rc = run_encoder(e, ids, nullptr, nullptr, n, L, T, max_len, false, st))) return rc;
+  HIPC(ae_launch_scatter_rows(e->x, e->cu, e->src_col, n, L, (int)T, hidden_out, st));
+  return AE_OK;
+}
+
+int ae_mlm_topk(ae_engine* e, const int32_t* ids, int32_t L, int32_t k, float* scores_out,
+                int32_t* ids_out, void* stream) {
+  if (!e || !ids || !scores_out || !ids_out) return fail(AE_EINVAL, "null argument");
+  if (!e->lm_dw) return fail(AE_EINVAL, "engine created without the MLM head (with_mlm=0)");
+  if (L < 1 || L > 4096 || k < 1 || k > 256) return fail(AE_EINVAL, "bad L/k");
+  HIPC(hipSetDevice(e->device));
+  hipStream_t st = (hipStream_t)stream;
+  int rc;
+  if ((rc = ensure_workspace(e, (size_t)L, 1))) return rc;
+  const int32_t lens[1] = {L};
+  int64_t T = 0;
+  if ((rc = upload_cu(e, lens, 1, L, st, &T))) return rc;
+  if ((rc = run_encoder(e, ids, nullptr, nullptr, 1, L, T, L, false, st))) return rc;
+  const int V = e->cfg.vocab, H = e->cfg.hidden;
+  if ((size_t)L * V > e->cap_logits) {
+    HIPC(hipDeviceSynchronize());
+    dev_free(e, e->logits);
+    if ((rc = dev_alloc(e, (void**)&e->logits, (size_t)L * V * 4))) return rc;
+    e->cap_logits = (size_t)L * V;
+  }
+  // lm_head: dense -> gelu -> LN -> decoder (tied word embeddings) + bias
+  HIPC(ae_launch_gemm_f32(e->x, e->lm_dw, e->lm_db, nullptr, e->tmp, L, H, H, H, H, H,
+                          EPI_BIAS_GELU, nullptr, st));
+  HIPC(ae_launch_layernorm(e->tmp, e->lm_lg, e->lm_lb, e->cfg.ln_eps, L, e->ctx, st));
+  HIPC(ae_launch_gemm_f32(e->ctx, e->wemb, e->lm_bias, nullptr, e->logits, L, V, H, H, H, V,
+                          EPI_BIAS, nullptr, st));
+  HIPC(ae_launch_topk(e->logits, L, V, k, scores_out, ids_out, st));
+  return AE_OK;
+}
+
+int ae_splice(const int32_t* word_tok, const int32_t* word_off, const int32_t* mut_words,
+              const int32_t* mut_off, int32_t n_mut, int32_t L, int32_t cls_id, int32_t sep_id,
+              int32_t pad_id, int32_t* ids_out, int32_t* lens_out, void* stream) {
+  if (!word_tok || !word_off || !mut_words || !mut_off || !ids_out || !lens_out)
+    return fail(AE_EINVAL, "null argument");
+  if (n_mut < 0 || L < 2) return fail(AE_EINVAL, "bad n_mut/L");
+  HIPC(ae_launch_splice(word_tok, word_off, mut_words, mut_off, n_mut, L, cls_id, sep_id, pad_id,
+                        ids_out, lens_out, (hipStream_t)stream));
+  return AE_OK;
+}
+
+int ae_topk(const float* x, int32_t rows, int32_t cols, int32_t k, float* vals_out,
+            int32_t* idx_out, void* stream) {
+  if (!x || !vals_out || !idx_out) return fail(AE_EINVAL, "null argument");
+  if (rows < 0 || cols < 1 || k < 1 || k > 256 || k > cols) return fail(AE_EINVAL, "bad shape");
+  HIPC(ae_launch_topk(x, rows, cols, k, vals_out, idx_out, (hipStream_t)stream));
+  return AE_OK;
+}
+
+int ae_cosine_rank(const float* ref, const float* cand, int32_t n, int32_t span_len,
+                   int32_t hidden, float eps, float* sims_out, void* stream) {
+  if (!ref || !cand || !sims_out) return fail(AE_EINVAL, "null argument");
+  if (n < 0 || span_len < 1 || hidden < 1) return fail(AE_EINVAL, "bad shape");
+  HIPC(ae_launch_cosine_rank(ref, cand, n, span_len, hidden, eps, sims_out, (hipStream_t)stream));
+  return AE_OK;
+}
+
+int ae_set_profiling(ae_engine* e, int32_t kind, int32_t enabled) {
+  if (!e) return fail(AE_EINVAL, "null engine");
+  e->prof_kind = enabled ? kind : -1;
+  return AE_OK;
+}
+
+int ae_kernel_time(ae_engine* e, double* ms_total, int64_t* launches, double* flop_total) {
+  if (!e || !ms_total || !launches || !flop_total) return fail(AE_EINVAL, "null argument");
+  HIPC(hipSetDevice(e->device));
+  double ms = 0, fl = 0;
+  int64_t cnt = 0;
+  for (auto& r : e->prof) {
+    HIPC(hipEventSynchronize(r.b));
+    float t = 0.f;
+    HIPC(hipEventElapsedTime(&t, r.a, r.b));
+    ms += t;
+    fl += r.flop;
+    ++cnt;
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  e->prof.clear();
+  *ms_total = ms;
+  *launches = cnt;
+  *flop_total = fl;
+  return AE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,263 @@
+// rowops.hip — pad compaction, fused embedding gather + LayerNorm, LayerNorm, CLS gather and the
+// task heads.  All are row kernels over 768-wide f32 rows: one wave per row, 12 floats per lane
+// (3 x float4, coalesced 1 KiB per wave-instruction), wave-shuffle reductions.
+//
+// Reference semantics (HF RoBERTa eager, reached from CodeXGLUE/Defect-detection/code/model.py:25):
+//   position ids  = cumsum(ids != pad) * (ids != pad) + pad   (modeling_roberta.py:142-155)
+//   embeddings    = LN(word[id] + pos[position] + type[0]), eps 1e-5
+//   heads: Devign   sigmoid(out_proj(tanh(dense(h_cls))))            model.py:24-34
+//          AA       softmax(out_proj(tanh(dense(h_cls))))            Authorship-Attribution/code/model.py:13-54
+//          clone    softmax(out_proj(tanh(dense(cat(h_cls_a, h_cls_b)))))  Clone-detection-BigCloneBench/code/model.py:13-53
+#include "common.h"
+
+// ---------------------------------------------------------------------------------------------
+// Pad compaction: one workgroup per sequence.  Writes the non-pad ids of row s, in order, to
+// tok_ids[cu[s] + j] and their position ids (explicit `pos` row, or the RoBERTa rule pad+1+j).
+// Also records where each compacted token came from (src_col) for ae_encode scatter-back.
+__global__ __launch_bounds__(256) void compact_kernel(const int* __restrict__ ids,
+                                                      const int* __restrict__ pos,
+                                                      const int* __restrict__ cu, int L, int pad,
+                                                      int* __restrict__ tok_ids,
+                                                      int* __restrict__ tok_pos,
+                                                      int* __restrict__ src_col) {
+  __shared__ int wave_tot[4];
+  __shared__ int carry;
+  const int s = blockIdx.x;
+  const int base = cu[s];
+  const int* row = ids + (size_t)s * L;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (int c0 = 0; c0 < L; c0 += 256) {
+    const int c = c0 + tid;
+    const int id = c < L ? row[c] : pad;
+    const int keep = id != pad;
+    const unsigned long long bal = __ballot(keep);
+    const int before = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wave_tot[wave] = __popcll(bal);
+    __syncthreads();
+    int off = carry;
+    for (int w = 0; w < wave; ++w) off += wave_tot[w];
+    if (keep) {
+      const int j = off + before;
+      tok_ids[base + j] = id;
+      tok_pos[base + j] = pos ? pos[(size_t)s * L + c] : pad + 1 + j;
+      if (src_col) src_col[base + j] = c;
+    }
+    __syncthreads();
+    if (tid == 0) carry += wave_tot[0] + wave_tot[1] + wave_tot[2] + wave_tot[3];
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ void ln_row_store(float (&v)[12], const float* __restrict__ g,
+                                             const float* __restrict__ b, float eps,
+                                             float* __restrict__ out, int lane) {
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) sum += v[i];
+  const float mean = wave_sum(sum) * (1.f / AE_HIDDEN);
+  float sq = 0.f;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const float d = v[i] - mean;
+    sq += d * d;
+  }
+  const float var = wave_sum(sq) * (1.f / AE_HIDDEN);
+  const float rstd = rsqrtf(var + eps);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const int col = c * 256 + lane * 4;
+    const floatx4 gg = *reinterpret_cast<const floatx4*>(g + col);
+    const floatx4 bb = *reinterpret_cast<const floatx4*>(b + col);
+    floatx4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (v[4 * c + e] - mean) * rstd * gg[e] + bb[e];
+    *reinterpret_cast<floatx4*>(out + col) = o;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Embedding gather + add + LayerNorm.  4 rows per 256-thread workgroup.
+__global__ __launch_bounds__(256) void embed_ln_kernel(
+    const int* __restrict__ tok_ids, const int* __restrict__ tok_pos,
+    const float* __restrict__ wemb, const float* __restrict__ pemb,
+    const float* __restrict__ temb, const float* __restrict__ g, const float* __restrict__ b,
+    float eps, int T, int max_pos, float* __restrict__ x) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= T) return;
+  const int id = tok_ids[row];
+  int p = tok_pos[row];
+  p = p < 0 ? 0 : (p >= max_pos ? max_pos - 1 : p);  // bound-check (GCB hazard)
+  const float* we = wemb + (size_t)id * AE_HIDDEN;
+  const float* pe = pemb + (size_t)p * AE_HIDDEN;
+  float v[12];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const int col = c * 256 + lane * 4;
+    const floatx4 a = *reinterpret_cast<const floatx4*>(we + col);
+    const floatx4 bb = *reinterpret_cast<const floatx4*>(pe + col);
+    const floatx4 t = *reinterpret_cast<const floatx4*>(temb + col);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[4 * c + e] = (a[e] + t[e]) + bb[e];
+  }
+  ln_row_store(v, g, b, eps, x + (size_t)row * AE_HIDDEN, lane);
+}
+
+// In-place (or out-of-place) LayerNorm of T rows.
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ in,
+                                                        const float* __restrict__ g,
+                                                        const float* __restrict__ b, float eps,
+                                                        int T, float* __restrict__ out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= T) return;
+  const float* r = in + (size_t)row * AE_HIDDEN;
+  float v[12];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const floatx4 a = *reinterpret_cast<const floatx4*>(r + c * 256 + lane * 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[4 * c + e] = a[e];
+  }
+  ln_row_store(v, g, b, eps, out + (size_t)row * AE_HIDDEN, lane);
+}
+
+// Gather the first (CLS) row of every sequence from two [T,768] matrices into compact [n,768].
+__global__ __launch_bounds__(256) void gather_cls_kernel(const float* __restrict__ a,
+                                                         const float* __restrict__ b,
+                                                         const int* __restrict__ cu, int n,
+                                                         float* __restrict__ ac,
+                                                         float* __restrict__ bc) {
+  const int s = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (s >= n) return;
+  const size_t src = (size_t)cu[s] * AE_HIDDEN;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const int col = c * 256 + lane * 4;
+    *reinterpret_cast<floatx4*>(ac + (size_t)s * AE_HIDDEN + col) =
+        *reinterpret_cast<const floatx4*>(a + src + col);
+    *reinterpret_cast<floatx4*>(bc + (size_t)s * AE_HIDDEN + col) =
+        *reinterpret_cast<const floatx4*>(b + src + col);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Classification heads over compact CLS rows h[n_seq][768].  One workgroup per output row.
+//   kind 0: sigmoid1  -> out[row] = sigmoid(...)            (num_labels must be 1)
+//   kind 1: softmaxN  -> out[row][0..C) = softmax(...)
+//   kind 2: pair2     -> features = cat(h[2row], h[2row+1]) (1536) ; softmax over 2
+__global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ h,
+                                                   const float* __restrict__ wd,
+                                                   const float* __restrict__ bd,
+                                                   const float* __restrict__ wo,
+                                                   const float* __restrict__ bo, int kind, int C,
+                                                   float* __restrict__ out) {
+  __shared__ float feat[2 * AE_HIDDEN];
+  __shared__ float hid[AE_HIDDEN];
+  __shared__ float logit[128];
+  const int row = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int in_dim = kind == 2 ? 2 * AE_HIDDEN : AE_HIDDEN;
+  const float* src = h + (size_t)row * (kind == 2 ? 2 : 1) * AE_HIDDEN;
+  for (int i = tid; i < in_dim; i += 256) feat[i] = src[i];
+  __syncthreads();
+  // dense + tanh: one wave per output neuron, lanes stride over the input (coalesced W rows)
+  for (int o = wave; o < AE_HIDDEN; o += 4) {
+    const float* wr = wd + (size_t)o * in_dim;
+    float acc = 0.f;
+    for (int k = lane; k < in_dim; k += 64) acc += wr[k] * feat[k];
+    acc = wave_sum(acc);
+    if (lane == 0) hid[o] = tanhf(acc + bd[o]);
+  }
+  __syncthreads();
+  for (int o = wave; o < C; o += 4) {
+    const float* wr = wo + (size_t)o * AE_HIDDEN;
+    float acc = 0.f;
+    for (int k = lane; k < AE_HIDDEN; k += 64) acc += wr[k] * hid[k];
+    acc = wave_sum(acc);
+    if (lane == 0) logit[o] = acc + bo[o];
+  }
+  __syncthreads();
+  if (wave == 0) {
+    if (kind == 0) {
+      if (lane == 0) out[row] = 1.f / (1.f + expf(-logit[0]));
+    } else {
+      float mx = -INFINITY;
+      for (int c = lane; c < C; c += 64) mx = fmaxf(mx, logit[c]);
+      mx = wave_max(mx);
+      float sm = 0.f;
+      for (int c = lane; c < C; c += 64) sm += expf(logit[c] - mx);
+      sm = wave_sum(sm);
+      for (int c = lane; c < C; c += 64) out[(size_t)row * C + c] = expf(logit[c] - mx) / sm;
+    }
+  }
+}
+
+// Scatter compacted rows back to the padded [n, L, 768] layout (ae_encode).
+__global__ __launch_bounds__(256) void scatter_rows_kernel(const float* __restrict__ x,
+                                                           const int* __restrict__ cu,
+                                                           const int* __restrict__ src_col, int n,
+                                                           int L, int T, float* __restrict__ out) {
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (t >= T) return;
+  int lo = 0, hi = n;  // find s with cu[s] <= t < cu[s+1]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (cu[mid] <= t) lo = mid; else hi = mid;
+  }
+  const size_t dst = ((size_t)lo * L + src_col[t]) * AE_HIDDEN;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const int col = c * 256 + lane * 4;
+    *reinterpret_cast<floatx4*>(out + dst + col) =
+        *reinterpret_cast<const floatx4*>(x + (size_t)t * AE_HIDDEN + col);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+extern "C" {
+hipError_t ae_launch_scatter_rows(const float* x, const int* cu, const int* src_col, int n, int L,
+                                  int T, float* out, hipStream_t st) {
+  if (T <= 0) return hipSuccess;
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3((T + 3) / 4), dim3(256), 0, st, x, cu, src_col, n,
+                     L, T, out);
+  return hipGetLastError();
+}
+hipError_t ae_launch_compact(const int* ids, const int* pos, const int* cu, int n, int L, int pad,
+                             int* tok_ids, int* tok_pos, int* src_col, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(compact_kernel, dim3(n), dim3(256), 0, st, ids, pos, cu, L, pad, tok_ids,
+                     tok_pos, src_col);
+  return hipGetLastError();
+}
+hipError_t ae_launch_embed_ln(const int* tok_ids, const int* tok_pos, const float* wemb,
+                              const float* pemb, const float* temb, const float* g, const float* b,
+                              float eps, int T, int max_pos, float* x, hipStream_t st) {
+  if (T <= 0) return hipSuccess;
+  hipLaunchKernelGGL(embed_ln_kernel, dim3((T + 3) / 4), dim3(256), 0, st, tok_ids, tok_pos, wemb,
+                     pemb, temb, g, b, eps, T, max_pos, x);
+  return hipGetLastError();
+}
+hipError_t ae_launch_layernorm(const float* in, const float* g, const float* b, float eps, int T,
+                               float* out, hipStream_t st) {
+  if (T <= 0) return hipSuccess;
+  hipLaunchKernelGGL(layernorm_kernel, dim3((T + 3) / 4), dim3(256), 0, st, in, g, b, eps, T, out);
+  return hipGetLastError();
+}
+hipError_t ae_launch_gather_cls(const float* a, const float* b, const int* cu, int n, float* ac,
+                                float* bc, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gather_cls_kernel, dim3((n + 3) / 4), dim3(256), 0, st, a, b, cu, n, ac, bc);
+  return hipGetLastError();
+}
+hipError_t ae_launch_head(const float* h, const float* wd, const float* bd, const float* wo,
+                          const float* bo, int kind, int C, int n_out, float* out, hipStream_t st) {
+  if (n_out <= 0) return hipSuccess;
+  hipLaunchKernelGGL(head_kernel, dim3(n_out), dim3(256), 0, st, h, wd, bd, wo, bo, kind, C, out);
+  return hipGetLastError();
+}
+}

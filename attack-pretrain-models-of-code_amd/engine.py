@@ -1,0 +1,223 @@
+"""ctypes binding of the C-ABI in include/alert_engine.h (lib/libalert_engine.so).
+
+There is no CPU or PyTorch fallback: if the HIP library is missing or fails to load, every entry
+point raises.  Device buffers are torch tensors (torch is the allocator / stream provider); the
+engine owns its weights and workspaces in HBM.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import LIB_PATH
+from .weights import CODEBERT, RobertaShape
+
+AE_HEAD = {"sigmoid1": 0, "softmaxN": 1, "pair2": 2, "none": 3}
+AE_PREC = {"fp32": 0, "bf16": 1}
+AE_KIND = {"gemm_ffn1": 0, "gemm_any": 1, "attention": 2}
+
+
+class AeConfig(ctypes.Structure):
+    _fields_ = [("layers", ctypes.c_int32), ("hidden", ctypes.c_int32), ("heads", ctypes.c_int32),
+                ("ffn", ctypes.c_int32), ("vocab", ctypes.c_int32), ("max_pos", ctypes.c_int32),
+                ("type_vocab", ctypes.c_int32), ("num_labels", ctypes.c_int32),
+                ("head_kind", ctypes.c_int32), ("precision", ctypes.c_int32),
+                ("pad_id", ctypes.c_int32), ("with_mlm", ctypes.c_int32),
+                ("ln_eps", ctypes.c_float)]
+
+
+class AeWeightView(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("data", ctypes.c_void_p), ("numel", ctypes.c_int64)]
+
+
+# every symbol include/alert_engine.h declares (checked by tests/test_abi.py)
+EXPORTS = ("ae_create", "ae_destroy", "ae_score", "ae_encode", "ae_mlm_topk", "ae_splice",
+           "ae_topk", "ae_cosine_rank", "ae_set_profiling", "ae_kernel_time", "ae_last_error",
+           "ae_version")
+
+_LIB = None
+
+
+def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
+    """Load (once) the engine library.  torch must be imported first so that the library binds to
+    the HIP runtime torch already loaded (one runtime per process: shared streams and pointers)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    import torch  # noqa: F401  (HIP runtime first)
+
+    p = str(path or LIB_PATH)
+    if not os.path.exists(p):
+        raise RuntimeError(f"HIP engine library not built: {p} is missing (run `make` or "
+                           f"__graft_entry__.build()); there is no CPU fallback")
+    lib = ctypes.CDLL(p)
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    lib.ae_create.argtypes = [ctypes.POINTER(AeConfig), ctypes.POINTER(AeWeightView), i32, i32,
+                              ctypes.POINTER(vp)]
+    lib.ae_destroy.argtypes = [vp]
+    lib.ae_score.argtypes = [vp, vp, vp, vp, vp, i32, i32, vp, vp]
+    lib.ae_encode.argtypes = [vp, vp, vp, i32, i32, vp, vp]
+    lib.ae_mlm_topk.argtypes = [vp, vp, i32, i32, vp, vp, vp]
+    lib.ae_splice.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp]
+    lib.ae_topk.argtypes = [vp, i32, i32, i32, vp, vp, vp]
+    lib.ae_cosine_rank.argtypes = [vp, vp, i32, i32, i32, ctypes.c_float, vp, vp]
+    lib.ae_set_profiling.argtypes = [vp, i32, i32]
+    lib.ae_kernel_time.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64),
+                                   ctypes.POINTER(ctypes.c_double)]
+    lib.ae_last_error.restype = ctypes.c_char_p
+    lib.ae_version.restype = ctypes.c_char_p
+    for name in EXPORTS:
+        if name not in ("ae_last_error", "ae_version"):
+            getattr(lib, name).restype = ctypes.c_int
+    _LIB = lib
+    return lib
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        msg = _LIB.ae_last_error().decode(errors="replace") if _LIB is not None else ""
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+def _ptr(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(None)
+
+
+def _stream(stream=None):
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class Engine:
+    """One RoBERTa victim (or MLM) resident on one GPU."""
+
+    def __init__(self, state_dict: dict[str, np.ndarray], head: str = "sigmoid1",
+                 num_labels: int = 1, precision: str = "fp32", device: int = 0,
+                 with_mlm: bool = False, shape: RobertaShape = CODEBERT):
+        import torch
+
+        self.lib = load_library()
+        if not torch.cuda.is_available():
+            raise RuntimeError("apmc_amd.Engine needs a ROCm GPU (torch.cuda.is_available() is "
+                               "False); there is no CPU fallback")
+        self.device = device
+        self.head = head
+        self.num_labels = num_labels
+        self.shape = shape
+        self.pad_id = shape.pad_id
+        cfg = AeConfig(shape.layers, shape.hidden, shape.heads, shape.ffn, shape.vocab,
+                       shape.max_pos, shape.type_vocab, num_labels, AE_HEAD[head],
+                       AE_PREC[precision], shape.pad_id, int(with_mlm), shape.ln_eps)
+        keep = []
+        views = (AeWeightView * len(state_dict))()
+        for i, (k, v) in enumerate(state_dict.items()):
+            a = np.ascontiguousarray(v, dtype=np.float32)
+            keep.append(a)
+            views[i] = AeWeightView(k.encode(), a.ctypes.data, a.size)
+        handle = ctypes.c_void_p()
+        torch.cuda.set_device(device)
+        _check(self.lib.ae_create(ctypes.byref(cfg), views, len(state_dict), device,
+                                  ctypes.byref(handle)), "ae_create")
+        self.handle = handle
+        self.out_cols = 1 if head == "sigmoid1" else num_labels
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.ae_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------------------------------
+    def score(self, ids, lens: np.ndarray, pos=None, mask_bits=None, out=None, stream=None):
+        """ids: device int32 [n, L]; lens: host int32 [n] (non-pad counts).  Returns device
+        float32 [n_out, C] (asynchronous on `stream`)."""
+        import torch
+
+        n, L = ids.shape
+        assert ids.dtype == torch.int32 and ids.is_cuda and ids.is_contiguous()
+        lens = np.ascontiguousarray(lens, dtype=np.int32)
+        assert lens.shape == (n,)
+        n_out = n // 2 if self.head == "pair2" else n
+        if out is None:
+            out = torch.empty((n_out, self.out_cols), dtype=torch.float32, device=ids.device)
+        _check(self.lib.ae_score(self.handle, _ptr(ids), ctypes.c_void_p(lens.ctypes.data),
+                                 _ptr(pos), _ptr(mask_bits), n, L, _ptr(out), _stream(stream)),
+               "ae_score")
+        return out
+
+    def encode(self, ids, lens: np.ndarray, stream=None):
+        import torch
+
+        n, L = ids.shape
+        lens = np.ascontiguousarray(lens, dtype=np.int32)
+        out = torch.zeros((n, L, self.shape.hidden), dtype=torch.float32, device=ids.device)
+        _check(self.lib.ae_encode(self.handle, _ptr(ids), ctypes.c_void_p(lens.ctypes.data), n, L,
+                                  _ptr(out), _stream(stream)), "ae_encode")
+        return out
+
+    def mlm_topk(self, ids, k: int, stream=None):
+        import torch
+
+        (L,) = ids.shape
+        scores = torch.empty((L, k), dtype=torch.float32, device=ids.device)
+        idx = torch.empty((L, k), dtype=torch.int32, device=ids.device)
+        _check(self.lib.ae_mlm_topk(self.handle, _ptr(ids), L, k, _ptr(scores), _ptr(idx),
+                                    _stream(stream)), "ae_mlm_topk")
+        return scores, idx
+
+    def set_profiling(self, kind: str, enabled: bool = True):
+        _check(self.lib.ae_set_profiling(self.handle, AE_KIND[kind], int(enabled)),
+               "ae_set_profiling")
+
+    def kernel_time(self):
+        ms, cnt, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+        _check(self.lib.ae_kernel_time(self.handle, ctypes.byref(ms), ctypes.byref(cnt),
+                                       ctypes.byref(fl)), "ae_kernel_time")
+        return ms.value, cnt.value, fl.value
+
+
+# ---------------------------------------------------------------------------------------------
+# engine-free device ops
+def splice(word_tok, word_off, mut_words, mut_off, n_mut: int, L: int, cls_id=0, sep_id=2,
+           pad_id=1, stream=None):
+    import torch
+
+    lib = load_library()
+    dev = word_tok.device
+    ids = torch.empty((n_mut, L), dtype=torch.int32, device=dev)
+    lens = torch.empty((n_mut,), dtype=torch.int32, device=dev)
+    _check(lib.ae_splice(_ptr(word_tok), _ptr(word_off), _ptr(mut_words), _ptr(mut_off), n_mut, L,
+                         cls_id, sep_id, pad_id, _ptr(ids), _ptr(lens), _stream(stream)),
+           "ae_splice")
+    return ids, lens
+
+
+def topk(x, k: int, stream=None):
+    import torch
+
+    rows, cols = x.shape
+    vals = torch.empty((rows, k), dtype=torch.float32, device=x.device)
+    idx = torch.empty((rows, k), dtype=torch.int32, device=x.device)
+    _check(load_library().ae_topk(_ptr(x), rows, cols, k, _ptr(vals), _ptr(idx), _stream(stream)),
+           "ae_topk")
+    return vals, idx
+
+
+def cosine_rank(ref, cand, eps: float = 1e-6, stream=None):
+    import torch
+
+    n, span, hidden = cand.shape
+    sims = torch.empty((n,), dtype=torch.float32, device=cand.device)
+    _check(load_library().ae_cosine_rank(_ptr(ref), _ptr(cand), n, span, hidden,
+                                         ctypes.c_float(eps), _ptr(sims), _stream(stream)),
+           "ae_cosine_rank")
+    return sims

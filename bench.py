@@ -1,0 +1,191 @@
+"""Benchmark of the victim-query hot path (BASELINE.json metric, config 2 workload shape).
+
+A "step" = one Model.get_results-equivalent pass of the engine over one GA population batch of
+synthetic mutants: B (=64, GA eval_batch_size, CodeXGLUE/Defect-detection/README.md:261) sequences
+x L=512 tokens (no padding, CLS=0 / SEP=2, interior ids uniform in [4, 50263], seed 0+rank),
+scored by the CodeBERT-shaped Devign victim (seeded synthetic weights: no checkpoint offline).
+Inputs are resident in HBM before the timed region.  Per-GPU work is fixed (weak scaling): each
+rank scores its own batches; there is no data-path collective.  The only collectives are the
+barrier around the timed region and the MAX-reduction of the elapsed time.
+
+Prints ONE JSON line (rank 0).  `roofline` is the dominant kernel (the FFN1 GEMM,
+[T,768]x[768,3072] + bias + GELU) timed live with HIP events on the launch stream;
+`cpu_baseline` is oracle/roberta_cpu.py (PyTorch-CPU fp32 eager restatement) on host cores.
+"""
+import argparse
+import glob
+import json
+import os
+import pathlib
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import _apmc  # noqa: E402,F401
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32-input MFMA dense peak (spec)
+BF16_MFMA_PEAK_TFLOPS = 2516.6  # dense bf16 (spec, no sparsity)
+METRIC = "victim queries/sec + attacked examples/min (node), CodeBERT Devign GA attack"
+
+
+def flops_per_query(L, C=1):
+    per_tok = 2 * (4 * 768 * 768 + 2 * 768 * 3072)
+    return 12 * (L * per_tok + 4 * L * L * 768) + 2 * 768 * 768 + 2 * 768 * C
+
+
+def pmc_traffic_per_launch():
+    """HBM bytes per FFN1 launch from the committed rocprofv3 PMC summary (profiles/*pmc*.json),
+    or None."""
+    for f in sorted(glob.glob(str(ROOT / "profiles" / "*pmc*ffn1*.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+            return float(d["hbm_bytes_per_launch"])
+        except Exception:
+            continue
+    return None
+
+
+def cpu_baseline(L, seconds, threads):
+    from apmc_amd.weights import synthetic_state_dict
+    from oracle import roberta_cpu as ora
+
+    torch.set_num_threads(threads)
+    sd = synthetic_state_dict(seed=0, head="sigmoid1")
+    rng = np.random.default_rng(0)
+    B = 4
+    ids = rng.integers(4, 50264, size=(B, L)).astype(np.int64)
+    ids[:, 0], ids[:, -1] = 0, 2
+    ora.score(sd, ids[:1, :64], "sigmoid1")  # warm up allocator / threads
+    done, t0 = 0, time.perf_counter()
+    while True:
+        ora.score(sd, ids, "sigmoid1")
+        done += B
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": done / el, "unit": "victim queries/s", "cores": threads, "kind": "port",
+            "sample": f"{done} queries of L={L} (batches of {B}) in {el:.1f} s, "
+                      f"oracle/roberta_cpu.py fp32 eager, torch threads={threads}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--seq", type=int, default=512)
+    ap.add_argument("--precision", default="fp32", choices=["fp32"])
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device(f"cuda:{local if world > 1 else 0}")
+
+    from apmc_amd.engine import Engine
+    from apmc_amd.weights import synthetic_state_dict
+
+    eng = Engine(synthetic_state_dict(seed=0, head="sigmoid1"), head="sigmoid1", num_labels=1,
+                 precision=args.precision, device=dev.index)
+    B, L = args.batch, args.seq
+    rng = np.random.default_rng(0 + rank)
+    ids = rng.integers(4, 50264, size=(B, L)).astype(np.int32)
+    ids[:, 0], ids[:, -1] = 0, 2
+    lens = np.full((B,), L, dtype=np.int32)
+    ids_dev = torch.from_numpy(ids).to(dev)
+    out = torch.empty((B, 1), dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    for _ in range(args.warmup):
+        eng.score(ids_dev, lens, out=out)
+    torch.cuda.synchronize(dev)
+    eng.kernel_time()  # drop anything recorded so far
+    eng.set_profiling("gemm_ffn1", True)
+
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.score(ids_dev, lens, out=out, stream=stream)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    eng.set_profiling("gemm_ffn1", False)
+    k_ms, k_n, k_flop = eng.kernel_time()
+
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        kt = torch.tensor([k_ms, float(k_n), k_flop], dtype=torch.float64, device=dev)
+        dist.all_reduce(kt, op=dist.ReduceOp.SUM)
+        k_ms, k_n, k_flop = float(kt[0]), int(kt[1]), float(kt[2])
+
+    probs = out.cpu().numpy()[:, 0]
+    total_q = world * args.steps * B
+    value = total_q / elapsed
+    per_launch_s = (k_ms / 1e3) / max(k_n, 1)
+    achieved = (k_flop / max(k_n, 1)) / per_launch_s / 1e12 if k_n else None
+    peak = FP32_MFMA_PEAK_TFLOPS
+    res = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "victim queries/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (seeded RoBERTa-base weights; uniform token ids; no checkpoint offline)",
+        "config": {"workload": "CodeBERT Devign victim scoring of one GA mutant population per "
+                               "step (config 2 shape: eval_batch_size 64 x block 512)",
+                   "global_batch": B * world, "seq_len": L, "parallelism": f"dp{world} (example shards)"},
+        "roofline": {
+            "bound": "mfma",
+            "kernel": "gemm_f32_nt_kernel<EPI_BIAS_GELU> (FFN1 [T,768]x[768,3072])",
+            "achieved": round(achieved, 3) if achieved else None,
+            "peak": peak,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4) if achieved else None,
+            "traffic": pmc_traffic_per_launch(),
+            "launches": k_n,
+            "avg_launch_us": round(per_launch_s * 1e6, 2),
+            "flop_per_launch": (k_flop / k_n) if k_n else None,
+        },
+        "whole_step_tflops": round(flops_per_query(L) * total_q / elapsed / 1e12, 3),
+        "whole_step_frac_of_fp32_peak": round(flops_per_query(L) * total_q / elapsed / 1e12 / world / peak, 4),
+        "probs_checksum": float(np.round(probs.astype(np.float64).sum(), 6)),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        res["cpu_baseline"] = cpu_baseline(L, args.cpu_seconds, threads)
+        res["speedup_vs_cpu"] = round(value / res["cpu_baseline"]["value"], 2)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

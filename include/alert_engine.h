@@ -1,0 +1,156 @@
+/*
+ * alert_engine.h — C-ABI of the MI355X victim-query engine.
+ *
+ * This is the drop-in boundary below ALERT's `Model.get_results` (the victim
+ * query boundary) and below the masked-LM substitute generation path.  Every
+ * entry point is plain C: pointers, sizes, ints, no C++ or torch types.  The
+ * Python host side (`attack-pretrain-models-of-code_amd/engine.py`) binds it
+ * with ctypes on torch-owned device buffers; INTEGRATION.md shows the binding a
+ * maintainer adds on the reference side.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the
+ * reference snapshot):
+ *   ae_create     <- RobertaForSequenceClassification/RobertaForMaskedLM construction +
+ *                    Model.load_state_dict(...) + .to("cuda")
+ *                    (CodeXGLUE/Defect-detection/code/gi_attack.py:122-152)
+ *   ae_score      <- Model.forward + the per-batch loop of Model.get_results
+ *                    (CodeXGLUE/Defect-detection/code/model.py:24-59; clone head
+ *                    CodeXGLUE/Clone-detection-BigCloneBench/code/model.py:13-85;
+ *                    authorship head CodeXGLUE/Authorship-Attribution/code/model.py:13-91;
+ *                    GraphCodeBERT GraphCodeBERT/Defect-detection/code/model.py:24-45)
+ *   ae_splice     <- the text-level mutant construction + re-tokenisation
+ *                    (python_parser/run_parser.py:218-266 get_example/get_example_batch,
+ *                    CodeXGLUE/Defect-detection/code/attacker.py:38-45 convert_code_to_features)
+ *                    expressed on token ids: word-id sequences -> padded [n, L] ids.
+ *   ae_mlm_topk   <- codebert_mlm(input_ids)[0] + torch.topk(., 60, -1)
+ *                    (CodeXGLUE/Defect-detection/preprocess/get_substitutes.py:62-63)
+ *   ae_encode     <- codebert_mlm.roberta(ids)[0] (get_substitutes.py:73,105)
+ *   ae_cosine_rank<- CosineSimilarity(dim=1) summed over the sub-word span / L_sub
+ *                    (get_substitutes.py:75,108)
+ *
+ * Conventions
+ *   - Every function returns 0 on success or a negative AE_E* code; the
+ *     message of the last failure on the calling thread is ae_last_error().
+ *   - The engine owns its weights and workspaces (HBM); the caller owns all
+ *     I/O buffers.  Pointers documented "device" are HIP device pointers.
+ *   - Calls are asynchronous on the caller's stream (hipStream_t passed as
+ *     void*; NULL = legacy default stream).  Nothing synchronises unless the
+ *     function says so.
+ *   - One engine per GPU per process; a handle is not re-entrant across host
+ *     threads.
+ */
+#ifndef ALERT_ENGINE_H
+#define ALERT_ENGINE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AE_OK 0
+#define AE_EINVAL (-22)  /* bad argument / shape */
+#define AE_ENOMEM (-12)  /* device allocation failed */
+#define AE_EDEVICE (-5)  /* HIP runtime error */
+#define AE_ENOENT (-2)   /* weight tensor missing */
+
+/* Task head on top of the CLS vector (reference model.py of each task). */
+#define AE_HEAD_SIGMOID1 0 /* Devign: RobertaClassificationHead(num_labels=1) -> sigmoid   */
+#define AE_HEAD_SOFTMAXN 1 /* Authorship: dense->tanh->out_proj(num_labels) -> softmax      */
+#define AE_HEAD_PAIR2 2    /* Clone: cat(CLS_a, CLS_b) 1536->768->tanh->2 -> softmax        */
+#define AE_HEAD_NONE 3     /* encoder only (MLM / cosine paths)                             */
+
+#define AE_PREC_FP32 0 /* exact-f32 MFMA (v_mfma_f32_32x32x2_f32) — parity mode      */
+#define AE_PREC_BF16 1 /* bf16 MFMA, f32 accumulate and f32 residual stream         */
+
+typedef struct ae_config {
+  int32_t layers;      /* 12 */
+  int32_t hidden;      /* 768 (kernels are specialised for 768) */
+  int32_t heads;       /* 12  (head dim 64) */
+  int32_t ffn;         /* 3072 */
+  int32_t vocab;       /* 50265 */
+  int32_t max_pos;     /* 514 */
+  int32_t type_vocab;  /* 1 */
+  int32_t num_labels;  /* 1 (Devign), 2 (clone), 66 (authorship) */
+  int32_t head_kind;   /* AE_HEAD_* */
+  int32_t precision;   /* AE_PREC_* */
+  int32_t pad_id;      /* 1 */
+  int32_t with_mlm;    /* 1: also upload the lm_head (MLM paths) */
+  float ln_eps;        /* 1e-5 */
+} ae_config;
+
+/* One named host tensor (fp32, row-major, HF state_dict naming). */
+typedef struct ae_weight_view {
+  const char *name;
+  const float *data; /* host pointer */
+  int64_t numel;
+} ae_weight_view;
+
+typedef struct ae_engine ae_engine;
+
+int ae_create(const ae_config *cfg, const ae_weight_view *weights, int32_t n_weights,
+              int32_t device, ae_engine **out);
+int ae_destroy(ae_engine *eng);
+
+/* Score n sequences of row length L.
+ *   ids       device int32 [n, L]  token ids, pad = cfg.pad_id anywhere in the row
+ *   lens      HOST  int32 [n]      count of non-pad ids of each row (the engine skips
+ *                                  pad rows entirely: they never influence the CLS row)
+ *   pos       device int32 [n, L] or NULL  explicit position ids (GraphCodeBERT); NULL =
+ *                                  RoBERTa rule cumsum(ids!=pad)*(ids!=pad)+pad
+ *   mask_bits device uint32 [n, L, ceil(L/32)] or NULL  explicit attention mask (GraphCodeBERT
+ *                                  data-flow mask, bit j of row i = query i may attend key j);
+ *                                  NULL = key-padding mask ids!=pad
+ *   probs_out device float [n_out, C]  n_out = n (n/2 for AE_HEAD_PAIR2), C = max(num_labels,1)
+ *                                  sigmoid head writes p (C=1); softmax heads write the row.
+ */
+int ae_score(ae_engine *eng, const int32_t *ids, const int32_t *lens, const int32_t *pos,
+             const uint32_t *mask_bits, int32_t n, int32_t L, float *probs_out, void *stream);
+
+/* Encoder hidden states of n sequences: hidden_out device float [n, L, hidden]
+ * (rows of pad positions are left untouched). */
+int ae_encode(ae_engine *eng, const int32_t *ids, const int32_t *lens, int32_t n, int32_t L,
+              float *hidden_out, void *stream);
+
+/* Masked-LM logits + top-k over the vocabulary for ONE sequence (no pad):
+ *   scores_out device float [L, k], ids_out device int32 [L, k] (descending, ties by lower id). */
+int ae_mlm_topk(ae_engine *eng, const int32_t *ids, int32_t L, int32_t k, float *scores_out,
+                int32_t *ids_out, void *stream);
+
+/* Mutant population builder on token ids.
+ *   word_tok   device int32 [n_word_tok]     concatenated token ids of every distinct word
+ *   word_off   device int32 [n_words+1]      offsets into word_tok
+ *   mut_words  device int32 [sum n_words_m]  word-id sequence of each mutant
+ *   mut_off    device int32 [n_mut+1]        offsets into mut_words
+ *   ids_out    device int32 [n_mut, L]       [cls] + first L-2 tokens + [sep] + pad
+ *   lens_out   device int32 [n_mut]          non-pad length of each row
+ */
+int ae_splice(const int32_t *word_tok, const int32_t *word_off, const int32_t *mut_words,
+              const int32_t *mut_off, int32_t n_mut, int32_t L, int32_t cls_id, int32_t sep_id,
+              int32_t pad_id, int32_t *ids_out, int32_t *lens_out, void *stream);
+
+/* Row-wise top-k of a [rows, cols] float matrix (device), descending, ties by lower index. */
+int ae_topk(const float *x, int32_t rows, int32_t cols, int32_t k, float *vals_out,
+            int32_t *idx_out, void *stream);
+
+/* sims_out[i] = (1/span_len) * sum_{t<span_len} cos(ref[t], cand[i, t]) with eps clamp
+ *   ref  device float [span_len, hidden], cand device float [n, span_len, hidden]. */
+int ae_cosine_rank(const float *ref, const float *cand, int32_t n, int32_t span_len, int32_t hidden,
+                   float eps, float *sims_out, void *stream);
+
+/* Profiling of the dominant kernel: when enabled, the engine brackets every launch of kernel
+ * class `kind` with HIP events on the launch stream.  ae_kernel_time synchronises and returns the
+ * summed milliseconds, launch count and algorithmic FLOP of those launches, then resets. */
+#define AE_KIND_GEMM_FFN1 0
+#define AE_KIND_GEMM_ANY 1
+#define AE_KIND_ATTENTION 2
+int ae_set_profiling(ae_engine *eng, int32_t kind, int32_t enabled);
+int ae_kernel_time(ae_engine *eng, double *ms_total, int64_t *launches, double *flop_total);
+
+const char *ae_last_error(void);
+const char *ae_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ALERT_ENGINE_H */
