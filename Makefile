@@ -7,13 +7,23 @@ SRCS := $(CSRC)/engine.hip $(CSRC)/gemm_f32.hip $(CSRC)/attention_f32.hip $(CSRC
 HDRS := $(CSRC)/common.h include/alert_engine.h
 HIPFLAGS := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Iinclude -Wall -Wno-unused-result
 
-all: $(LIB)
+HOSTLIB := $(PKG)/lib/libalert_host.so
+HOSTSRCS := $(CSRC)/host/bpe.cpp $(CSRC)/host/lexer.cpp $(CSRC)/host/mutate.cpp $(CSRC)/host/capi.cpp
+HOSTHDRS := $(CSRC)/host/host.h $(CSRC)/host/unicode_tables.h include/alert_host.h
+CXX ?= g++
+HOSTFLAGS := -O2 -std=c++17 -fPIC -shared -Wall -Wextra -Wno-unused-parameter -Iinclude
+
+all: $(LIB) $(HOSTLIB)
+
+$(HOSTLIB): $(HOSTSRCS) $(HOSTHDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(HOSTFLAGS) -o $@ $(HOSTSRCS)
 
 $(LIB): $(SRCS) $(HDRS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -o $@ $(SRCS)
 
 clean:
-	rm -f $(LIB)
+	rm -f $(LIB) $(HOSTLIB)
 
 .PHONY: all clean

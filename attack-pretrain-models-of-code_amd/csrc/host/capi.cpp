@@ -1,0 +1,225 @@
+// capi.cpp — extern "C" surface of libalert_host.so (include/alert_host.h).
+#include <cstring>
+#include <memory>
+#include <string>
+#include <unordered_map>
+
+#include "../../../include/alert_host.h"
+#include "host.h"
+
+struct ah_tokenizer {
+  ah::Tokenizer t;
+};
+
+struct ah_example {
+  ah::Example ex;
+  // word table for the device splice: (word, first) -> id, token runs
+  std::unordered_map<std::string, int32_t> word_id[2];
+  std::vector<int32_t> word_tok;
+  std::vector<int32_t> word_off{0};
+};
+
+namespace {
+thread_local std::string g_err;
+int32_t fail(const std::string& m) {
+  g_err = m;
+  return -1;
+}
+
+// ' '.join(code.split()) -> tokenize -> [:L-2] -> [CLS] .. [SEP] -> pad (attacker.py:38-45)
+void featurize_words(ah::Tokenizer& t, const std::vector<std::string>& words, int32_t L,
+                     int32_t* ids, int32_t* len) {
+  const int32_t cap = L - 2;
+  int32_t n = 0;
+  ids[0] = t.cls_id;
+  for (size_t w = 0; w < words.size() && n < cap; ++w) {
+    const std::vector<int32_t>& run = t.word_ids(words[w], w == 0);
+    for (int32_t id : run) {
+      if (n >= cap) break;
+      ids[1 + n++] = id;
+    }
+  }
+  ids[1 + n] = t.sep_id;
+  for (int32_t k = n + 2; k < L; ++k) ids[k] = t.pad_id;
+  *len = n + 2;
+}
+
+bool build_mutant(ah_example* e, int32_t mode, int32_t b, int32_t end, const char* const* tgts,
+                  const char* const* subs, std::string& out) {
+  if (mode == AH_MODE_SINGLE) {
+    if (end - b != 1) return false;
+    out = ah::get_example(e->ex, tgts[b], subs[b]);
+    return true;
+  }
+  std::vector<std::string> tv, sv;
+  for (int32_t k = b; k < end; ++k) {
+    tv.emplace_back(tgts[k]);
+    sv.emplace_back(subs[k]);
+  }
+  out = ah::get_example_batch(e->ex, tv, sv);
+  return true;
+}
+}  // namespace
+
+extern "C" {
+
+const char* ah_last_error(void) { return g_err.c_str(); }
+
+ah_tokenizer* ah_tokenizer_load(const char* vocab_json, const char* merges_txt) {
+  auto* t = new ah_tokenizer();
+  std::string err;
+  if (!t->t.load(vocab_json, merges_txt, &err)) {
+    g_err = err;
+    delete t;
+    return nullptr;
+  }
+  return t;
+}
+
+void ah_tokenizer_free(ah_tokenizer* t) { delete t; }
+
+int32_t ah_tokenizer_special(ah_tokenizer* t, int32_t which) {
+  switch (which) {
+    case 0: return t->t.cls_id;
+    case 1: return t->t.pad_id;
+    case 2: return t->t.sep_id;
+    case 3: return t->t.unk_id;
+    case 4: return t->t.mask_id;
+  }
+  return fail("bad special index");
+}
+
+int32_t ah_tokenize(ah_tokenizer* t, const char* text, int32_t* out, int32_t cap) {
+  if (!t || !text) return fail("null argument");
+  std::vector<int32_t> ids;
+  t->t.encode(text, ids);
+  for (int32_t k = 0; k < (int32_t)ids.size() && k < cap; ++k) out[k] = ids[k];
+  return (int32_t)ids.size();
+}
+
+int32_t ah_decode(ah_tokenizer* t, const int32_t* ids, int32_t n, char* out, int32_t cap) {
+  if (!t || (!ids && n)) return fail("null argument");
+  const std::string s = t->t.decode(ids, n);
+  if (out && cap > 0) {
+    const int32_t m = std::min<int32_t>(cap - 1, (int32_t)s.size());
+    std::memcpy(out, s.data(), m);
+    out[m] = 0;
+  }
+  return (int32_t)s.size() + 1;
+}
+
+int32_t ah_featurize_batch(ah_tokenizer* t, int32_t n, const char* const* codes, int32_t L,
+                           int32_t* ids_out, int32_t* lens_out) {
+  if (!t || !codes || !ids_out || !lens_out || L < 2) return fail("bad argument");
+  for (int32_t i = 0; i < n; ++i)
+    featurize_words(t->t, ah::py_split(codes[i]), L, ids_out + (size_t)i * L, lens_out + i);
+  return n;
+}
+
+ah_example* ah_example_new(const char* code, int32_t lang) {
+  if (!code || lang < 0 || lang > 2) {
+    fail("bad argument");
+    return nullptr;
+  }
+  auto* e = new ah_example();
+  ah::example_init(e->ex, code, (ah::Lang)lang);
+  return e;
+}
+
+void ah_example_free(ah_example* e) { delete e; }
+
+int32_t ah_example_num_leaves(ah_example* e, int32_t which) {
+  return (int32_t)(which ? e->ex.id_leaves : e->ex.leaves).size();
+}
+
+int32_t ah_example_leaves(ah_example* e, int32_t which, char* buf, int32_t cap) {
+  const std::vector<ah::Leaf>& lv = which ? e->ex.id_leaves : e->ex.leaves;
+  size_t need = 0;
+  for (auto& lf : lv) need += lf.text.size() + 1;
+  if (buf && (size_t)cap >= need) {
+    size_t p = 0;
+    for (auto& lf : lv) {
+      std::memcpy(buf + p, lf.text.data(), lf.text.size());
+      p += lf.text.size();
+      buf[p++] = 0;
+    }
+  }
+  return (int32_t)need;
+}
+
+int32_t ah_example_mutant_text(ah_example* e, int32_t mode, int32_t n_pairs,
+                               const char* const* tgts, const char* const* subs, char* out,
+                               int32_t cap) {
+  if (!e) return fail("null example");
+  std::string s;
+  if (!build_mutant(e, mode, 0, n_pairs, tgts, subs, s)) return fail("single mode needs 1 pair");
+  if (out && cap > 0) {
+    const int32_t m = std::min<int32_t>(cap - 1, (int32_t)s.size());
+    std::memcpy(out, s.data(), m);
+    out[m] = 0;
+  }
+  return (int32_t)s.size() + 1;
+}
+
+int32_t ah_example_mutants(ah_example* e, ah_tokenizer* t, int32_t mode, int32_t n_mut,
+                           const int32_t* pair_off, const char* const* tgts,
+                           const char* const* subs, int32_t L, int32_t* ids_out,
+                           int32_t* lens_out) {
+  if (!e || !t || !pair_off || !ids_out || !lens_out || L < 2) return fail("bad argument");
+  std::string code;
+  for (int32_t m = 0; m < n_mut; ++m) {
+    if (!build_mutant(e, mode, pair_off[m], pair_off[m + 1], tgts, subs, code))
+      return fail("single mode needs 1 pair per mutant");
+    featurize_words(t->t, ah::py_split(code), L, ids_out + (size_t)m * L, lens_out + m);
+  }
+  return n_mut;
+}
+
+int32_t ah_example_mutant_words(ah_example* e, ah_tokenizer* t, int32_t mode, int32_t n_mut,
+                                const int32_t* pair_off, const char* const* tgts,
+                                const char* const* subs, int32_t L, int32_t* mut_words,
+                                int32_t cap_words, int32_t* mut_off, int32_t* lens_out) {
+  if (!e || !t || !pair_off || !mut_off || !lens_out || L < 2) return fail("bad argument");
+  std::string code;
+  std::vector<int32_t> seq;
+  mut_off[0] = 0;
+  for (int32_t m = 0; m < n_mut; ++m) {
+    if (!build_mutant(e, mode, pair_off[m], pair_off[m + 1], tgts, subs, code))
+      return fail("single mode needs 1 pair per mutant");
+    const std::vector<std::string> words = ah::py_split(code);
+    int32_t ntok = 0;
+    for (size_t w = 0; w < words.size(); ++w) {
+      const int first = w == 0 ? 1 : 0;
+      auto it = e->word_id[first].find(words[w]);
+      int32_t id;
+      if (it == e->word_id[first].end()) {
+        const std::vector<int32_t>& run = t->t.word_ids(words[w], first);
+        id = (int32_t)e->word_off.size() - 1;
+        e->word_tok.insert(e->word_tok.end(), run.begin(), run.end());
+        e->word_off.push_back((int32_t)e->word_tok.size());
+        e->word_id[first].emplace(words[w], id);
+      } else {
+        id = it->second;
+      }
+      seq.push_back(id);
+      ntok += e->word_off[id + 1] - e->word_off[id];
+    }
+    mut_off[m + 1] = (int32_t)seq.size();
+    lens_out[m] = std::min(ntok, L - 2) + 2;
+  }
+  if ((int32_t)seq.size() > cap_words) return -(int32_t)seq.size();
+  if (mut_words) std::memcpy(mut_words, seq.data(), seq.size() * 4);
+  return (int32_t)seq.size();
+}
+
+int32_t ah_example_word_table(ah_example* e, int32_t* word_tok, int32_t cap_tok,
+                              int32_t* word_off, int32_t cap_off, int32_t* n_words_out) {
+  const int32_t nt = (int32_t)e->word_tok.size();
+  const int32_t nw = (int32_t)e->word_off.size() - 1;
+  *n_words_out = nw;
+  if (word_tok && cap_tok >= nt) std::memcpy(word_tok, e->word_tok.data(), nt * 4);
+  if (word_off && cap_off >= nw + 1) std::memcpy(word_off, e->word_off.data(), (nw + 1) * 4);
+  return nt;
+}
+
+}  // extern "C"

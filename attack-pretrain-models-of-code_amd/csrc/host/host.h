@@ -1,0 +1,88 @@
+// host.h — internal C++ API of the host featurisation library (libalert_host.so).
+//
+// Replaces, on the host side of the victim query boundary:
+//   RobertaTokenizer.tokenize / convert_tokens_to_ids   (byte-level BPE; reference call sites
+//       CodeXGLUE/Defect-detection/code/attacker.py:38-45, utils.py:174-189)
+//   tree-sitter leaf extraction                          (python_parser/parser_folder/utils.py:89-129)
+//   get_example / get_example_batch                       (python_parser/run_parser.py:218-266)
+//   convert_code_to_features                              (attacker.py:38-45)
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace ah {
+
+// ------------------------------------------------------------------------------------ utf-8
+// Decode one code point at s[i] (advances i).  Invalid bytes decode as themselves (U+FFFD-free).
+uint32_t utf8_next(const std::string& s, size_t& i);
+void utf8_append(std::string& out, uint32_t cp);
+std::vector<uint32_t> utf8_decode(const std::string& s);
+std::string utf8_encode(const std::vector<uint32_t>& cps, size_t b, size_t e);
+bool py_isspace(uint32_t cp);  // Python str.split() whitespace
+
+// ------------------------------------------------------------------------------------ BPE
+class Tokenizer {
+ public:
+  bool load(const std::string& vocab_json, const std::string& merges_txt, std::string* err);
+  // tokenize(text) ids, RobertaTokenizer semantics (special tokens split first).
+  void encode(const std::string& text, std::vector<int32_t>& out);
+  // ids of one whitespace-delimited word, with (" " + word) when !first; cached.
+  const std::vector<int32_t>& word_ids(const std::string& word, bool first);
+  int32_t cls_id = 0, sep_id = 2, pad_id = 1, unk_id = 3, mask_id = 50264;
+  const std::string& id_to_token(int32_t id) const { return inv_[id]; }
+  size_t vocab_size() const { return inv_.size(); }
+  // decode byte-level tokens to text (tokenizer._decode / convert_tokens_to_string)
+  std::string decode(const int32_t* ids, int n) const;
+
+ private:
+  void encode_plain(const std::string& seg, std::vector<int32_t>& out);
+  void bpe(const std::string& pretok, std::vector<int32_t>& out);
+  std::unordered_map<std::string, int32_t> vocab_;
+  std::vector<std::string> inv_;
+  std::unordered_map<std::string, int32_t> ranks_;  // "a b" -> rank
+  std::vector<std::string> byte_enc_;               // byte -> utf-8 of its unicode stand-in
+  std::unordered_map<uint32_t, uint8_t> byte_dec_;  // stand-in code point -> byte
+  std::unordered_map<std::string, std::vector<int32_t>> bpe_cache_;
+  std::unordered_map<std::string, std::vector<int32_t>> word_cache_[2];
+  std::vector<std::string> specials_;
+};
+
+// ------------------------------------------------------------------------------------ lexer
+enum Lang { LANG_C = 0, LANG_JAVA = 1, LANG_PYTHON = 2 };
+
+struct Leaf {
+  int sl, sc, el, ec;  // start/end line, byte column (tree-sitter Point semantics)
+  std::string text;    // index_to_code_token(start, end, lines)
+};
+
+// Leaves of `code` (already '\\n'-replaced by the caller when the reference does so).
+std::vector<Leaf> lex(const std::string& code, Lang lang);
+
+// ------------------------------------------------------------------------------------ mutants
+std::vector<std::string> split_lines(const std::string& code);
+std::string join_lines(const std::vector<std::string>& lines);
+
+struct Example {
+  Lang lang;
+  std::string code;                // as given (func text)
+  std::string rcode;               // code.replace("\\n", "\n")
+  std::vector<Leaf> leaves;        // lex(rcode): the leaves get_example(_batch) edits
+  std::vector<Leaf> id_leaves;     // lex(remove_comments(rcode)): get_identifiers code tokens
+  std::vector<std::vector<uint32_t>> lines_cp;  // rcode.split('\n') as code points
+};
+
+void example_init(Example& ex, const std::string& code, Lang lang);
+std::string remove_comments(const std::string& src);
+// get_example (single variable, run_parser.py:218-239)
+std::string get_example(const Example& ex, const std::string& tgt, const std::string& sub);
+// get_example_batch (chromosome in dict order, run_parser.py:242-266)
+std::string get_example_batch(const Example& ex, const std::vector<std::string>& tgts,
+                              const std::vector<std::string>& subs);
+
+// ' '.join(code.split()) words
+std::vector<std::string> py_split(const std::string& s);
+
+}  // namespace ah

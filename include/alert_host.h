@@ -1,0 +1,83 @@
+/*
+ * alert_host.h — C-ABI of the host featurisation library (libalert_host.so).
+ *
+ * The host half of the victim query path: tokenisation, tree-sitter-free leaf extraction and the
+ * text-level identifier substitution that turns a chromosome into model input ids.
+ * Reference interfaces replaced (paths relative to the reference snapshot):
+ *   ah_tokenize / ah_decode   <- RobertaTokenizer.tokenize + convert_tokens_to_ids / _decode
+ *                                (utils.py:174-189 _tokenize, utils.py:269 _decode)
+ *   ah_featurize(_batch)      <- convert_code_to_features
+ *                                (CodeXGLUE/Defect-detection/code/attacker.py:38-45,
+ *                                 run.py:79-86 convert_examples_to_features)
+ *   ah_example_leaves         <- get_identifiers(code, lang)[1] code tokens
+ *                                (python_parser/run_parser.py:185-216,272-281)
+ *   ah_example_mutant_text    <- get_example / get_example_batch (run_parser.py:218-266)
+ *   ah_example_mutants        <- convert_code_to_features(map_chromesome(...)) for a population
+ *   ah_example_mutant_words   <- the same, as word-id sequences for the device splice (ae_splice)
+ * All strings are UTF-8, NUL-terminated.  Functions return >= 0 on success (a count) or a
+ * negative code; ah_last_error() describes the last failure of the calling thread.
+ */
+#ifndef ALERT_HOST_H
+#define ALERT_HOST_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AH_LANG_C 0
+#define AH_LANG_JAVA 1
+#define AH_LANG_PYTHON 2
+
+#define AH_MODE_BATCH 0  /* get_example_batch(code, chromosome) */
+#define AH_MODE_SINGLE 1 /* get_example(code, tgt, sub): exactly one pair per mutant */
+
+typedef struct ah_tokenizer ah_tokenizer;
+typedef struct ah_example ah_example;
+
+ah_tokenizer *ah_tokenizer_load(const char *vocab_json, const char *merges_txt);
+void ah_tokenizer_free(ah_tokenizer *tok);
+int32_t ah_tokenizer_special(ah_tokenizer *tok, int32_t which); /* 0 cls 1 pad 2 sep 3 unk 4 mask */
+/* ids of tokenizer.tokenize(text); returns the count (writes at most cap) */
+int32_t ah_tokenize(ah_tokenizer *tok, const char *text, int32_t *out, int32_t cap);
+/* tokenizer decode of ids (byte-level, errors='replace'); returns bytes needed incl. NUL */
+int32_t ah_decode(ah_tokenizer *tok, const int32_t *ids, int32_t n, char *out, int32_t cap);
+/* convert_code_to_features of n texts: ids_out [n, L], lens_out [n] (non-pad length) */
+int32_t ah_featurize_batch(ah_tokenizer *tok, int32_t n, const char *const *codes, int32_t L,
+                           int32_t *ids_out, int32_t *lens_out);
+
+ah_example *ah_example_new(const char *code, int32_t lang);
+void ah_example_free(ah_example *ex);
+/* which = 0: leaves of the code as get_example parses it (code.replace("\\n", "\n"));
+ * which = 1: get_identifiers' code tokens (comments removed first, run_parser.py:190-216). */
+int32_t ah_example_num_leaves(ah_example *ex, int32_t which);
+/* leaves' texts separated by '\0'; returns bytes needed */
+int32_t ah_example_leaves(ah_example *ex, int32_t which, char *buf, int32_t cap);
+/* mutant source text; returns bytes needed incl. NUL */
+int32_t ah_example_mutant_text(ah_example *ex, int32_t mode, int32_t n_pairs,
+                               const char *const *tgts, const char *const *subs, char *out,
+                               int32_t cap);
+/* population -> ids.  Mutant m uses pairs [pair_off[m], pair_off[m+1]) of tgts/subs. */
+int32_t ah_example_mutants(ah_example *ex, ah_tokenizer *tok, int32_t mode, int32_t n_mut,
+                           const int32_t *pair_off, const char *const *tgts,
+                           const char *const *subs, int32_t L, int32_t *ids_out,
+                           int32_t *lens_out);
+/* population -> word-id sequences (device splice input).  Appends to the example's word table;
+ * mut_words [cap_words], mut_off [n_mut+1], lens_out [n_mut].  Returns total words written or
+ * -(needed) if cap_words is too small. */
+int32_t ah_example_mutant_words(ah_example *ex, ah_tokenizer *tok, int32_t mode, int32_t n_mut,
+                                const int32_t *pair_off, const char *const *tgts,
+                                const char *const *subs, int32_t L, int32_t *mut_words,
+                                int32_t cap_words, int32_t *mut_off, int32_t *lens_out);
+/* the example's word table: returns number of table tokens (word_tok needs that many),
+ * *n_words_out = number of words (word_off needs n_words+1). */
+int32_t ah_example_word_table(ah_example *ex, int32_t *word_tok, int32_t cap_tok,
+                              int32_t *word_off, int32_t cap_off, int32_t *n_words_out);
+
+const char *ah_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ALERT_HOST_H */

@@ -1,0 +1,188 @@
+"""CPU: host featurisation library (C++) against the Python oracle (oracle/featurize_ref.py) and
+the installed transformers RobertaTokenizer, on the reference's own attack fixtures
+(data/devign/test_subs_*.jsonl, copied from CodeXGLUE/Defect-detection/preprocess/dataset)."""
+import json
+import random
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from oracle import featurize_ref as ref
+
+DEVIGN = sorted((ROOT / "data" / "devign").glob("test_subs_*.jsonl"))
+
+
+def load(path, limit=None):
+    out = []
+    with open(path) as f:
+        for i, line in enumerate(f):
+            if limit is not None and i >= limit:
+                break
+            out.append(json.loads(line))
+    return out
+
+
+@pytest.fixture(scope="module")
+def tok():
+    from apmc_amd.host import Tokenizer
+    return Tokenizer()
+
+
+@pytest.fixture(scope="module")
+def devign_small():
+    return load(DEVIGN[0], 120)
+
+
+def test_tokenizer_matches_transformers_on_all_fixture_functions(tok):
+    rt = ref.tokenizer()
+    n = 0
+    for path in DEVIGN:
+        for js in load(path):
+            text = " ".join(js["func"].split())
+            assert tok.encode_ids(text) == rt.convert_tokens_to_ids(rt.tokenize(text))
+            n += 1
+    assert n == 2732
+
+
+@pytest.mark.parametrize("s", ["a <unk> b", "x<mask>y <s></s>", "  foo  ", "\t\tx\n\n  y",
+                               "it's 'll 're 've", "说啊 ab12 3.5e-3", "\xa0x\u2003y", "", "<pad>",
+                               "'z' \"s\\n\" /* c */ // d"])
+def test_tokenizer_edge_cases(tok, s):
+    rt = ref.tokenizer()
+    assert tok.encode_ids(s) == rt.convert_tokens_to_ids(rt.tokenize(s))
+
+
+def test_decode_roundtrip(tok):
+    for s in ["int x = 1; // 说", " foo_bar", "\tq"]:
+        assert tok.decode(tok.encode_ids(s)) == s
+
+
+def test_leaves_match_oracle(devign_small):
+    from apmc_amd.host import Example
+    for js in devign_small:
+        code = js["func"].replace("\\n", "\n")
+        ex = Example(js["func"])
+        assert ex.leaves() == ref.code_tokens(code, "c")
+        assert ex.leaves(identifiers=True) == ref.identifier_code_tokens(js["func"], "c")
+
+
+def test_remove_comments_matches_regex():
+    from apmc_amd.host import Example
+    cases = ["a = 1; // c\nb = '/*'; /* x\n y */ c = \"//\";",
+             "don't /* it's */ x = 'a';\n  \n\t\ny", "/* open", "'\\'' // q"]
+    for c in cases:
+        assert Example(c).leaves(identifiers=True) == ref.identifier_code_tokens(c), c
+
+
+def test_leaf_edge_cases():
+    from apmc_amd.host import Example
+    cases = [
+        'int a = -1; b = a-1; c = x[2]-3; s = "a\\tb\\x41\\101"; ch = \'\\n\';',
+        "#include <stdio.h>\n#define MAX(a, b) ((a) > (b) ? (a) : (b)) /* c */\nint x;",
+        "#if defined(FOO) && BAR > 2\n  y++;\n#endif\n#pragma once\n  # undef Z",
+        'x = L"wide" u8"u" U\'c\'; y = 0x1Fu + 1.5e-3f + .5 + 1e+10;',
+        "p->q.r ... a >>= b <<= c; d = e ? f : g;",
+        'line "unterminated\nnext = 1; /* multi\nline */ z;',
+        'a = "说"; b = c; // 说\n d = e;',
+        "q = 'x'; r = '\\'';",
+    ]
+    for c in cases:
+        assert Example(c).leaves() == ref.code_tokens(c.replace("\\n", "\n"), "c"), c
+
+
+def _random_chromosomes(js, rng, n):
+    subs = js["substitutes"]
+    keys = list(subs.keys())
+    out = []
+    for _ in range(n):
+        chrom = {}
+        for k in keys:
+            if subs[k] and rng.random() < 0.6:
+                chrom[k] = rng.choice(subs[k])
+            else:
+                chrom[k] = k
+        out.append(chrom)
+    return out
+
+
+def test_get_example_batch_text_and_ids_match_oracle(devign_small, tok):
+    from apmc_amd.host import Example
+    rng = random.Random(0)
+    for js in devign_small[:60]:
+        if not js["substitutes"]:
+            continue
+        ex = Example(js["func"])
+        chroms = _random_chromosomes(js, rng, 4)
+        pops = [list(c.items()) for c in chroms]
+        ids, lens = ex.mutant_ids(tok, pops, 512)
+        for c, pairs, row, ln in zip(chroms, pops, ids, lens):
+            text = ref.get_example_batch(js["func"], c, "c")
+            assert ex.mutant_text(pairs) == text
+            exp = ref.convert_code_to_features(text, 512)
+            assert row.tolist() == exp
+            assert ln == int((np.asarray(exp) != 1).sum())
+
+
+def test_get_example_single_matches_oracle(devign_small, tok):
+    from apmc_amd.host import MODE_SINGLE, Example
+    for js in devign_small[:60]:
+        ex = Example(js["func"])
+        pops = []
+        for var, subs in js["substitutes"].items():
+            for s in subs[:5]:
+                pops.append([(var, s)])
+        if not pops:
+            continue
+        ids, lens = ex.mutant_ids(tok, pops, 512, mode=MODE_SINGLE)
+        for pairs, row in zip(pops, ids):
+            text = ref.get_example(js["func"], pairs[0][0], pairs[0][1], "c")
+            assert ex.mutant_text(pairs, mode=MODE_SINGLE) == text
+            assert row.tolist() == ref.convert_code_to_features(text, 512)
+
+
+def test_offset_quirk_reproduced():
+    """get_example_batch applies same-line edits in key order with a running diff."""
+    from apmc_amd.host import Example
+    code = "b = a;\nint c = b + a;"
+    chrom = {"a": "xyz", "b": "b"}
+    exp = ref.get_example_batch(code, chrom)
+    assert exp != "b = xyz;\nint c = b + xyz;"  # the quirk garbles the line
+    assert Example(code).mutant_text(list(chrom.items())) == exp
+
+
+def test_mutant_words_feed_the_same_ids(devign_small, tok):
+    from apmc_amd.host import Example
+    rng = random.Random(1)
+    for js in devign_small[:20]:
+        if not js["substitutes"]:
+            continue
+        ex = Example(js["func"])
+        pops = [list(c.items()) for c in _random_chromosomes(js, rng, 5)]
+        ids, lens = ex.mutant_ids(tok, pops, 512)
+        word_tok, word_off, mut_words, mut_off, lens2 = ex.mutant_words(tok, pops, 512)
+        assert (lens == lens2).all()
+        for m in range(len(pops)):
+            ws = mut_words[mut_off[m]:mut_off[m + 1]]
+            toks = [t for w in ws for t in word_tok[word_off[w]:word_off[w + 1]]][:510]
+            assert [0] + toks + [2] + [1] * (510 - len(toks)) == ids[m].tolist()
+
+
+@pytest.mark.slow
+def test_fixture_keys_are_lexer_identifiers():
+    """Known-answer check: every substitute key of every Devign fixture example is an
+    identifier leaf of our lexer (the reference took the keys from tree-sitter DFG identifiers)."""
+    from apmc_amd.host import Example
+    missing, total = [], 0
+    for path in DEVIGN:
+        for js in load(path):
+            leaves = set(Example(js["func"]).leaves(identifiers=True))
+            for k in js["substitutes"]:
+                total += 1
+                if k not in leaves:
+                    missing.append(k)
+    assert total == 17427
+    # the only misses: 'm' / 'memory' GNU-asm constraint and clobber strings
+    # (test_subs_800_1200 #151, test_subs_1200_1600 #161/#341), which tree-sitter's error
+    # recovery surfaced as identifiers; parity with tree-sitter is unpinned there
+    assert sorted(missing) == ["memory", "memory", "m", "m"][::-1] or sorted(missing) == sorted(["m", "m", "memory", "memory"]), missing
