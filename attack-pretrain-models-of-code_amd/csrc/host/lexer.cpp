@@ -8,7 +8,8 @@
 // the token rules of the tree-sitter-c / -java / -python grammars of the reference's era.
 //
 // C (tree-sitter-c 0.20.x):
-//   * whitespace and backslash-newline are extras; // and /* */ comments are dropped;
+//   * whitespace and backslash-newline are extras; // and /* */ comments are dropped (an
+//     unterminated /* is not a comment: its characters lex as operators / identifiers);
 //   * identifiers [A-Za-z_][A-Za-z0-9_]*; numbers (optional sign when an operand is expected,
 //     0x/0b, digits, '.', exponent sign after e/E/p/P, suffix letters);
 //   * string literal: opening quote (with L/u/U/u8 prefix) and closing quote are leaves, escape
@@ -98,7 +99,7 @@ class Lexer {
         skip_line_comment();
         continue;
       }
-      if (lang_ != LANG_PYTHON && ch == '/' && c_.at(1) == '*') {
+      if (lang_ != LANG_PYTHON && ch == '/' && c_.at(1) == '*' && block_comment_closes()) {
         skip_block_comment();
         continue;
       }
@@ -147,6 +148,9 @@ class Lexer {
       else c_.adv();
     }
   }
+  // an unterminated /* is not a comment token: '/' and '*' lex as operators (tree-sitter-c's
+  // comment regex needs the closing */)
+  bool block_comment_closes() const { return c_.s.find("*/", c_.i + 2) != std::string::npos; }
   void skip_block_comment() {
     c_.adv(2);
     while (!c_.eof() && !(c_.at() == '*' && c_.at(1) == '/')) c_.adv();
@@ -455,7 +459,7 @@ class Lexer {
       if (ch == '\\' && c_.at(1) == '\n') { c_.adv(2); continue; }
       if (ch == '\\' && c_.at(1) == '\r' && c_.at(2) == '\n') { c_.adv(3); continue; }
       if (ch == '/' && c_.at(1) == '/') { skip_line_comment(); continue; }
-      if (ch == '/' && c_.at(1) == '*') { skip_block_comment(); continue; }
+      if (ch == '/' && c_.at(1) == '*' && block_comment_closes()) { skip_block_comment(); continue; }
       token();
     }
   }

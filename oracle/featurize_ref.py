@@ -102,6 +102,9 @@ class _Lex:
             k = self.nl_cont()
             self.adv(k if k else 1)
 
+    def closes(self):
+        return self.b.find(b"*/", self.i + 2) >= 0
+
     def skip_block_comment(self):
         self.adv(2)
         while not self.eof() and not (self.at() == "*" and self.at(1) == "/"):
@@ -125,7 +128,7 @@ class _Lex:
             if self.lang != "python" and ch == "/" and self.at(1) == "/":
                 self.skip_line_comment()
                 continue
-            if self.lang != "python" and ch == "/" and self.at(1) == "*":
+            if self.lang != "python" and ch == "/" and self.at(1) == "*" and self.closes():
                 self.skip_block_comment()
                 continue
             if self.lang == "python" and ch == "#":
@@ -395,7 +398,7 @@ class _Lex:
             if ch == "/" and self.at(1) == "/":
                 self.skip_line_comment()
                 continue
-            if ch == "/" and self.at(1) == "*":
+            if ch == "/" and self.at(1) == "*" and self.closes():
                 self.skip_block_comment()
                 continue
             self.token()
