@@ -1,0 +1,484 @@
+"""ALERT attacks over the engine: greedy (importance-ordered), GA, and the MHM-NS baseline.
+
+Same classes, signatures, return values and Python-`random` call order as the reference
+(CodeXGLUE/Defect-detection/code/attacker.py): Attacker.greedy_attack :277-453,
+Attacker.ga_attack :96-272, get_importance_score :48-83, compute_fitness :25-35,
+convert_code_to_features :38-45, MHM_Attacker.mcmc / mcmc_random :466-608,
+__replaceUID / __replaceUID_random :610-738.  Every victim query still goes through
+Model.get_results semantics (query counter, probs/preds format); mutant text -> ids runs in the
+C++ host library and the population's ids are built on the GPU by ae_splice.
+"""
+from __future__ import annotations
+
+import copy
+import random
+
+import numpy as np
+
+from .host import MODE_BATCH, MODE_SINGLE, Example
+from .utils import (CodeDataset, InputFeatures, IdsDataset, _tokenize, crossover,
+                    get_identifier_posistions_from_code, get_masked_code_by_position, isUID,
+                    map_chromesome, mutate, select_parents)
+
+
+def _label_of(example):
+    lab = example[1]
+    return int(lab.item()) if hasattr(lab, "item") else int(lab)
+
+
+def convert_code_to_features(code, tokenizer, label, args):
+    """attacker.py:38-45 (host tokenizer; ' '.join(code.split()) -> [:block-2] -> CLS/SEP/pad)."""
+    ids, _ = tokenizer.featurize([code], args.block_size)
+    row = ids[0].tolist()
+    n = int((ids[0] != tokenizer.pad_token_id).sum())
+    return InputFeatures(None, row, 0, label)
+
+
+def get_identifiers(code, lang):
+    """run_parser.py:272-281 — returns (identifiers, code_tokens).  Only the code tokens feed the
+    attacks; the DFG identifier list is produced by apmc_amd.dataflow when available."""
+    ex = Example(code, lang)
+    toks = ex.leaves(identifiers=True)
+    try:
+        from .dataflow import dfg_identifiers
+
+        idents = [[i] for i in dfg_identifiers(code, lang)]
+    except Exception:
+        idents = None
+    return idents, toks
+
+
+class _Scorer:
+    """Victim queries for one attacked example: ids built from chromosomes (host) and scored."""
+
+    def __init__(self, attacker, code, lang="c"):
+        self.a = attacker
+        self.ex = Example(code, lang)
+
+    def population(self, pops, mode):
+        """pops: list of [(tgt, sub), ...] -> (probs, preds) via the device splice path."""
+        m = self.a.model_tgt
+        return m.get_results_population(self.ex, self.a.tokenizer_tgt, pops, mode,
+                                        self.a.args.block_size)
+
+    def texts(self, texts):
+        ids, lens = self.a.tokenizer_tgt.featurize(texts, self.a.args.block_size)
+        return self.a.model_tgt.get_results(IdsDataset(ids, lens), self.a.args.eval_batch_size)
+
+
+def get_importance_score(args, example, code, words_list, sub_words, variable_names, tgt_model,
+                         tokenizer, label_list, batch_size=16, max_length=512,
+                         model_type="classification"):
+    """attacker.py:48-83: 1 + #occurrences queries (original + one '<unk>' copy per occurrence)."""
+    positions = get_identifier_posistions_from_code(words_list, variable_names)
+    if len(positions) == 0:
+        return None, None, None
+    masked_token_list, replace_token_positions = get_masked_code_by_position(words_list, positions)
+    texts = [" ".join(tokens) for tokens in [words_list] + masked_token_list]
+    ids, lens = tokenizer.featurize(texts, args.block_size)
+    logits, preds = tgt_model.get_results(IdsDataset(ids, lens), args.eval_batch_size)
+    orig_probs = logits[0]
+    orig_label = preds[0]
+    orig_prob = max(orig_probs)
+    importance_score = [orig_prob - prob[orig_label] for prob in logits[1:]]
+    return importance_score, replace_token_positions, positions
+
+
+def compute_fitness(chromesome, codebert_tgt, tokenizer_tgt, orig_prob, orig_label, true_label,
+                    code, names_positions_dict, args, scorer=None):
+    """attacker.py:25-35: one query for one chromosome."""
+    if scorer is not None:
+        new_logits, preds = scorer.population([list(chromesome.items())], MODE_BATCH)
+    else:
+        temp_code = map_chromesome(chromesome, code, "c")
+        new_feature = convert_code_to_features(temp_code, tokenizer_tgt, true_label, args)
+        new_logits, preds = codebert_tgt.get_results(CodeDataset([new_feature]), args.eval_batch_size)
+    fitness_value = orig_prob - new_logits[0][orig_label]
+    return fitness_value, preds[0]
+
+
+class Attacker:
+    def __init__(self, args, model_tgt, tokenizer_tgt, model_mlm, tokenizer_mlm, use_bpe,
+                 threshold_pred_score) -> None:
+        self.args = args
+        self.model_tgt = model_tgt
+        self.tokenizer_tgt = tokenizer_tgt
+        self.model_mlm = model_mlm
+        self.tokenizer_mlm = tokenizer_mlm
+        self.use_bpe = use_bpe
+        self.threshold_pred_score = threshold_pred_score
+        self.lang = getattr(args, "lang", "c")
+
+    # ------------------------------------------------------------------------------------------
+    def ga_attack(self, example, code, substituions, initial_replace=None):
+        """Genetic attack (attacker.py:96-272); returns the reference's 12-tuple."""
+        logits, preds = self.model_tgt.get_results([example], self.args.eval_batch_size)
+        orig_prob = logits[0]
+        orig_label = preds[0]
+        current_prob = max(orig_prob)
+        true_label = _label_of(example)
+        adv_code = ""
+        temp_label = None
+
+        identifiers, code_tokens = get_identifiers(code, self.lang)
+        prog_length = len(code_tokens)
+        processed_code = " ".join(code_tokens)
+        words, sub_words, keys = _tokenize(processed_code, self.tokenizer_mlm)
+        variable_names = list(substituions.keys())
+
+        if not orig_label == true_label:
+            return code, prog_length, adv_code, true_label, orig_label, temp_label, -4, \
+                variable_names, None, None, None, None
+        if len(variable_names) == 0:
+            return code, prog_length, adv_code, true_label, orig_label, temp_label, -3, \
+                variable_names, None, None, None, None
+
+        names_positions_dict = get_identifier_posistions_from_code(words, variable_names)
+        nb_changed_var = 0
+        nb_changed_pos = 0
+        is_success = -1
+        variable_substitue_dict = {w: substituions[w] for w in names_positions_dict.keys()}
+        if len(variable_substitue_dict) == 0:
+            return code, prog_length, adv_code, true_label, orig_label, temp_label, -3, \
+                variable_names, None, None, None, None
+
+        scorer = _Scorer(self, code, self.lang)
+        fitness_values = []
+        base_chromesome = {word: word for word in variable_substitue_dict.keys()}
+        population = [base_chromesome]
+        for tgt_word in variable_substitue_dict.keys():
+            if initial_replace is None:
+                # pick the substitute with the largest probability gap (one batch per variable)
+                current_prob = max(orig_prob)
+                most_gap = 0.0
+                substitute_list = list(variable_substitue_dict[tgt_word])
+                if len(substitute_list) == 0:
+                    continue
+                logits, preds = scorer.population([[(tgt_word, s)] for s in substitute_list],
+                                                  MODE_SINGLE)
+                best = -1
+                for index, temp_prob in enumerate(logits):
+                    temp_label = preds[index]
+                    gap = current_prob - temp_prob[temp_label]
+                    if gap > most_gap:
+                        most_gap = gap
+                        best = index
+                initial_candidate = tgt_word if best == -1 else substitute_list[best]
+            else:
+                initial_candidate = initial_replace[tgt_word]
+            temp_chromesome = copy.deepcopy(base_chromesome)
+            temp_chromesome[tgt_word] = initial_candidate
+            population.append(temp_chromesome)
+            temp_fitness, temp_label = compute_fitness(temp_chromesome, self.model_tgt,
+                                                       self.tokenizer_tgt, max(orig_prob),
+                                                       orig_label, true_label, code,
+                                                       names_positions_dict, self.args, scorer)
+            fitness_values.append(temp_fitness)
+
+        cross_probability = 0.7
+        max_iter = max(5 * len(population), 10)
+        for i in range(max_iter):
+            _temp_mutants = []
+            for j in range(self.args.eval_batch_size):
+                p = random.random()
+                chromesome_1, index_1, chromesome_2, index_2 = select_parents(population)
+                if p < cross_probability:
+                    if chromesome_1 == chromesome_2:
+                        child_1 = mutate(chromesome_1, variable_substitue_dict)
+                        continue
+                    child_1, child_2 = crossover(chromesome_1, chromesome_2)
+                    if child_1 == chromesome_1 or child_1 == chromesome_2:
+                        child_1 = mutate(chromesome_1, variable_substitue_dict)
+                else:
+                    child_1 = mutate(chromesome_1, variable_substitue_dict)
+                _temp_mutants.append(child_1)
+            if len(_temp_mutants) == 0:
+                continue
+            # the dicts are read only now, after every in-place mutate of this iteration
+            mutate_logits, mutate_preds = scorer.population(
+                [list(m.items()) for m in _temp_mutants], MODE_BATCH)
+            mutate_fitness_values = []
+            for index, logits in enumerate(mutate_logits):
+                if mutate_preds[index] != orig_label:
+                    adv_code = map_chromesome(_temp_mutants[index], code, "c", scorer.ex)
+                    for old_word in _temp_mutants[index].keys():
+                        if old_word == _temp_mutants[index][old_word]:
+                            nb_changed_var += 1   # counts UNchanged names (reference quirk)
+                            nb_changed_pos += len(names_positions_dict[old_word])
+                    return code, prog_length, adv_code, true_label, orig_label, \
+                        mutate_preds[index], 1, variable_names, None, nb_changed_var, \
+                        nb_changed_pos, _temp_mutants[index]
+                mutate_fitness_values.append(max(orig_prob) - logits[orig_label])
+            for index, fitness_value in enumerate(mutate_fitness_values):
+                min_value = min(fitness_values)
+                if fitness_value > min_value:
+                    min_index = fitness_values.index(min_value)
+                    population[min_index] = _temp_mutants[index]
+                    fitness_values[min_index] = fitness_value
+
+        return code, prog_length, adv_code, true_label, orig_label, temp_label, is_success, \
+            variable_names, None, nb_changed_var, nb_changed_pos, None
+
+    # ------------------------------------------------------------------------------------------
+    def greedy_attack(self, example, code, substituions):
+        """Importance-ordered greedy attack (attacker.py:277-453); returns the 12-tuple."""
+        logits, preds = self.model_tgt.get_results([example], self.args.eval_batch_size)
+        orig_prob = logits[0]
+        orig_label = preds[0]
+        current_prob = max(orig_prob)
+        true_label = _label_of(example)
+        adv_code = ""
+        temp_label = None
+
+        identifiers, code_tokens = get_identifiers(code, self.lang)
+        prog_length = len(code_tokens)
+        processed_code = " ".join(code_tokens)
+        words, sub_words, keys = _tokenize(processed_code, self.tokenizer_mlm)
+        variable_names = list(substituions.keys())
+
+        if not orig_label == true_label:
+            return code, prog_length, adv_code, true_label, orig_label, temp_label, -4, \
+                variable_names, None, None, None, None
+        if len(variable_names) == 0:
+            return code, prog_length, adv_code, true_label, orig_label, temp_label, -3, \
+                variable_names, None, None, None, None
+
+        importance_score, replace_token_positions, names_positions_dict = get_importance_score(
+            self.args, example, processed_code, words, sub_words, variable_names, self.model_tgt,
+            self.tokenizer_tgt, [0, 1], batch_size=self.args.eval_batch_size,
+            max_length=self.args.block_size, model_type="classification")
+        if importance_score is None:
+            return code, prog_length, adv_code, true_label, orig_label, temp_label, -3, \
+                variable_names, None, None, None, None
+
+        token_pos_to_score_pos = {pos: i for i, pos in enumerate(replace_token_positions)}
+        names_to_importance_score = {}
+        for name in names_positions_dict.keys():
+            total_score = 0.0
+            for token_pos in names_positions_dict[name]:
+                total_score += importance_score[token_pos_to_score_pos[token_pos]]
+            names_to_importance_score[name] = total_score
+        sorted_list_of_names = sorted(names_to_importance_score.items(), key=lambda x: x[1],
+                                      reverse=True)
+
+        final_code = copy.deepcopy(code)
+        nb_changed_var = 0
+        nb_changed_pos = 0
+        is_success = -1
+        replaced_words = {}
+        for name_and_score in sorted_list_of_names:
+            tgt_word = name_and_score[0]
+            all_substitues = substituions[tgt_word]
+            most_gap = 0.0
+            candidate = None
+            substitute_list = list(all_substitues)
+            if len(substitute_list) == 0:
+                continue
+            # get_example(final_code, tgt, sub) per substitute, one batch
+            scorer = _Scorer(self, final_code, self.lang)
+            logits, preds = scorer.population([[(tgt_word, s)] for s in substitute_list],
+                                              MODE_SINGLE)
+            assert len(logits) == len(substitute_list)
+            for index, temp_prob in enumerate(logits):
+                temp_label = preds[index]
+                if temp_label != orig_label:
+                    is_success = 1
+                    nb_changed_var += 1
+                    nb_changed_pos += len(names_positions_dict[tgt_word])
+                    candidate = substitute_list[index]
+                    replaced_words[tgt_word] = candidate
+                    adv_code = scorer.ex.mutant_text([(tgt_word, candidate)], MODE_SINGLE)
+                    if getattr(self.args, "verbose", False):
+                        print("%s SUC! %s => %s (%.5f => %.5f)" % (
+                            ">>", tgt_word, candidate, current_prob, temp_prob[orig_label]),
+                            flush=True)
+                    return code, prog_length, adv_code, true_label, orig_label, temp_label, \
+                        is_success, variable_names, names_to_importance_score, nb_changed_var, \
+                        nb_changed_pos, replaced_words
+                gap = current_prob - temp_prob[temp_label]
+                if gap > most_gap:
+                    most_gap = gap
+                    candidate = substitute_list[index]
+            if most_gap > 0:
+                nb_changed_var += 1
+                nb_changed_pos += len(names_positions_dict[tgt_word])
+                current_prob = current_prob - most_gap
+                replaced_words[tgt_word] = candidate
+                final_code = scorer.ex.mutant_text([(tgt_word, candidate)], MODE_SINGLE)
+            else:
+                replaced_words[tgt_word] = tgt_word
+            adv_code = final_code
+
+        return code, prog_length, adv_code, true_label, orig_label, temp_label, is_success, \
+            variable_names, names_to_importance_score, nb_changed_var, nb_changed_pos, \
+            replaced_words
+
+
+class MHM_Attacker:
+    """MHM-NS baseline (attacker.py:457-738)."""
+
+    def __init__(self, args, model_tgt, model_mlm, tokenizer_mlm, _token2idx, _idx2token) -> None:
+        self.classifier = model_tgt
+        self.model_mlm = model_mlm
+        self.token2idx = _token2idx
+        self.idx2token = _idx2token
+        self.args = args
+        self.tokenizer_mlm = tokenizer_mlm
+        self.lang = getattr(args, "lang", "c")
+
+    def _run(self, tokenizer, substituions, code, _label, _n_candi, _max_iter, _prob_threshold,
+             replace, attack_type):
+        identifiers, code_tokens = get_identifiers(code, self.lang)
+        prog_length = len(code_tokens)
+        processed_code = " ".join(code_tokens)
+        words, sub_words, keys = _tokenize(processed_code, tokenizer)
+        raw_tokens = copy.deepcopy(words)
+        variable_names = list(substituions.keys())
+        uid = get_identifier_posistions_from_code(words, variable_names)
+        if len(uid) <= 0:
+            return {"succ": None, "tokens": None, "raw_tokens": None}
+        variable_substitue_dict = {w: substituions[w] for w in uid.keys()}
+        if len(variable_substitue_dict) <= 0:
+            return {"succ": None, "tokens": None, "raw_tokens": None}
+        old_uids = {}
+        old_uid = ""
+        res = None
+        for iteration in range(1, 1 + _max_iter):
+            res = replace(_tokens=code, _label=_label, _uid=uid,
+                          substitute_dict=variable_substitue_dict, _n_candi=_n_candi,
+                          _prob_threshold=_prob_threshold)
+            self._print_res(iteration, res)
+            if res["status"].lower() in ["s", "a"]:
+                if iteration == 1:
+                    old_uids[res["old_uid"]] = [res["new_uid"]]
+                    old_uid = res["old_uid"]
+                flag = 0
+                for k in old_uids.keys():
+                    if res["old_uid"] == old_uids[k][-1]:
+                        flag = 1
+                        old_uids[k].append(res["new_uid"])
+                        old_uid = k
+                        break
+                if flag == 0:
+                    old_uids[res["old_uid"]] = [res["new_uid"]]
+                    old_uid = res["old_uid"]
+                code = res["tokens"]
+                uid[res["new_uid"]] = uid.pop(res["old_uid"])
+                variable_substitue_dict[res["new_uid"]] = variable_substitue_dict.pop(res["old_uid"])
+                for i in range(len(raw_tokens)):
+                    if raw_tokens[i] == res["old_uid"]:
+                        raw_tokens[i] = res["new_uid"]
+                if res["status"].lower() == "s":
+                    replace_info, nb_changed_pos = {}, 0
+                    for uid_ in old_uids.keys():
+                        replace_info[uid_] = old_uids[uid_][-1]
+                        nb_changed_pos += len(uid[old_uids[uid_][-1]])
+                    return {"succ": True, "tokens": code, "raw_tokens": raw_tokens,
+                            "prog_length": prog_length, "new_pred": res["new_pred"],
+                            "is_success": 1, "old_uid": old_uid,
+                            "score_info": res["old_prob"][0] - res["new_prob"][0],
+                            "nb_changed_var": len(old_uids), "nb_changed_pos": nb_changed_pos,
+                            "replace_info": replace_info, "attack_type": attack_type}
+        replace_info, nb_changed_pos = {}, 0
+        for uid_ in old_uids.keys():
+            replace_info[uid_] = old_uids[uid_][-1]
+            nb_changed_pos += len(uid[old_uids[uid_][-1]])
+        return {"succ": False, "tokens": res["tokens"], "raw_tokens": None,
+                "prog_length": prog_length, "new_pred": res["new_pred"], "is_success": -1,
+                "old_uid": old_uid, "score_info": res["old_prob"][0] - res["new_prob"][0],
+                "nb_changed_var": len(old_uids), "nb_changed_pos": nb_changed_pos,
+                "replace_info": replace_info, "attack_type": attack_type}
+
+    def mcmc(self, tokenizer, substituions, code=None, _label=None, _n_candi=30, _max_iter=100,
+             _prob_threshold=0.95):
+        return self._run(tokenizer, substituions, code, _label, _n_candi, _max_iter,
+                         _prob_threshold, self._replace_uid, "MHM")
+
+    def mcmc_random(self, tokenizer, substituions, code=None, _label=None, _n_candi=30,
+                    _max_iter=100, _prob_threshold=0.95):
+        return self._run(tokenizer, substituions, code, _label, _n_candi, _max_iter,
+                         _prob_threshold, self._replace_uid_random, "MHM-Origin")
+
+    def _candidates_result(self, _tokens, _label, selected_uid, candi_token, candi_pairs,
+                           _prob_threshold):
+        """Shared tail of __replaceUID / __replaceUID_random (attacker.py:634-670)."""
+        # candidate 0 is the unmodified code; the others are get_example(code, uid, c)
+        ex = Example(_tokens, self.lang)
+        tok = self.tokenizer_mlm
+        L = self.args.block_size
+        pops = [[(selected_uid, c)] for c in candi_pairs]
+        ids0, lens0 = tok.featurize([_tokens], L)
+        if pops:
+            idsm, lensm = ex.mutant_ids(tok, pops, L, MODE_SINGLE)
+            ids = np.concatenate([ids0, idsm], 0)
+            lens = np.concatenate([lens0, lensm], 0)
+        else:
+            ids, lens = ids0, lens0
+        prob, pred = self.classifier.get_results(IdsDataset(ids, lens), self.args.eval_batch_size)
+        candi_tokens = [_tokens] + [None] * len(pops)
+
+        def text(i):
+            if candi_tokens[i] is None:
+                candi_tokens[i] = ex.mutant_text(pops[i - 1], MODE_SINGLE)
+            return candi_tokens[i]
+
+        for i in range(len(candi_token)):
+            if pred[i] != _label:
+                return {"status": "s", "alpha": 1, "tokens": text(i), "old_uid": selected_uid,
+                        "new_uid": candi_token[i], "old_prob": prob[0], "new_prob": prob[i],
+                        "old_pred": pred[0], "new_pred": pred[i],
+                        "nb_changed_pos": _tokens.count(selected_uid)}
+        candi_idx = 0
+        min_prob = 1.0
+        for idx, a_prob in enumerate(prob[1:]):
+            if a_prob[_label] < min_prob:
+                candi_idx = idx + 1
+                min_prob = a_prob[_label]
+        alpha = (1 - prob[candi_idx][_label] + 1e-10) / (1 - prob[0][_label] + 1e-10)
+        # the reference reports candi_tokens[i] with i the LAST loop index (attacker.py:662-670)
+        i = len(candi_token) - 1
+        status = "r" if (random.uniform(0, 1) > alpha or alpha < _prob_threshold) else "a"
+        return {"status": status, "alpha": alpha, "tokens": text(i), "old_uid": selected_uid,
+                "new_uid": candi_token[i], "old_prob": prob[0], "new_prob": prob[i],
+                "old_pred": pred[0], "new_pred": pred[i],
+                "nb_changed_pos": _tokens.count(selected_uid)}
+
+    def _replace_uid(self, _tokens, _label=None, _uid={}, substitute_dict={}, _n_candi=30,
+                     _prob_threshold=0.95, _candi_mode="random"):
+        assert _candi_mode.lower() in ["random", "nearby"]
+        selected_uid = random.sample(list(substitute_dict.keys()), 1)[0]
+        candi_token = [selected_uid]
+        pairs = []
+        pool = substitute_dict[selected_uid]
+        for c in random.sample(pool, min(_n_candi, len(pool))):
+            if c in _uid.keys():
+                continue
+            if isUID(c):
+                candi_token.append(c)
+                pairs.append(c)
+        return self._candidates_result(_tokens, _label, selected_uid, candi_token, pairs,
+                                       _prob_threshold)
+
+    def _replace_uid_random(self, _tokens, _label=None, _uid={}, substitute_dict={},
+                            _n_candi=30, _prob_threshold=0.95, _candi_mode="random"):
+        assert _candi_mode.lower() in ["random", "nearby"]
+        selected_uid = random.sample(list(substitute_dict.keys()), 1)[0]
+        candi_token = [selected_uid]
+        pairs = []
+        for c in random.sample(self.idx2token, _n_candi):
+            if c in _uid.keys():
+                continue
+            if isUID(c):
+                candi_token.append(c)
+                pairs.append(c)
+        return self._candidates_result(_tokens, _label, selected_uid, candi_token, pairs,
+                                       _prob_threshold)
+
+    def _print_res(self, _iter=None, _res=None, _prefix="  => "):
+        if not getattr(self.args, "verbose", False):
+            return
+        tag = {"s": "SUCC!", "r": "REJ.", "a": "ACC!"}[_res["status"].lower()]
+        print("%s iter %d, %s %s => %s (%d => %d, %.5f => %.5f) a=%.3f" % (
+            _prefix, _iter, tag, _res["old_uid"], _res["new_uid"], _res["old_pred"],
+            _res["new_pred"], _res["old_prob"][_res["old_pred"]],
+            _res["new_prob"][_res["old_pred"]], _res["alpha"]), flush=True)

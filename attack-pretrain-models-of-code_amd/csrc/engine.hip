@@ -31,8 +31,8 @@ hipError_t ae_launch_layernorm(const float*, const float*, const float*, float, 
                                hipStream_t);
 hipError_t ae_launch_gather_cls(const float*, const float*, const int*, int, float*, float*,
                                 hipStream_t);
-hipError_t ae_launch_head(const float*, const float*, const float*, const float*, const float*,
-                          int, int, int, float*, hipStream_t);
+hipError_t ae_launch_head_out(const float*, const float*, const float*, int, int, int, float*,
+                              hipStream_t);
 hipError_t ae_launch_splice(const int*, const int*, const int*, const int*, int, int, int, int,
                             int, int*, int*, hipStream_t);
 hipError_t ae_launch_topk(const float*, int, int, int, float*, int*, hipStream_t);
@@ -56,7 +56,7 @@ int fail(int code, const std::string& msg) {
       return fail(AE_EDEVICE, std::string(#x) + ": " + hipGetErrorString(_e));          \
   } while (0)
 
-enum { EPI_BIAS = 0, EPI_BIAS_GELU = 1, EPI_BIAS_RESIDUAL = 2 };
+enum { EPI_BIAS = 0, EPI_BIAS_GELU = 1, EPI_BIAS_RESIDUAL = 2, EPI_BIAS_TANH = 3 };
 
 struct LayerW {
   float *wqkv, *bqkv, *wo, *bo, *ln1g, *ln1b, *w1, *b1, *w2, *b2, *ln2g, *ln2b;
@@ -458,8 +458,12 @@ int ae_score(ae_engine* e, const int32_t* ids, const int32_t* lens, const int32_
   if ((rc = run_encoder(e, ids, pos, mask_bits, n, L, T, max_len, true, st))) return rc;
   const int kind = e->cfg.head_kind == AE_HEAD_SIGMOID1 ? 0 : (e->cfg.head_kind == AE_HEAD_PAIR2 ? 2 : 1);
   const int n_out = kind == 2 ? n / 2 : n;
-  HIPC(ae_launch_head(e->xc, e->hd_w, e->hd_b, e->ho_w, e->ho_b, kind, e->cfg.num_labels, n_out,
-                      probs_out, st));
+  // head: dense (+tanh) as a GEMM over the compact CLS rows (pair head: [n/2, 1536] view), then
+  // out_proj + sigmoid/softmax
+  const int in_dim = kind == 2 ? 2 * e->cfg.hidden : e->cfg.hidden;
+  HIPC(ae_launch_gemm_f32(e->xc, e->hd_w, e->hd_b, nullptr, e->tc, n_out, e->cfg.hidden, in_dim,
+                          in_dim, in_dim, e->cfg.hidden, EPI_BIAS_TANH, nullptr, st));
+  HIPC(ae_launch_head_out(e->tc, e->ho_w, e->ho_b, kind, e->cfg.num_labels, n_out, probs_out, st));
   return AE_OK;
 }
 

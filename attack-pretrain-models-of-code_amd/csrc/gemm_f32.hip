@@ -1,6 +1,6 @@
 // gemm_f32.hip — exact-f32 MFMA GEMM with fused epilogues for the RoBERTa encoder (parity mode).
 //
-// C[M,N] = A[M,K] · W[N,K]^T + bias[N]  (+ GELU | + residual R[M,N])
+// C[M,N] = A[M,K] · W[N,K]^T + bias[N]  (+ GELU | + residual R[M,N] | tanh)
 // This is every nn.Linear of the encoder the reference reaches through
 // RobertaForSequenceClassification (CodeXGLUE/Defect-detection/code/model.py:25): QKV, attention
 // output, intermediate (GELU) and output projections.  W keeps the HF nn.Linear layout
@@ -19,7 +19,7 @@ namespace {
 constexpr int BM = 128, BN = 128, BK = 32, LDS_STRIDE = 36;
 }
 
-enum { EPI_BIAS = 0, EPI_BIAS_GELU = 1, EPI_BIAS_RESIDUAL = 2 };
+enum { EPI_BIAS = 0, EPI_BIAS_GELU = 1, EPI_BIAS_RESIDUAL = 2, EPI_BIAS_TANH = 3 };
 
 template <int EPI>
 __global__ __launch_bounds__(256, 2) void gemm_f32_nt_kernel(
@@ -123,6 +123,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_nt_kernel(
         if (row < M) {
           float v = acc[a][b][r] + bv;
           if (EPI == EPI_BIAS_GELU) v = gelu_erf(v);
+          if (EPI == EPI_BIAS_TANH) v = tanhf(v);
           if (EPI == EPI_BIAS_RESIDUAL) v += R[(size_t)row * ldc + col];
           C[(size_t)row * ldc + col] = v;
         }
@@ -148,6 +149,10 @@ extern "C" hipError_t ae_launch_gemm_f32(const float* A, const float* W, const f
       break;
     case EPI_BIAS_GELU:
       hipLaunchKernelGGL(gemm_f32_nt_kernel<EPI_BIAS_GELU>, grid, block, 0, stream, A, W, bias, R,
+                         C, M, N, K, lda, ldw, ldc, row_map);
+      break;
+    case EPI_BIAS_TANH:
+      hipLaunchKernelGGL(gemm_f32_nt_kernel<EPI_BIAS_TANH>, grid, block, 0, stream, A, W, bias, R,
                          C, M, N, K, lda, ldw, ldc, row_map);
       break;
     default:

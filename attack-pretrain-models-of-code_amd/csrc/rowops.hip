@@ -145,55 +145,52 @@ __global__ __launch_bounds__(256) void gather_cls_kernel(const float* __restrict
 }
 
 // ---------------------------------------------------------------------------------------------
-// Classification heads over compact CLS rows h[n_seq][768].  One workgroup per output row.
-//   kind 0: sigmoid1  -> out[row] = sigmoid(...)            (num_labels must be 1)
-//   kind 1: softmaxN  -> out[row][0..C) = softmax(...)
-//   kind 2: pair2     -> features = cat(h[2row], h[2row+1]) (1536) ; softmax over 2
-__global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ h,
-                                                   const float* __restrict__ wd,
-                                                   const float* __restrict__ bd,
-                                                   const float* __restrict__ wo,
-                                                   const float* __restrict__ bo, int kind, int C,
-                                                   float* __restrict__ out) {
-  __shared__ float feat[2 * AE_HIDDEN];
-  __shared__ float hid[AE_HIDDEN];
-  __shared__ float logit[128];
-  const int row = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int in_dim = kind == 2 ? 2 * AE_HIDDEN : AE_HIDDEN;
-  const float* src = h + (size_t)row * (kind == 2 ? 2 : 1) * AE_HIDDEN;
-  for (int i = tid; i < in_dim; i += 256) feat[i] = src[i];
-  __syncthreads();
-  // dense + tanh: one wave per output neuron, lanes stride over the input (coalesced W rows)
-  for (int o = wave; o < AE_HIDDEN; o += 4) {
-    const float* wr = wd + (size_t)o * in_dim;
-    float acc = 0.f;
-    for (int k = lane; k < in_dim; k += 64) acc += wr[k] * feat[k];
-    acc = wave_sum(acc);
-    if (lane == 0) hid[o] = tanhf(acc + bd[o]);
+// Classification head output layer.  The head's dense layer (+tanh) runs as an MFMA GEMM over the
+// compact CLS rows (for the clone pair head the [n,768] CLS matrix IS the [n/2,1536] pair-feature
+// matrix); this kernel applies out_proj and the final activation, one wave per output row.
+//   kind 0: sigmoid1  -> out[row] = sigmoid(logit)        (C == 1)
+//   kind 1: softmaxN / kind 2: pair2 -> out[row][0..C) = softmax(logits)
+__global__ __launch_bounds__(256) void head_out_kernel(const float* __restrict__ hid,
+                                                       const float* __restrict__ wo,
+                                                       const float* __restrict__ bo, int kind,
+                                                       int C, int n_out, float* __restrict__ out) {
+  __shared__ float logit[4][128];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + wave;
+  if (row >= n_out) return;
+  const float* h = hid + (size_t)row * AE_HIDDEN;
+  float hv[12];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const floatx4 a = *reinterpret_cast<const floatx4*>(h + c * 256 + lane * 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) hv[4 * c + e] = a[e];
   }
-  __syncthreads();
-  for (int o = wave; o < C; o += 4) {
+  for (int o = 0; o < C; ++o) {
     const float* wr = wo + (size_t)o * AE_HIDDEN;
     float acc = 0.f;
-    for (int k = lane; k < AE_HIDDEN; k += 64) acc += wr[k] * hid[k];
-    acc = wave_sum(acc);
-    if (lane == 0) logit[o] = acc + bo[o];
-  }
-  __syncthreads();
-  if (wave == 0) {
-    if (kind == 0) {
-      if (lane == 0) out[row] = 1.f / (1.f + expf(-logit[0]));
-    } else {
-      float mx = -INFINITY;
-      for (int c = lane; c < C; c += 64) mx = fmaxf(mx, logit[c]);
-      mx = wave_max(mx);
-      float sm = 0.f;
-      for (int c = lane; c < C; c += 64) sm += expf(logit[c] - mx);
-      sm = wave_sum(sm);
-      for (int c = lane; c < C; c += 64) out[(size_t)row * C + c] = expf(logit[c] - mx) / sm;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const floatx4 w = *reinterpret_cast<const floatx4*>(wr + c * 256 + lane * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc += w[e] * hv[4 * c + e];
     }
+    acc = wave_sum(acc);
+    if (lane == 0) logit[wave][o] = acc + bo[o];
   }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  if (kind == 0) {
+    if (lane == 0) out[row] = 1.f / (1.f + expf(-logit[wave][0]));
+    return;
+  }
+  float mx = -INFINITY;
+  for (int c = lane; c < C; c += 64) mx = fmaxf(mx, logit[wave][c]);
+  mx = wave_max(mx);
+  float sm = 0.f;
+  for (int c = lane; c < C; c += 64) sm += expf(logit[wave][c] - mx);
+  sm = wave_sum(sm);
+  for (int c = lane; c < C; c += 64) out[(size_t)row * C + c] = expf(logit[wave][c] - mx) / sm;
 }
 
 // Scatter compacted rows back to the padded [n, L, 768] layout (ae_encode).
@@ -254,10 +251,12 @@ hipError_t ae_launch_gather_cls(const float* a, const float* b, const int* cu, i
   hipLaunchKernelGGL(gather_cls_kernel, dim3((n + 3) / 4), dim3(256), 0, st, a, b, cu, n, ac, bc);
   return hipGetLastError();
 }
-hipError_t ae_launch_head(const float* h, const float* wd, const float* bd, const float* wo,
-                          const float* bo, int kind, int C, int n_out, float* out, hipStream_t st) {
+hipError_t ae_launch_head_out(const float* hid, const float* wo, const float* bo, int kind, int C,
+                              int n_out, float* out, hipStream_t st) {
   if (n_out <= 0) return hipSuccess;
-  hipLaunchKernelGGL(head_kernel, dim3(n_out), dim3(256), 0, st, h, wd, bd, wo, bo, kind, C, out);
+  if (C < 1 || C > 128) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(head_out_kernel, dim3((n_out + 3) / 4), dim3(256), 0, st, hid, wo, bo, kind,
+                     C, n_out, out);
   return hipGetLastError();
 }
 }

@@ -1,0 +1,157 @@
+"""Attack drivers: the per-example loops of gi_attack.py (greedy, then GA on failure) and
+mhm_attack.py (MHM-NS), over the engine.
+
+Follows CodeXGLUE/Defect-detection/code/gi_attack.py:154-218 and mhm_attack.py:160-236: the
+original example's features come from the fixture's `func` (run.py:79-86), substitutes from its
+`substitutes`; one Recorder CSV row per example; success rate over examples the victim classified
+correctly.  Also the multi-GPU form: examples are pulled from a dynamic queue shared by all ranks
+(an atomic counter in the torch.distributed store; no tensor traffic) and the per-rank statistics
+are all-gathered at the end.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import random
+import time
+
+import numpy as np
+
+from .attacker import Attacker, MHM_Attacker
+from .host import Tokenizer
+from .utils import Recorder, build_vocab, set_seed
+
+
+@dataclasses.dataclass
+class AttackArgs:
+    block_size: int = 512
+    eval_batch_size: int = 64
+    use_ga: bool = True
+    seed: int = 123456
+    lang: str = "c"
+    verbose: bool = False
+    csv_store_path: str | None = None
+    rng: str = "global"   # "global": one random stream in example order (reference);
+                          # "per_example": random.seed(seed + index) before each example
+
+
+def load_fixture(path, start=0, end=None):
+    codes, subs, labels = [], [], []
+    with open(path) as f:
+        for i, line in enumerate(f):
+            if i < start or (end is not None and i >= end):
+                continue
+            js = json.loads(line)
+            codes.append(js["func"] if "func" in js else js["code"])
+            subs.append(js["substitutes"])
+            labels.append(int(js.get("target", js.get("label", 0))))
+    return codes, subs, labels
+
+
+def _example(tok, code, label, block):
+    """TextDataset item: (ids, label) of ' '.join(func.split()) (run.py:79-86)."""
+    import torch
+
+    ids, _ = tok.featurize([code], block)
+    return torch.from_numpy(ids[0].astype(np.int64)), torch.tensor(label)
+
+
+def attack_one(attacker, tok, code, subs, label, args):
+    example = _example(tok, code, label, args.block_size)
+    res = attacker.greedy_attack(example, code, subs)
+    attack_type = "Greedy"
+    if res[6] == -1 and args.use_ga:
+        res = attacker.ga_attack(example, code, subs, initial_replace=res[11])
+        attack_type = "GA"
+    return res, attack_type
+
+
+def run_gi_attack(model, codes, subs, labels, args: AttackArgs, indices=None, tok=None,
+                  queue=None, log=None):
+    """greedy (+GA) over the given examples; returns per-example records and totals.
+    queue: optional callable returning the next example index (or None when drained)."""
+    tok = tok or Tokenizer()
+    attacker = Attacker(args, model, tok, None, tok, use_bpe=1, threshold_pred_score=0)
+    recorder = Recorder(args.csv_store_path) if args.csv_store_path else None
+    if args.rng == "global":
+        set_seed(args.seed)
+    order = list(range(len(codes))) if indices is None else list(indices)
+    records = []
+    t0 = time.time()
+    pos = 0
+    while True:
+        if queue is not None:
+            index = queue()
+            if index is None:
+                break
+        else:
+            if pos >= len(order):
+                break
+            index = order[pos]
+            pos += 1
+        if args.rng == "per_example":
+            random.seed(args.seed + index)
+        q0 = model.query
+        ts = time.time()
+        res, attack_type = attack_one(attacker, tok, codes[index], subs[index], labels[index], args)
+        (code, prog_length, adv_code, true_label, orig_label, temp_label, is_success,
+         variable_names, names_to_importance_score, nb_changed_var, nb_changed_pos,
+         replaced_words) = res
+        dt = (time.time() - ts) / 60
+        score_info = ""
+        if names_to_importance_score is not None:
+            for key in names_to_importance_score.keys():
+                score_info += key + ":" + str(names_to_importance_score[key]) + ","
+        replace_info = ""
+        if replaced_words is not None:
+            for key in replaced_words.keys():
+                replace_info += key + ":" + replaced_words[key] + ","
+        queries = model.query - q0
+        if recorder:
+            recorder.write(index, code, prog_length, adv_code, true_label, orig_label, temp_label,
+                           is_success, variable_names, score_info, nb_changed_var, nb_changed_pos,
+                           replace_info, attack_type, queries, dt)
+        records.append(dict(index=index, is_success=is_success, attack_type=attack_type,
+                            queries=queries, adv_code=adv_code, replace_info=replace_info,
+                            nb_changed_var=nb_changed_var, nb_changed_pos=nb_changed_pos,
+                            prog_length=prog_length, time_s=dt * 60))
+        if log:
+            log(records[-1])
+    total = time.time() - t0
+    done = len(records)
+    correct = sum(r["is_success"] >= -1 for r in records)
+    succ = sum(r["is_success"] == 1 for r in records)
+    return dict(records=records, examples=done, total_cnt=correct, success=succ,
+                success_rate=(succ / correct) if correct else 0.0,
+                queries=sum(r["queries"] for r in records), wall_s=total)
+
+
+def run_mhm_attack(model, codes, subs, labels, args: AttackArgs, indices=None, tok=None,
+                   n_candi=30, max_iter=100, prob_threshold=1, original=False):
+    """mhm_attack.py:160-236 (MHM-NS; `original` = MHM with the random-token candidates)."""
+    tok = tok or Tokenizer()
+    from .attacker import get_identifiers
+
+    set_seed(args.seed)
+    code_tokens = [get_identifiers(c, args.lang)[1] for c in codes]
+    id2token, token2id = build_vocab(code_tokens, 5000)
+    attacker = MHM_Attacker(args, model, None, tok, token2id, id2token)
+    order = list(range(len(codes))) if indices is None else list(indices)
+    records, t0 = [], time.time()
+    for index in order:
+        example = _example(tok, codes[index], labels[index], args.block_size)
+        q0 = model.query
+        probs, preds = model.get_results([example], args.eval_batch_size)
+        if preds[0] != labels[index]:
+            records.append(dict(index=index, is_success=-4, queries=model.query - q0))
+            continue
+        fn = attacker.mcmc_random if original else attacker.mcmc
+        res = fn(tok, subs[index], _label=labels[index], code=codes[index], _n_candi=n_candi,
+                 _max_iter=max_iter, _prob_threshold=prob_threshold)
+        ok = 1 if res["succ"] else (-1 if res["succ"] is not None else -3)
+        records.append(dict(index=index, is_success=ok, queries=model.query - q0))
+    correct = sum(r["is_success"] >= -1 for r in records)
+    succ = sum(r["is_success"] == 1 for r in records)
+    return dict(records=records, examples=len(records), total_cnt=correct, success=succ,
+                success_rate=(succ / correct) if correct else 0.0,
+                queries=sum(r["queries"] for r in records), wall_s=time.time() - t0)

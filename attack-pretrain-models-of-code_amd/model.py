@@ -70,7 +70,7 @@ class Model:
     def to(self, *a, **k):
         return self
 
-    def _score_ids(self, ids: np.ndarray) -> np.ndarray:
+    def _score_ids(self, ids: np.ndarray, lens: np.ndarray | None = None) -> np.ndarray:
         import torch
 
         pad = self.engine.pad_id
@@ -83,9 +83,10 @@ class Model:
         step = self.max_rows_per_launch
         for s in range(0, n, step):
             chunk = np.ascontiguousarray(ids[s:s + step], dtype=np.int32)
-            lens = (chunk != pad).sum(axis=1).astype(np.int32)
+            cl = (chunk != pad).sum(axis=1).astype(np.int32) if lens is None or \
+                self.task == "clone" else np.ascontiguousarray(lens[s:s + step], dtype=np.int32)
             dev = torch.from_numpy(chunk).to(f"cuda:{self.engine.device}", non_blocking=False)
-            outs.append(self.engine.score(dev, lens))
+            outs.append(self.engine.score(dev, cl))
         return torch.cat(outs, 0).cpu().numpy() if len(outs) > 1 else outs[0].cpu().numpy()
 
     def get_results(self, dataset, batch_size=None, threshold: float = 0.5):
@@ -93,7 +94,39 @@ class Model:
         self.query += len(dataset)
         if len(dataset) == 0:
             return [], []
-        logits = self._score_ids(stack_ids(dataset))
+        if hasattr(dataset, "ids") and hasattr(dataset, "lens"):  # utils.IdsDataset fast path
+            logits = self._score_ids(dataset.ids, dataset.lens)
+        else:
+            logits = self._score_ids(stack_ids(dataset))
+        return self._format(logits, threshold)
+
+    def get_results_population(self, example, tokenizer, population, mode: int, block_size: int,
+                               threshold: float = 0.5):
+        """Score a population of chromosomes of one program (len(population) queries).
+
+        The host library reduces every mutant to its word-id sequence (the mutant text is built
+        exactly as get_example / get_example_batch would); ae_splice assembles the [n, block]
+        ids on the GPU from the example's word table; the engine scores them.  Identical ids to
+        featurising the mutant texts (tests/test_host.py, tests/test_engine_gpu.py)."""
+        import torch
+
+        from .engine import splice
+
+        n = len(population)
+        self.query += n
+        if n == 0:
+            return [], []
+        word_tok, word_off, mut_words, mut_off, lens = example.mutant_words(
+            tokenizer, population, block_size, mode)
+        dev = f"cuda:{self.engine.device}"
+        ids, _ = splice(torch.from_numpy(word_tok).to(dev), torch.from_numpy(word_off).to(dev),
+                        torch.from_numpy(mut_words).to(dev), torch.from_numpy(mut_off).to(dev),
+                        n, block_size, tokenizer.cls_token_id, tokenizer.sep_token_id,
+                        tokenizer.pad_token_id)
+        logits = self.engine.score(ids, lens).cpu().numpy()
+        return self._format(logits, threshold)
+
+    def _format(self, logits, threshold: float = 0.5):
         if self.task == "devign":
             # model.py:56-57
             probs = [[1 - prob[0], prob[0]] for prob in logits]

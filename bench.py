@@ -73,6 +73,51 @@ def cpu_baseline(L, seconds, threads):
                       f"oracle/roberta_cpu.py fp32 eager, torch threads={threads}"}
 
 
+def attack_leg(dev, seconds, rank, world):
+    """End-to-end config-2 workload: greedy -> GA attack (gi_attack.py --use_ga) over the
+    test_subs_0_400 fixture, examples pulled in order from a shared queue until the time budget is
+    spent; victim queries/s and attacked examples/min over the whole job."""
+    from apmc_amd.drivers import AttackArgs, load_fixture, run_gi_attack
+    from apmc_amd.model import Model
+    from apmc_amd.weights import synthetic_state_dict
+
+    codes, subs, labels = load_fixture(ROOT / "data" / "devign" / "test_subs_0_400.jsonl")
+    model = Model(synthetic_state_dict(seed=0, head="sigmoid1"), task="devign", device=dev.index)
+    args = AttackArgs(block_size=512, eval_batch_size=64, seed=123456, rng="per_example")
+    t_end = time.time() + seconds
+    nxt = [rank]
+
+    def queue():
+        # static round-robin over ranks, bounded by the time budget (each rank its own slice)
+        if time.time() > t_end or nxt[0] >= len(codes):
+            return None
+        i = nxt[0]
+        nxt[0] += world
+        return i
+
+    out = run_gi_attack(model, codes, subs, labels, args, queue=queue)
+    stats = np.array([out["examples"], out["total_cnt"], out["success"], out["queries"],
+                      out["wall_s"]], dtype=np.float64)
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor(stats, device=dev)
+        g = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(g, t)
+        allst = torch.stack(g).cpu().numpy()
+    else:
+        allst = stats[None]
+    ex, cnt, suc, q = allst[:, 0].sum(), allst[:, 1].sum(), allst[:, 2].sum(), allst[:, 3].sum()
+    wall = allst[:, 4].max()
+    ga = sum(r["attack_type"] == "GA" for r in out["records"])
+    return {"workload": "CodeBERT Devign greedy->GA attack (gi_attack --use_ga), "
+                        "test_subs_0_400.jsonl in order, block 512, eval_batch_size 64",
+            "examples": int(ex), "correctly_classified": int(cnt), "successes": int(suc),
+            "success_rate": round(suc / cnt, 4) if cnt else None, "victim_queries": int(q),
+            "wall_s": round(wall, 2), "victim_queries_per_s": round(q / wall, 2),
+            "attacked_examples_per_min": round(60 * ex / wall, 3),
+            "rank0_ga_runs": int(ga), "rng": "random.seed(123456 + index) per example"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -83,6 +128,9 @@ def main():
     ap.add_argument("--precision", default="fp32", choices=["fp32"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--attack-seconds", type=float, default=90.0,
+                    help="time budget of the end-to-end GA attack leg over test_subs_0_400 "
+                         "(0 disables)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -176,6 +224,8 @@ def main():
         "whole_step_frac_of_fp32_peak": round(flops_per_query(L) * total_q / elapsed / 1e12 / world / peak, 4),
         "probs_checksum": float(np.round(probs.astype(np.float64).sum(), 6)),
     }
+    if args.attack_seconds > 0:
+        res["attack"] = attack_leg(dev, args.attack_seconds, rank, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
         res["cpu_baseline"] = cpu_baseline(L, args.cpu_seconds, threads)

@@ -7,7 +7,7 @@ TAG=${1:-prof}
 STEPS=${STEPS:-5}
 mkdir -p gpurun_out/$TAG
 export TMPDIR=/tmp
-B="$GRAFT_REPO_ROOT/bench.py --steps $STEPS --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-}"
+B="$GRAFT_REPO_ROOT/bench.py --steps $STEPS --warmup 2 --no-cpu-baseline --attack-seconds 0 ${BENCH_ARGS:-}"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/$TAG/trace" -o run -- python3 $B 2>&1 | tee gpurun_out/$TAG/trace.log
 rc=$?; echo "trace rc=$rc"; [ $rc -ne 0 ] && exit $rc
 for C in FETCH_SIZE WRITE_SIZE; do

@@ -1,0 +1,76 @@
+"""Summarise a rocprofv3 run of bench.py (scripts/gpu_profile.sh output) into profiles/.
+
+Writes profiles/<name>_kernel_stats.csv (the rocprofv3 --stats summary, copied verbatim) and
+profiles/<name>_pmc_ffn1.json: per-launch HBM traffic of the FFN1 GEMM (the roofline kernel)
+from FETCH_SIZE / WRITE_SIZE (KiB per dispatch).  gfx950 correction (MI355X_MICROARCH.md §HBM):
+FETCH_SIZE reports half the bytes of wide coalesced streaming reads, so read bytes = 2 x
+FETCH_SIZE x 1024; WRITE_SIZE is exact for 16-B-per-lane stores (our epilogue stores are 4-B
+per lane, so WRITE_SIZE is reported uncorrected and flagged uncalibrated).
+
+Usage: python tools/summarize_profile.py gpurun_out/prof_r1 r1
+"""
+import csv
+import json
+import pathlib
+import shutil
+import statistics
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+FFN1 = "gemm_f32_nt_kernel<1>"
+T, H, F = 64 * 512, 768, 3072
+ALGO_BYTES = 4 * (T * H + F * H + F + T * F)  # A + W + bias read, C written (fp32)
+
+
+def ffn1_rows(path, counter):
+    vals = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if FFN1 in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                # full-size launches only (grid = 256 rows/tile-blocks x 24 col tiles x 256 thr)
+                if int(r["Grid_Size"]) >= 256 * 24 * 256:
+                    vals.append(float(r["Counter_Value"]))
+    return vals
+
+
+def durations(path):
+    out = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if FFN1 in r["Kernel_Name"] and int(r["Grid_Size_X"]) >= 256 * 24 * 256:
+                out.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    return out
+
+
+def main():
+    src = pathlib.Path(sys.argv[1])
+    name = sys.argv[2]
+    out = ROOT / "profiles"
+    out.mkdir(exist_ok=True)
+    shutil.copy(src / "trace" / "run_kernel_stats.csv", out / f"{name}_kernel_stats.csv")
+    fetch = ffn1_rows(src / "pmc_FETCH_SIZE" / "run_counter_collection.csv", "FETCH_SIZE")
+    write = ffn1_rows(src / "pmc_WRITE_SIZE" / "run_counter_collection.csv", "WRITE_SIZE")
+    durs = durations(src / "trace" / "run_kernel_trace.csv")
+    fetch_b = 2 * statistics.mean(fetch) * 1024 if fetch else None
+    write_b = statistics.mean(write) * 1024 if write else None
+    res = {
+        "kernel": FFN1 + " (FFN1 [32768,768]x[768,3072] + bias + GELU, B=64 x L=512)",
+        "dispatches": len(fetch),
+        "avg_duration_us_trace": statistics.mean(durs) / 1e3 if durs else None,
+        "fetch_size_kib_mean_raw": statistics.mean(fetch) if fetch else None,
+        "write_size_kib_mean_raw": statistics.mean(write) if write else None,
+        "read_bytes_corrected": fetch_b,
+        "write_bytes": write_b,
+        "hbm_bytes_per_launch": (fetch_b or 0) + (write_b or 0),
+        "algorithmic_bytes_per_launch": ALGO_BYTES,
+        "traffic_over_algorithmic": ((fetch_b or 0) + (write_b or 0)) / ALGO_BYTES,
+        "notes": "read bytes = 2 x FETCH_SIZE (gfx950 half-count on wide streaming reads); "
+                 "WRITE_SIZE uncalibrated for 4-B-per-lane stores; Infinity Cache hits are "
+                 "counted by FETCH_SIZE, so A/W re-reads served on-die appear here",
+    }
+    (out / f"{name}_pmc_ffn1.json").write_text(json.dumps(res, indent=1))
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
