@@ -21,6 +21,9 @@
 extern "C" {
 hipError_t ae_launch_gemm_f32(const float*, const float*, const float*, const float*, float*, int,
                               int, int, int, int, int, int, const int*, hipStream_t);
+hipError_t ae_launch_gemm_x3(const float*, const unsigned short*, const unsigned short*,
+                             const float*, const float*, float*, int, int, int, int, int, int,
+                             int, int, hipStream_t);
 hipError_t ae_launch_attention_f32(const float*, float*, const int*, const int*, int, int, int,
                                    const uint32_t*, int, hipStream_t);
 hipError_t ae_launch_compact(const int*, const int*, const int*, int, int, int, int*, int*, int*,
@@ -60,7 +63,9 @@ enum { EPI_BIAS = 0, EPI_BIAS_GELU = 1, EPI_BIAS_RESIDUAL = 2, EPI_BIAS_TANH = 3
 
 struct LayerW {
   float *wqkv, *bqkv, *wo, *bo, *ln1g, *ln1b, *w1, *b1, *w2, *b2, *ln2g, *ln2b;
-  unsigned short *wqkv_h, *wo_h, *w1_h, *w2_h;  // bf16 copies (AE_PREC_BF16)
+  // split-bf16 planes (AE_PREC_BF16: hi only; AE_PREC_F32X3: hi + lo)
+  unsigned short *wqkv_h, *wo_h, *w1_h, *w2_h;
+  unsigned short *wqkv_l, *wo_l, *w1_l, *w2_l;
 };
 
 struct ProfRec {
@@ -136,12 +141,28 @@ unsigned short host_f2bf(float f) {
   return (unsigned short)(u >> 16);
 }
 
-int upload_bf16(ae_engine* e, const std::vector<float>& host, unsigned short** dst) {
-  std::vector<unsigned short> h(host.size());
-  for (size_t i = 0; i < host.size(); ++i) h[i] = host_f2bf(host[i]);
-  int rc = dev_alloc(e, (void**)dst, h.size() * 2);
+float host_bf2f(unsigned short b) {
+  const uint32_t u = (uint32_t)b << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+// W = hi + lo with hi = bf16(W), lo = bf16(W - hi) (round-to-nearest-even); lo only if dst_lo
+int upload_split(ae_engine* e, const float* host, size_t n, unsigned short** dst_hi,
+                 unsigned short** dst_lo) {
+  std::vector<unsigned short> h(n), l(dst_lo ? n : 0);
+  for (size_t i = 0; i < n; ++i) {
+    h[i] = host_f2bf(host[i]);
+    if (dst_lo) l[i] = host_f2bf(host[i] - host_bf2f(h[i]));
+  }
+  int rc = dev_alloc(e, (void**)dst_hi, n * 2);
   if (rc) return rc;
-  HIPC(hipMemcpy(*dst, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(*dst_hi, h.data(), n * 2, hipMemcpyHostToDevice));
+  if (dst_lo) {
+    if ((rc = dev_alloc(e, (void**)dst_lo, n * 2))) return rc;
+    HIPC(hipMemcpy(*dst_lo, l.data(), n * 2, hipMemcpyHostToDevice));
+  }
   return AE_OK;
 }
 
@@ -224,12 +245,17 @@ struct Prof {
   }
 };
 
-int gemm(ae_engine* e, const float* A, const float* W, const unsigned short* Wh, const float* bias,
-         const float* R, float* C, int M, int N, int K, int epi, hipStream_t st, bool is_ffn1) {
+int gemm(ae_engine* e, const float* A, const float* W, const unsigned short* Wh,
+         const unsigned short* Wl, const float* bias, const float* R, float* C, int M, int N, int K,
+         int epi, hipStream_t st, bool is_ffn1) {
   const bool prof = (e->prof_kind == AE_KIND_GEMM_ANY) || (e->prof_kind == AE_KIND_GEMM_FFN1 && is_ffn1);
   Prof p(e, st, prof, 2.0 * M * N * K);
-  (void)Wh;
-  HIPC(ae_launch_gemm_f32(A, W, bias, R, C, M, N, K, K, K, N, epi, nullptr, st));
+  if (e->cfg.precision != AE_PREC_FP32 && Wh) {
+    const int terms = e->cfg.precision == AE_PREC_F32X3 ? 3 : 1;
+    HIPC(ae_launch_gemm_x3(A, Wh, Wl, bias, R, C, M, N, K, K, K, N, epi, terms, st));
+  } else {
+    HIPC(ae_launch_gemm_f32(A, W, bias, R, C, M, N, K, K, K, N, epi, nullptr, st));
+  }
   return AE_OK;
 }
 
@@ -247,7 +273,7 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
     const LayerW& w = e->layers[li];
     const bool last_cls = cls_only && li == NL - 1;
     int rc;
-    if ((rc = gemm(e, e->x, w.wqkv, w.wqkv_h, w.bqkv, nullptr, e->qkv, (int)T, 3 * H, H, EPI_BIAS,
+    if ((rc = gemm(e, e->x, w.wqkv, w.wqkv_h, w.wqkv_l, w.bqkv, nullptr, e->qkv, (int)T, 3 * H, H, EPI_BIAS,
                    st, false)))
       return rc;
     {
@@ -257,27 +283,27 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
                                    last_cls ? 1 : max_len, n, heads, mask_bits, L, st));
     }
     if (!last_cls) {
-      if ((rc = gemm(e, e->ctx, w.wo, w.wo_h, w.bo, e->x, e->tmp, (int)T, H, H, EPI_BIAS_RESIDUAL,
+      if ((rc = gemm(e, e->ctx, w.wo, w.wo_h, w.wo_l, w.bo, e->x, e->tmp, (int)T, H, H, EPI_BIAS_RESIDUAL,
                      st, false)))
         return rc;
       HIPC(ae_launch_layernorm(e->tmp, w.ln1g, w.ln1b, eps, (int)T, e->x, st));
-      if ((rc = gemm(e, e->x, w.w1, w.w1_h, w.b1, nullptr, e->h1, (int)T, F, H, EPI_BIAS_GELU, st,
+      if ((rc = gemm(e, e->x, w.w1, w.w1_h, w.w1_l, w.b1, nullptr, e->h1, (int)T, F, H, EPI_BIAS_GELU, st,
                      true)))
         return rc;
-      if ((rc = gemm(e, e->h1, w.w2, w.w2_h, w.b2, e->x, e->tmp, (int)T, H, F, EPI_BIAS_RESIDUAL,
+      if ((rc = gemm(e, e->h1, w.w2, w.w2_h, w.w2_l, w.b2, e->x, e->tmp, (int)T, H, F, EPI_BIAS_RESIDUAL,
                      st, false)))
         return rc;
       HIPC(ae_launch_layernorm(e->tmp, w.ln2g, w.ln2b, eps, (int)T, e->x, st));
     } else {
       HIPC(ae_launch_gather_cls(e->ctx, e->x, e->cu, n, e->cc, e->xc, st));
-      if ((rc = gemm(e, e->cc, w.wo, w.wo_h, w.bo, e->xc, e->tc, n, H, H, EPI_BIAS_RESIDUAL, st,
+      if ((rc = gemm(e, e->cc, w.wo, w.wo_h, w.wo_l, w.bo, e->xc, e->tc, n, H, H, EPI_BIAS_RESIDUAL, st,
                      false)))
         return rc;
       HIPC(ae_launch_layernorm(e->tc, w.ln1g, w.ln1b, eps, n, e->xc, st));
-      if ((rc = gemm(e, e->xc, w.w1, w.w1_h, w.b1, nullptr, e->hc, n, F, H, EPI_BIAS_GELU, st,
+      if ((rc = gemm(e, e->xc, w.w1, w.w1_h, w.w1_l, w.b1, nullptr, e->hc, n, F, H, EPI_BIAS_GELU, st,
                      false)))
         return rc;
-      if ((rc = gemm(e, e->hc, w.w2, w.w2_h, w.b2, e->xc, e->tc, n, H, F, EPI_BIAS_RESIDUAL, st,
+      if ((rc = gemm(e, e->hc, w.w2, w.w2_h, w.w2_l, w.b2, e->xc, e->tc, n, H, F, EPI_BIAS_RESIDUAL, st,
                      false)))
         return rc;
       HIPC(ae_launch_layernorm(e->tc, w.ln2g, w.ln2b, eps, n, e->xc, st));
@@ -310,8 +336,8 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
     return fail(AE_EINVAL, "sigmoid head needs num_labels=1");
   if (cfg->head_kind == AE_HEAD_PAIR2 && cfg->num_labels != 2)
     return fail(AE_EINVAL, "pair head needs num_labels=2");
-  if (cfg->precision != AE_PREC_FP32)
-    return fail(AE_EINVAL, "only AE_PREC_FP32 is built in this version");
+  if (cfg->precision < AE_PREC_FP32 || cfg->precision > AE_PREC_F32X3)
+    return fail(AE_EINVAL, "precision must be AE_PREC_FP32, AE_PREC_BF16 or AE_PREC_F32X3");
   HIPC(hipSetDevice(device));
   ae_engine* e = new ae_engine();
   e->cfg = *cfg;
@@ -380,15 +406,16 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
     UP(p + "output.dense.bias", H, &w.b2);
     UP(p + "output.LayerNorm.weight", H, &w.ln2g);
     UP(p + "output.LayerNorm.bias", H, &w.ln2b);
-    if (cfg->precision == AE_PREC_BF16) {
-      auto grab = [&](const std::string& n) {
-        const ae_weight_view* t = wt.get(n);
-        return std::vector<float>(t->data, t->data + t->numel);
-      };
-      if ((rc = upload_bf16(e, hw, &w.wqkv_h)) ||
-          (rc = upload_bf16(e, grab(p + "attention.output.dense.weight"), &w.wo_h)) ||
-          (rc = upload_bf16(e, grab(p + "intermediate.dense.weight"), &w.w1_h)) ||
-          (rc = upload_bf16(e, grab(p + "output.dense.weight"), &w.w2_h))) {
+    if (cfg->precision != AE_PREC_FP32) {
+      const bool lo = cfg->precision == AE_PREC_F32X3;
+      auto view = [&](const std::string& n) { return wt.get(n); };
+      const ae_weight_view* vo = view(p + "attention.output.dense.weight");
+      const ae_weight_view* v1 = view(p + "intermediate.dense.weight");
+      const ae_weight_view* v2 = view(p + "output.dense.weight");
+      if ((rc = upload_split(e, hw.data(), hw.size(), &w.wqkv_h, lo ? &w.wqkv_l : nullptr)) ||
+          (rc = upload_split(e, vo->data, vo->numel, &w.wo_h, lo ? &w.wo_l : nullptr)) ||
+          (rc = upload_split(e, v1->data, v1->numel, &w.w1_h, lo ? &w.w1_l : nullptr)) ||
+          (rc = upload_split(e, v2->data, v2->numel, &w.w2_h, lo ? &w.w2_l : nullptr))) {
         std::string m = g_err;
         ae_destroy(e);
         return fail(rc, m);

@@ -15,7 +15,7 @@ from . import LIB_PATH
 from .weights import CODEBERT, RobertaShape
 
 AE_HEAD = {"sigmoid1": 0, "softmaxN": 1, "pair2": 2, "none": 3}
-AE_PREC = {"fp32": 0, "bf16": 1}
+AE_PREC = {"fp32": 0, "bf16": 1, "f32x3": 2}
 AE_KIND = {"gemm_ffn1": 0, "gemm_any": 1, "attention": 2}
 
 

@@ -125,7 +125,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--seq", type=int, default=512)
-    ap.add_argument("--precision", default="fp32", choices=["fp32"])
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "f32x3", "bf16"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--attack-seconds", type=float, default=90.0,
@@ -191,7 +191,18 @@ def main():
     value = total_q / elapsed
     per_launch_s = (k_ms / 1e3) / max(k_n, 1)
     achieved = (k_flop / max(k_n, 1)) / per_launch_s / 1e12 if k_n else None
-    peak = FP32_MFMA_PEAK_TFLOPS
+    # roofline peak of the arithmetic the GEMMs run: f32 MFMA; bf16 MFMA; split-bf16 issues
+    # 3 bf16 MFMAs per product, so its ceiling in algorithmic FLOP/s is the bf16 peak / 3
+    peak = {"fp32": FP32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS,
+            "f32x3": BF16_MFMA_PEAK_TFLOPS / 3}[args.precision]
+    parity = None
+    if args.precision != "fp32" and rank == 0:
+        # the split / bf16 numbers are only meaningful with their parity on this very batch
+        ref_eng = Engine(synthetic_state_dict(seed=0, head="sigmoid1"), head="sigmoid1",
+                         num_labels=1, precision="fp32", device=dev.index)
+        ref = ref_eng.score(ids_dev, lens).cpu().numpy()[:, 0]
+        ref_eng.close()
+        parity = float(np.abs(out.cpu().numpy()[:, 0] - ref).max())
     res = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -203,14 +214,18 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": {"fp32": "fp32", "f32x3": "fp32 (split-bf16 x3 MFMA, f32 accumulate)",
+                  "bf16": "bf16 (f32 accumulate / residual)"}[args.precision],
+        "precision_mode": args.precision,
+        "max_abs_dprob_vs_fp32_mode": parity,
         "data": "synthetic (seeded RoBERTa-base weights; uniform token ids; no checkpoint offline)",
         "config": {"workload": "CodeBERT Devign victim scoring of one GA mutant population per "
                                "step (config 2 shape: eval_batch_size 64 x block 512)",
                    "global_batch": B * world, "seq_len": L, "parallelism": f"dp{world} (example shards)"},
         "roofline": {
             "bound": "mfma",
-            "kernel": "gemm_f32_nt_kernel<EPI_BIAS_GELU> (FFN1 [T,768]x[768,3072])",
+            "kernel": ("gemm_f32_nt_kernel<EPI_BIAS_GELU>" if args.precision == "fp32" else
+                       "gemm_x3_kernel<256,256,...,EPI_GELU>") + " (FFN1 [T,768]x[768,3072])",
             "achieved": round(achieved, 3) if achieved else None,
             "peak": peak,
             "unit": "TFLOP/s",
@@ -221,7 +236,7 @@ def main():
             "flop_per_launch": (k_flop / k_n) if k_n else None,
         },
         "whole_step_tflops": round(flops_per_query(L) * total_q / elapsed / 1e12, 3),
-        "whole_step_frac_of_fp32_peak": round(flops_per_query(L) * total_q / elapsed / 1e12 / world / peak, 4),
+        "whole_step_frac_of_peak": round(flops_per_query(L) * total_q / elapsed / 1e12 / world / peak, 4),
         "probs_checksum": float(np.round(probs.astype(np.float64).sum(), 6)),
     }
     if args.attack_seconds > 0:

@@ -60,8 +60,10 @@ extern "C" {
 #define AE_HEAD_PAIR2 2    /* Clone: cat(CLS_a, CLS_b) 1536->768->tanh->2 -> softmax        */
 #define AE_HEAD_NONE 3     /* encoder only (MLM / cosine paths)                             */
 
-#define AE_PREC_FP32 0 /* exact-f32 MFMA (v_mfma_f32_32x32x2_f32) — parity mode      */
-#define AE_PREC_BF16 1 /* bf16 MFMA, f32 accumulate and f32 residual stream         */
+#define AE_PREC_FP32 0  /* exact-f32 MFMA (v_mfma_f32_32x32x2_f32) for every GEMM           */
+#define AE_PREC_BF16 1  /* GEMMs on bf16 MFMA (one term), f32 accumulate / residual stream  */
+#define AE_PREC_F32X3 2 /* GEMMs as split-bf16 (hi*hi + hi*lo + lo*hi) on bf16 MFMA:
+                           f32-class accuracy (probabilities within 1e-4) at 3 bf16 MFMAs  */
 
 typedef struct ae_config {
   int32_t layers;      /* 12 */

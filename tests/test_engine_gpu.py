@@ -15,13 +15,13 @@ pytestmark = pytest.mark.gpu
 PROB_TOL = 1e-4
 
 
-def _engine(seed, head, num_labels=1, with_mlm=False):
+def _engine(seed, head, num_labels=1, with_mlm=False, precision="fp32"):
     from apmc_amd.engine import Engine
     cache = _engine.__dict__.setdefault("cache", {})
-    key = (seed, head, num_labels, with_mlm)
+    key = (seed, head, num_labels, with_mlm, precision)
     if key not in cache:
         cache[key] = Engine(synthetic_sd(seed, head, num_labels, with_mlm), head=head,
-                            num_labels=num_labels, with_mlm=with_mlm)
+                            num_labels=num_labels, with_mlm=with_mlm, precision=precision)
     return cache[key]
 
 
@@ -170,3 +170,24 @@ def test_model_get_results_contract(gpu):
     assert preds == [int(v > 0.5) for v in p1]
     assert isinstance(probs[0][1], np.float32)
     assert probs2[0][1] == probs[0][1]
+
+
+# split-bf16 ("f32x3") must stay inside the fp32 parity tolerance; plain bf16 is the stated
+# bf16 tolerance (2e-2 on probabilities, measured ~1e-2 max in CPU emulation)
+@pytest.mark.parametrize("precision,tol", [("f32x3", PROB_TOL), ("bf16", 2e-2)])
+def test_split_precision_modes(gpu, precision, tol):
+    rng = np.random.default_rng(21)
+    lens = [512, 300, 129, 77, 512, 5, 256, 400]
+    ids = _rand_ids(rng, len(lens), 512, lens)
+    sd = synthetic_sd(0, "sigmoid1")
+    ref = ora.score(sd, ids, "sigmoid1")
+    p = _score(_engine(0, "sigmoid1", precision=precision), ids)
+    np.testing.assert_allclose(p, ref, atol=tol, rtol=0)
+
+
+def test_split_precision_other_heads(gpu):
+    g = golden()
+    p = _score(_engine(1, "softmaxN", 66, precision="f32x3"), g["aa_ids"])
+    np.testing.assert_allclose(p, g["aa_probs"], atol=PROB_TOL, rtol=0)
+    p = _score(_engine(2, "pair2", 2, precision="f32x3"), g["clone_ids"])
+    np.testing.assert_allclose(p, g["clone_probs"], atol=PROB_TOL, rtol=0)
