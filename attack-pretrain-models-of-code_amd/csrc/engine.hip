@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -24,6 +25,9 @@ hipError_t ae_launch_gemm_f32(const float*, const float*, const float*, const fl
 hipError_t ae_launch_gemm_x3(const float*, const unsigned short*, const unsigned short*,
                              const float*, const float*, float*, int, int, int, int, int, int,
                              int, int, hipStream_t);
+hipError_t ae_launch_gemm_x3g(const float*, const unsigned short*, const unsigned short*,
+                              const float*, const float*, float*, int, int, int, int, int, int,
+                              int, int, hipStream_t);
 hipError_t ae_launch_attention_f32(const float*, float*, const int*, const int*, int, int, int,
                                    const uint32_t*, int, hipStream_t);
 hipError_t ae_launch_compact(const int*, const int*, const int*, int, int, int, int*, int*, int*,
@@ -93,6 +97,8 @@ struct ae_engine {
   int* pinned_cu = nullptr;
   size_t cap_pinned = 0;
   hipEvent_t pinned_ready = nullptr;
+  // GEMM variant for the split-bf16 modes: 1 = LDS-DMA ring (default), 0 = register-staged
+  int gemm_variant = 1;
   // profiling
   int prof_kind = -1;
   std::vector<ProfRec> prof;
@@ -252,7 +258,10 @@ int gemm(ae_engine* e, const float* A, const float* W, const unsigned short* Wh,
   Prof p(e, st, prof, 2.0 * M * N * K);
   if (e->cfg.precision != AE_PREC_FP32 && Wh) {
     const int terms = e->cfg.precision == AE_PREC_F32X3 ? 3 : 1;
-    HIPC(ae_launch_gemm_x3(A, Wh, Wl, bias, R, C, M, N, K, K, K, N, epi, terms, st));
+    if (e->gemm_variant == 1 && M >= 256 && K % 16 == 0)
+      HIPC(ae_launch_gemm_x3g(A, Wh, Wl, bias, R, C, M, N, K, K, K, N, epi, terms, st));
+    else
+      HIPC(ae_launch_gemm_x3(A, Wh, Wl, bias, R, C, M, N, K, K, K, N, epi, terms, st));
   } else {
     HIPC(ae_launch_gemm_f32(A, W, bias, R, C, M, N, K, K, K, N, epi, nullptr, st));
   }
@@ -342,6 +351,7 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
   ae_engine* e = new ae_engine();
   e->cfg = *cfg;
   e->device = device;
+  if (const char* v = std::getenv("AE_GEMM_VARIANT")) e->gemm_variant = std::atoi(v);
   WeightTable wt;
   for (int i = 0; i < n_weights; ++i) wt.by_name[weights[i].name] = &weights[i];
   const int64_t H = cfg->hidden, F = cfg->ffn, V = cfg->vocab;
