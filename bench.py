@@ -84,17 +84,15 @@ def attack_leg(dev, seconds, rank, world):
     codes, subs, labels = load_fixture(ROOT / "data" / "devign" / "test_subs_0_400.jsonl")
     model = Model(synthetic_state_dict(seed=0, head="sigmoid1"), task="devign", device=dev.index)
     args = AttackArgs(block_size=512, eval_batch_size=64, seed=123456, rng="per_example")
-    t_end = time.time() + seconds
-    nxt = [rank]
+    from apmc_amd.dist import DynamicQueue
 
-    def queue():
-        # static round-robin over ranks, bounded by the time budget (each rank its own slice)
-        if time.time() > t_end or nxt[0] >= len(codes):
-            return None
-        i = nxt[0]
-        nxt[0] += world
-        return i
-
+    # all ranks pull the next example index from one atomic counter in the torch.distributed
+    # store (no tensor traffic), until the time budget is spent
+    queue = DynamicQueue(len(codes), key=f"bench_attack_{int(time.time())}",
+                         deadline=time.time() + seconds)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
     out = run_gi_attack(model, codes, subs, labels, args, queue=queue)
     stats = np.array([out["examples"], out["total_cnt"], out["success"], out["queries"],
                       out["wall_s"]], dtype=np.float64)
@@ -115,7 +113,8 @@ def attack_leg(dev, seconds, rank, world):
             "success_rate": round(suc / cnt, 4) if cnt else None, "victim_queries": int(q),
             "wall_s": round(wall, 2), "victim_queries_per_s": round(q / wall, 2),
             "attacked_examples_per_min": round(60 * ex / wall, 3),
-            "rank0_ga_runs": int(ga), "rng": "random.seed(123456 + index) per example"}
+            "rank0_ga_runs": int(ga), "rng": "random.seed(123456 + index) per example",
+            "sharding": "dynamic queue (torch.distributed store counter)"}
 
 
 def main():
