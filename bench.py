@@ -88,7 +88,7 @@ def attack_leg(dev, seconds, rank, world):
 
     # all ranks pull the next example index from one atomic counter in the torch.distributed
     # store (no tensor traffic), until the time budget is spent
-    queue = DynamicQueue(len(codes), key=f"bench_attack_{int(time.time())}",
+    queue = DynamicQueue(len(codes), key="bench_attack_queue",
                          deadline=time.time() + seconds)
     if world > 1:
         import torch.distributed as dist
