@@ -18,6 +18,8 @@
 // barrier per K-tile.  Tile order is XCD-remapped so neighbouring tiles share an XCD's L2.
 #include "common.h"
 
+#include <cstdlib>
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
@@ -227,12 +229,19 @@ extern "C" hipError_t ae_launch_gemm_x3(const float* A, const unsigned short* Wh
   const __bf16* wh = reinterpret_cast<const __bf16*>(Whi);
   const __bf16* wl = reinterpret_cast<const __bf16*>(Wlo);
   const long big_tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
+  // 256x256 (1 workgroup / CU) only when it fills >= 2 full rounds of 256 CUs; otherwise
+  // 128x128 (2 workgroups / CU, 4x the tiles).  AE_X3_TILE=128|256 forces a shape (A/B runs).
+  static const int force = [] {
+    const char* v = std::getenv("AE_X3_TILE");
+    return v ? std::atoi(v) : 0;
+  }();
+  const bool big = force ? force == 256 : big_tiles >= 512;
   if (terms == 3) {
-    if (big_tiles >= 384)
+    if (big)
       return launch_cfg<256, 256, 2, 4, 3>(A, wh, wl, bias, R, C, M, N, K, lda, ldw, ldc, epi, st);
     return launch_cfg<128, 128, 2, 4, 3>(A, wh, wl, bias, R, C, M, N, K, lda, ldw, ldc, epi, st);
   }
-  if (big_tiles >= 384)
+  if (big)
     return launch_cfg<256, 256, 2, 4, 1>(A, wh, wl, bias, R, C, M, N, K, lda, ldw, ldc, epi, st);
   return launch_cfg<128, 128, 2, 4, 1>(A, wh, wl, bias, R, C, M, N, K, lda, ldw, ldc, epi, st);
 }
