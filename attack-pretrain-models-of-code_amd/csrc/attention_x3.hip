@@ -1,0 +1,249 @@
+// attention_x3.hip — the fused attention of attention_f32.hip on bf16 matrix cores.
+//
+// Same algorithm and layout (ragged pad-compacted sequences, 128 queries of one (sequence, head)
+// per workgroup, online softmax with the query on the lane, optional bit-packed data-flow mask),
+// but both products run on v_mfma_f32_32x32x16_bf16 with every operand split into bf16 hi + lo
+// (TERMS = 3: x·y ≈ x_hi·y_hi + x_hi·y_lo + x_lo·y_hi, f32 accumulate) — f32-class accuracy at
+// the bf16 matrix rate; TERMS = 1 is plain bf16 (the stated-tolerance mode).
+//
+//   S^T[key][q]  = K · Q^T   A = K (LDS, key rows, 16-B chunks XOR-swizzled by key&7), B = Q^T
+//                            (this lane's query row, pre-scaled by 1/8 and split once, in VGPRs)
+//   O^T[d][q]   += V^T · P^T A = V^T (LDS, stored transposed [d][key] with 72-B rows: the two
+//                            4-key runs a lane reads are conflict-free ds_read_b64), B = P^T taken
+//                            straight from the S^T accumulator: accumulator registers 8t..8t+7 of
+//                            lane half h hold keys (j&3)+8(j>>2)+4h+16t — that permuted key order
+//                            is used for the V^T operand of the same k-slot.
+#include "common.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+namespace {
+constexpr int QPB = 128, KT = 32;
+constexpr int K_ROWB = 128;          // 64 d bf16 per key row
+constexpr int K_PLANE = KT * K_ROWB; // 4 KiB
+constexpr int VT_ROWB = 72;          // 32 keys bf16 + 8 B pad
+constexpr int VT_PLANE = 64 * VT_ROWB;
+constexpr int STAGE = 2 * K_PLANE + 2 * VT_PLANE;  // hi/lo planes of K and V^T
+constexpr int OSTRIDE = 65;
+constexpr int LDS_BYTES = (2 * STAGE > 4 * 32 * OSTRIDE * 4) ? 2 * STAGE : 4 * 32 * OSTRIDE * 4;
+
+__device__ __forceinline__ int kswz(int key, int chunk) { return chunk ^ (key & 7); }
+}  // namespace
+
+template <int TERMS, bool HAS_MASK>
+__global__ __launch_bounds__(256, 2) void attn_x3_kernel(const float* __restrict__ qkv,
+                                                         float* __restrict__ out,
+                                                         const int* __restrict__ cu,
+                                                         const int* __restrict__ q_rows,
+                                                         const uint32_t* __restrict__ mask,
+                                                         int mask_L) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
+  const int seq = blockIdx.z, head = blockIdx.y, qb = blockIdx.x;
+  const int start = cu[seq];
+  const int len = cu[seq + 1] - start;
+  const int nq = q_rows ? min(len, q_rows[0]) : len;
+  if (qb * QPB >= nq) return;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  constexpr int LDQKV = 3 * AE_HIDDEN;
+
+  // Q fragments: step s covers d = 16s + 8h .. +8 (B operand: B[k=d][j=q])
+  const int q = qb * QPB + wave * 32 + li;
+  const int qr = q < nq ? q : nq - 1;
+  bf16x8 qh[4], ql[4];
+  {
+    const float* qp = qkv + (size_t)(start + qr) * LDQKV + head * AE_HEAD_DIM;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const floatx4 a = *reinterpret_cast<const floatx4*>(qp + 16 * s + 8 * lh);
+      const floatx4 b = *reinterpret_cast<const floatx4*>(qp + 16 * s + 8 * lh + 4);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = (e < 4 ? a[e] : b[e - 4]) * 0.125f;
+        const __bf16 h = (__bf16)v;
+        qh[s][e] = h;
+        ql[s][e] = (__bf16)(v - (float)h);
+      }
+    }
+  }
+
+  // staging: thread -> key row (tid>>4) and +16, float4 chunk (tid&15) of K and of V
+  const int st_key = tid >> 4, st_c4 = tid & 15;
+  floatx4 rk[2], rv[2];
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int key = kt * KT + st_key + 16 * i;
+      key = key < len ? key : len - 1;
+      const float* base = qkv + (size_t)(start + key) * LDQKV + head * AE_HEAD_DIM + st_c4 * 4;
+      rk[i] = *reinterpret_cast<const floatx4*>(base + AE_HIDDEN);
+      rv[i] = *reinterpret_cast<const floatx4*>(base + 2 * AE_HIDDEN);
+    }
+  };
+  auto lstore = [&](int buf) {
+    unsigned char* st = lds + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int key = st_key + 16 * i;
+      // K: 4 consecutive d at d0 = 4*st_c4 -> 8 B in chunk d0/8, half (d0/4)&1
+      bf16x4 kh, kl;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const __bf16 h = (__bf16)rk[i][e];
+        kh[e] = h;
+        kl[e] = (__bf16)(rk[i][e] - (float)h);
+      }
+      const int off = key * K_ROWB + kswz(key, st_c4 >> 1) * 16 + (st_c4 & 1) * 8;
+      *reinterpret_cast<bf16x4*>(st + off) = kh;
+      if (TERMS == 3) *reinterpret_cast<bf16x4*>(st + K_PLANE + off) = kl;
+      // V^T: element (key, d) -> row d, column key
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int d = st_c4 * 4 + e;
+        const __bf16 h = (__bf16)rv[i][e];
+        *reinterpret_cast<__bf16*>(st + 2 * K_PLANE + d * VT_ROWB + key * 2) = h;
+        if (TERMS == 3)
+          *reinterpret_cast<__bf16*>(st + 2 * K_PLANE + VT_PLANE + d * VT_ROWB + key * 2) =
+              (__bf16)(rv[i][e] - (float)h);
+      }
+    }
+  };
+
+  floatx16 o0, o1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; }
+  float m_run = -INFINITY, l_run = 0.f;
+  const uint32_t* mrow = nullptr;
+  if (HAS_MASK) mrow = mask + ((size_t)seq * mask_L + qr) * (mask_L / 32);
+
+  const int nkt = (len + KT - 1) / KT;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) gload(kt + 1);
+    const unsigned char* st = lds + cur * STAGE;
+
+    // ---- S^T = K Q^T (4 k-steps of 16 d)
+    floatx16 s;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int off = li * K_ROWB + kswz(li, 2 * ks + lh) * 16;
+      const bf16x8 kh = *reinterpret_cast<const bf16x8*>(st + off);
+      if (TERMS == 3) {
+        const bf16x8 kl = *reinterpret_cast<const bf16x8*>(st + K_PLANE + off);
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl, qh[ks], s, 0, 0, 0);
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, ql[ks], s, 0, 0, 0);
+      }
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, qh[ks], s, 0, 0, 0);
+    }
+
+    // ---- mask + online softmax (lane = query)
+    uint32_t mbits = 0xffffffffu;
+    if (HAS_MASK) mbits = mrow[kt];
+    float mt = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int kk = mfma32_row(r, lh);
+      const bool ok = (kt * KT + kk < len) && ((mbits >> kk) & 1u);
+      s[r] = ok ? s[r] : -INFINITY;
+      mt = fmaxf(mt, s[r]);
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float m_new = fmaxf(m_run, mt);
+    const float alpha = (m_run == -INFINITY) ? 0.f : __expf(m_run - m_new);
+    float psum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = (s[r] == -INFINITY) ? 0.f : __expf(s[r] - m_new);
+      s[r] = p;
+      psum += p;
+    }
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+
+    // ---- O^T += V^T P^T (2 k-steps of 16 keys, 2 d-tiles)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      bf16x8 ph, pl;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float p = s[8 * t + j];
+        const __bf16 h = (__bf16)p;
+        ph[j] = h;
+        pl[j] = (__bf16)(p - (float)h);
+      }
+      // keys of this k-slot: 16t + 4h + {0..3} and 16t + 8 + 4h + {0..3}
+      const int k0 = 16 * t + 4 * lh;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int d = dt * 32 + li;
+        const unsigned char* vrow = st + 2 * K_PLANE + d * VT_ROWB;
+        bf16x8 vh, vl;
+        {
+          const bf16x4 a = *reinterpret_cast<const bf16x4*>(vrow + 2 * k0);
+          const bf16x4 b = *reinterpret_cast<const bf16x4*>(vrow + 2 * (k0 + 8));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { vh[e] = a[e]; vh[4 + e] = b[e]; }
+        }
+        if (TERMS == 3) {
+          const bf16x4 a = *reinterpret_cast<const bf16x4*>(vrow + VT_PLANE + 2 * k0);
+          const bf16x4 b = *reinterpret_cast<const bf16x4*>(vrow + VT_PLANE + 2 * (k0 + 8));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { vl[e] = a[e]; vl[4 + e] = b[e]; }
+        }
+        floatx16& o = dt == 0 ? o0 : o1;
+        if (TERMS == 3) {
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl, ph, o, 0, 0, 0);
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, pl, o, 0, 0, 0);
+        }
+        o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, ph, o, 0, 0, 0);
+      }
+    }
+
+    if (kt + 1 < nkt) lstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  float* os = reinterpret_cast<float*>(lds) + wave * 32 * OSTRIDE;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int d = mfma32_row(r, lh);
+    os[li * OSTRIDE + d] = o0[r] * inv;
+    os[li * OSTRIDE + 32 + d] = o1[r] * inv;
+  }
+  __syncthreads();
+  for (int rr = 0; rr < 32; ++rr) {
+    const int qq = qb * QPB + wave * 32 + rr;
+    if (qq < nq)
+      out[(size_t)(start + qq) * AE_HIDDEN + head * AE_HEAD_DIM + lane] = os[rr * OSTRIDE + lane];
+  }
+}
+
+extern "C" hipError_t ae_launch_attention_x3(const float* qkv, float* out, const int* cu,
+                                             const int* q_rows, int max_q, int n, int heads,
+                                             const uint32_t* mask, int mask_L, int terms,
+                                             hipStream_t stream) {
+  if (n <= 0 || max_q <= 0) return hipSuccess;
+  dim3 grid((max_q + QPB - 1) / QPB, heads, n), block(256);
+#define ATT_LAUNCH(T, M)                                                                    \
+  hipLaunchKernelGGL((attn_x3_kernel<T, M>), grid, block, 0, stream, qkv, out, cu, q_rows, \
+                     mask, mask_L)
+  if (terms == 3) {
+    if (mask) ATT_LAUNCH(3, true); else ATT_LAUNCH(3, false);
+  } else {
+    if (mask) ATT_LAUNCH(1, true); else ATT_LAUNCH(1, false);
+  }
+#undef ATT_LAUNCH
+  return hipGetLastError();
+}

@@ -30,6 +30,8 @@ hipError_t ae_launch_gemm_x3g(const float*, const unsigned short*, const unsigne
                               int, int, hipStream_t);
 hipError_t ae_launch_attention_f32(const float*, float*, const int*, const int*, int, int, int,
                                    const uint32_t*, int, hipStream_t);
+hipError_t ae_launch_attention_x3(const float*, float*, const int*, const int*, int, int, int,
+                                  const uint32_t*, int, int, hipStream_t);
 hipError_t ae_launch_compact(const int*, const int*, const int*, int, int, int, int*, int*, int*,
                              hipStream_t);
 hipError_t ae_launch_embed_ln(const int*, const int*, const float*, const float*, const float*,
@@ -288,8 +290,13 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
     {
       const double flop = 0.0;  // attention FLOP are accounted by the caller
       Prof p(e, st, e->prof_kind == AE_KIND_ATTENTION, flop);
-      HIPC(ae_launch_attention_f32(e->qkv, e->ctx, e->cu, last_cls ? e->one : nullptr,
-                                   last_cls ? 1 : max_len, n, heads, mask_bits, L, st));
+      if (e->cfg.precision == AE_PREC_FP32)
+        HIPC(ae_launch_attention_f32(e->qkv, e->ctx, e->cu, last_cls ? e->one : nullptr,
+                                     last_cls ? 1 : max_len, n, heads, mask_bits, L, st));
+      else
+        HIPC(ae_launch_attention_x3(e->qkv, e->ctx, e->cu, last_cls ? e->one : nullptr,
+                                    last_cls ? 1 : max_len, n, heads, mask_bits, L,
+                                    e->cfg.precision == AE_PREC_F32X3 ? 3 : 1, st));
     }
     if (!last_cls) {
       if ((rc = gemm(e, e->ctx, w.wo, w.wo_h, w.wo_l, w.bo, e->x, e->tmp, (int)T, H, H, EPI_BIAS_RESIDUAL,

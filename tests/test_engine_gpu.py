@@ -191,3 +191,40 @@ def test_split_precision_other_heads(gpu):
     np.testing.assert_allclose(p, g["aa_probs"], atol=PROB_TOL, rtol=0)
     p = _score(_engine(2, "pair2", 2, precision="f32x3"), g["clone_ids"])
     np.testing.assert_allclose(p, g["clone_probs"], atol=PROB_TOL, rtol=0)
+
+
+def _pack_mask(m):
+    """bool [n, L, L] -> uint32 [n, L, L/32] (bit k%32 of word k/32 = query may attend key k)."""
+    n, L, _ = m.shape
+    bits = m.reshape(n, L, L // 32, 32).astype(np.uint64)
+    w = (bits << np.arange(32, dtype=np.uint64)).sum(-1)
+    return w.astype(np.uint32)
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", PROB_TOL), ("f32x3", PROB_TOL)])
+def test_dataflow_mask_and_explicit_positions(gpu, precision, tol):
+    """GraphCodeBERT path (GraphCodeBERT/Defect-detection/code/model.py:24-45): explicit position
+    ids and a [L, L] attention mask (bit-packed), pads only at the tail."""
+    rng = np.random.default_rng(17)
+    L, lens = 96, [96, 70, 33]
+    ids = _rand_ids(rng, len(lens), L, lens)
+    pos = np.ones((len(lens), L), dtype=np.int32)
+    m = np.zeros((len(lens), L, L), dtype=bool)
+    for i, ln in enumerate(lens):
+        n_code = ln - ln // 4                       # code tokens then "DFG nodes"
+        pos[i, :n_code] = np.arange(2, n_code + 2)
+        pos[i, n_code:ln] = 0
+        ids[i, n_code:ln - 1] = 3                   # nodes carry <unk>
+        blk = rng.random((ln, ln)) < 0.3
+        blk[np.arange(ln), np.arange(ln)] = True
+        blk[:n_code, :n_code] = True
+        blk[0, :] = True
+        m[i, :ln, :ln] = blk
+    sd = synthetic_sd(0, "sigmoid1")
+    ref = ora.score(sd, ids, "sigmoid1", pos=pos, attn_mask=m)
+    eng = _engine(0, "sigmoid1", precision=precision)
+    lens_np = np.array(lens, np.int32)
+    out = eng.score(torch.from_numpy(ids).cuda(), lens_np, pos=torch.from_numpy(pos).cuda(),
+                    mask_bits=torch.from_numpy(_pack_mask(m)).cuda())
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(out.cpu().numpy(), ref, atol=tol, rtol=0)
