@@ -99,8 +99,8 @@ struct ae_engine {
   int* pinned_cu = nullptr;
   size_t cap_pinned = 0;
   hipEvent_t pinned_ready = nullptr;
-  // GEMM variant for the split-bf16 modes: 1 = LDS-DMA ring (default), 0 = register-staged
-  int gemm_variant = 1;
+  // GEMM variant for the split-bf16 modes: 0 = register-staged (default, faster today), 1 = LDS-DMA ring
+  int gemm_variant = 0;
   // profiling
   int prof_kind = -1;
   std::vector<ProfRec> prof;
