@@ -31,9 +31,12 @@ constexpr int LDS_BYTES = (2 * STAGE > 4 * 32 * OSTRIDE * 4) ? 2 * STAGE : 4 * 3
 __device__ __forceinline__ int kswz(int key, int chunk) { return chunk ^ (key & 7); }
 }  // namespace
 
-template <int TERMS, bool HAS_MASK>
+// PLANES: write the context as packed bf16 planes (hi = bf16(o), lo = bf16(o - hi); layout of
+// gemm_planes.hip) for the O-projection instead of f32 rows in out.
+template <int TERMS, bool HAS_MASK, bool PLANES>
 __global__ __launch_bounds__(256, 2) void attn_x3_kernel(const float* __restrict__ qkv,
                                                          float* __restrict__ out,
+                                                         unsigned short* __restrict__ op,
                                                          const int* __restrict__ cu,
                                                          const int* __restrict__ q_rows,
                                                          const uint32_t* __restrict__ mask,
@@ -225,25 +228,45 @@ __global__ __launch_bounds__(256, 2) void attn_x3_kernel(const float* __restrict
   __syncthreads();
   for (int rr = 0; rr < 32; ++rr) {
     const int qq = qb * QPB + wave * 32 + rr;
-    if (qq < nq)
-      out[(size_t)(start + qq) * AE_HIDDEN + head * AE_HEAD_DIM + lane] = os[rr * OSTRIDE + lane];
+    if (qq < nq) {
+      const size_t o = (size_t)(start + qq) * AE_HIDDEN + head * AE_HEAD_DIM + lane;
+      const float v = os[rr * OSTRIDE + lane];
+      if (PLANES) {  // packed planes (gemm_planes.hip layout), np = 2 for TERMS 3 else 1
+        constexpr int NP = TERMS == 3 ? 2 : 1;
+        const int c = head * AE_HEAD_DIM + lane;
+        unsigned short* dst = op + (size_t)(start + qq) * NP * AE_HIDDEN + (c >> 5) * 32 * NP + (c & 31);
+        const unsigned short h = f2bf(v);
+        dst[0] = h;
+        if (NP == 2) dst[32] = f2bf(v - __builtin_bit_cast(float, (uint32_t)h << 16));
+      } else {
+        out[o] = v;
+      }
+    }
   }
 }
 
-extern "C" hipError_t ae_launch_attention_x3(const float* qkv, float* out, const int* cu,
+extern "C" hipError_t ae_launch_attention_x3(const float* qkv, float* out, unsigned short* op,
+                                             const int* cu,
                                              const int* q_rows, int max_q, int n, int heads,
                                              const uint32_t* mask, int mask_L, int terms,
                                              hipStream_t stream) {
   if (n <= 0 || max_q <= 0) return hipSuccess;
   dim3 grid((max_q + QPB - 1) / QPB, heads, n), block(256);
-#define ATT_LAUNCH(T, M)                                                                    \
-  hipLaunchKernelGGL((attn_x3_kernel<T, M>), grid, block, 0, stream, qkv, out, cu, q_rows, \
-                     mask, mask_L)
-  if (terms == 3) {
-    if (mask) ATT_LAUNCH(3, true); else ATT_LAUNCH(3, false);
-  } else {
-    if (mask) ATT_LAUNCH(1, true); else ATT_LAUNCH(1, false);
+#define ATT_LAUNCH(T, M, P)                                                                  \
+  hipLaunchKernelGGL((attn_x3_kernel<T, M, P>), grid, block, 0, stream, qkv, out, op, cu,     \
+                     q_rows, mask, mask_L)
+#define ATT_MP(T)                                              \
+  if (op) {                                                    \
+    if (mask) ATT_LAUNCH(T, true, true); else ATT_LAUNCH(T, false, true);   \
+  } else {                                                     \
+    if (mask) ATT_LAUNCH(T, true, false); else ATT_LAUNCH(T, false, false); \
   }
+  if (terms == 3) {
+    ATT_MP(3)
+  } else {
+    ATT_MP(1)
+  }
+#undef ATT_MP
 #undef ATT_LAUNCH
   return hipGetLastError();
 }

@@ -6,6 +6,7 @@
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef short shortx8 __attribute__((ext_vector_type(8)));
+typedef unsigned short ushortx4 __attribute__((ext_vector_type(4)));
 
 #define AE_HIDDEN 768
 #define AE_HEAD_DIM 64

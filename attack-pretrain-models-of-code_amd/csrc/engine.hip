@@ -30,14 +30,18 @@ hipError_t ae_launch_gemm_x3g(const float*, const unsigned short*, const unsigne
                               int, int, hipStream_t);
 hipError_t ae_launch_attention_f32(const float*, float*, const int*, const int*, int, int, int,
                                    const uint32_t*, int, hipStream_t);
-hipError_t ae_launch_attention_x3(const float*, float*, const int*, const int*, int, int, int,
-                                  const uint32_t*, int, int, hipStream_t);
+hipError_t ae_launch_attention_x3(const float*, float*, unsigned short*, const int*, const int*,
+                                  int, int, int, const uint32_t*, int, int, hipStream_t);
+hipError_t ae_launch_gemm_packed(const unsigned short*, const unsigned short*, const float*,
+                                 const float*, float*, unsigned short*, int, int, int, int, int,
+                                 hipStream_t);
 hipError_t ae_launch_compact(const int*, const int*, const int*, int, int, int, int*, int*, int*,
                              hipStream_t);
 hipError_t ae_launch_embed_ln(const int*, const int*, const float*, const float*, const float*,
-                              const float*, const float*, float, int, int, float*, hipStream_t);
+                              const float*, const float*, float, int, int, float*, unsigned short*,
+                              int, hipStream_t);
 hipError_t ae_launch_layernorm(const float*, const float*, const float*, float, int, float*,
-                               hipStream_t);
+                               unsigned short*, int, hipStream_t);
 hipError_t ae_launch_gather_cls(const float*, const float*, const int*, int, float*, float*,
                                 hipStream_t);
 hipError_t ae_launch_head_out(const float*, const float*, const float*, int, int, int, float*,
@@ -72,6 +76,8 @@ struct LayerW {
   // split-bf16 planes (AE_PREC_BF16: hi only; AE_PREC_F32X3: hi + lo)
   unsigned short *wqkv_h, *wo_h, *w1_h, *w2_h;
   unsigned short *wqkv_l, *wo_l, *w1_l, *w2_l;
+  // packed planes for gemm_planes.hip (F32X3: [N][K/32][hi 32 | lo 32]; BF16: = the hi plane)
+  unsigned short *wqkv_p, *wo_p, *w1_p, *w2_p;
 };
 
 struct ProfRec {
@@ -93,6 +99,11 @@ struct ae_engine {
   size_t cap_T = 0, cap_n = 0;
   float *x = nullptr, *qkv = nullptr, *ctx = nullptr, *tmp = nullptr, *h1 = nullptr;
   float *xc = nullptr, *cc = nullptr, *tc = nullptr, *hc = nullptr;
+  // packed bf16 activation planes of the split-precision path (gemm_planes.hip layout, np planes):
+  // LN output, attention context, FFN1 output.  Allocated only when `planes` is on.
+  unsigned short *xp = nullptr, *cp = nullptr, *hp = nullptr;
+  bool planes = false;
+  int np = 1;
   int *tok_ids = nullptr, *tok_pos = nullptr, *src_col = nullptr, *cu = nullptr, *one = nullptr;
   float* logits = nullptr;
   size_t cap_logits = 0;
@@ -174,14 +185,34 @@ int upload_split(ae_engine* e, const float* host, size_t n, unsigned short** dst
   return AE_OK;
 }
 
+// Packed planes of gemm_planes.hip for np = 2: row r = K/32 blocks of [hi(32) | lo(32)].
+int upload_packed(ae_engine* e, const float* host, size_t rows, size_t K, unsigned short** dst) {
+  if (K % 32) return fail(AE_EINVAL, "packed planes need K % 32 == 0");
+  std::vector<unsigned short> pk(rows * K * 2);
+  for (size_t r = 0; r < rows; ++r)
+    for (size_t k = 0; k < K; ++k) {
+      const float v = host[r * K + k];
+      const unsigned short h = host_f2bf(v);
+      unsigned short* blk = pk.data() + r * 2 * K + (k / 32) * 64;
+      blk[k % 32] = h;
+      blk[32 + k % 32] = host_f2bf(v - host_bf2f(h));
+    }
+  int rc = dev_alloc(e, (void**)dst, pk.size() * 2);
+  if (rc) return rc;
+  HIPC(hipMemcpy(*dst, pk.data(), pk.size() * 2, hipMemcpyHostToDevice));
+  return AE_OK;
+}
+
 int ensure_workspace(ae_engine* e, size_t T, size_t n) {
   const size_t H = e->cfg.hidden, F = e->cfg.ffn;
   if (T > e->cap_T) {
     size_t nt = T + T / 4 + 128;
     HIPC(hipDeviceSynchronize());
     for (void* p : {(void*)e->x, (void*)e->qkv, (void*)e->ctx, (void*)e->tmp, (void*)e->h1,
-                    (void*)e->tok_ids, (void*)e->tok_pos, (void*)e->src_col})
+                    (void*)e->tok_ids, (void*)e->tok_pos, (void*)e->src_col, (void*)e->xp,
+                    (void*)e->cp, (void*)e->hp})
       dev_free(e, p);
+    e->xp = e->cp = e->hp = nullptr;
     int rc = 0;
     if ((rc = dev_alloc(e, (void**)&e->x, nt * H * 4))) return rc;
     if ((rc = dev_alloc(e, (void**)&e->qkv, nt * 3 * H * 4))) return rc;
@@ -191,6 +222,11 @@ int ensure_workspace(ae_engine* e, size_t T, size_t n) {
     if ((rc = dev_alloc(e, (void**)&e->tok_ids, nt * 4))) return rc;
     if ((rc = dev_alloc(e, (void**)&e->tok_pos, nt * 4))) return rc;
     if ((rc = dev_alloc(e, (void**)&e->src_col, nt * 4))) return rc;
+    if (e->planes) {
+      if ((rc = dev_alloc(e, (void**)&e->xp, nt * H * 2 * e->np))) return rc;
+      if ((rc = dev_alloc(e, (void**)&e->cp, nt * H * 2 * e->np))) return rc;
+      if ((rc = dev_alloc(e, (void**)&e->hp, nt * F * 2 * e->np))) return rc;
+    }
     e->cap_T = nt;
   }
   if (n + 1 > e->cap_n) {
@@ -270,6 +306,17 @@ int gemm(ae_engine* e, const float* A, const float* W, const unsigned short* Wh,
   return AE_OK;
 }
 
+// Packed-plane GEMM of the split-precision path: packed bf16 planes in, f32 (or packed planes for
+// the GELU epilogue) out.
+int gemm_pk(ae_engine* e, const unsigned short* A, const unsigned short* Wp, const float* bias,
+            const float* R, float* C, unsigned short* Cp, int M, int N, int K, int epi,
+            hipStream_t st, bool is_ffn1) {
+  const bool prof = (e->prof_kind == AE_KIND_GEMM_ANY) || (e->prof_kind == AE_KIND_GEMM_FFN1 && is_ffn1);
+  Prof p(e, st, prof, 2.0 * M * N * K);
+  HIPC(ae_launch_gemm_packed(A, Wp, bias, R, C, Cp, M, N, K, epi, e->np, st));
+  return AE_OK;
+}
+
 // Runs the encoder over compacted tokens; on return the last-layer CLS rows are in e->xc
 // (cls_only) or all rows in e->x.
 int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint32_t* mask_bits,
@@ -278,15 +325,21 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
   const float eps = e->cfg.ln_eps;
   HIPC(ae_launch_compact(ids, pos, e->cu, n, L, e->cfg.pad_id, e->tok_ids, e->tok_pos, e->src_col,
                          st));
+  const bool pl = e->planes;
   HIPC(ae_launch_embed_ln(e->tok_ids, e->tok_pos, e->wemb, e->pemb, e->temb, e->eg, e->eb, eps,
-                          (int)T, e->cfg.max_pos, e->x, st));
+                          (int)T, e->cfg.max_pos, e->x, pl ? e->xp : nullptr, e->np, st));
   for (int li = 0; li < NL; ++li) {
     const LayerW& w = e->layers[li];
     const bool last_cls = cls_only && li == NL - 1;
     int rc;
-    if ((rc = gemm(e, e->x, w.wqkv, w.wqkv_h, w.wqkv_l, w.bqkv, nullptr, e->qkv, (int)T, 3 * H, H, EPI_BIAS,
-                   st, false)))
+    if (pl) {
+      if ((rc = gemm_pk(e, e->xp, w.wqkv_p, w.bqkv, nullptr, e->qkv, nullptr, (int)T, 3 * H, H,
+                        EPI_BIAS, st, false)))
+        return rc;
+    } else if ((rc = gemm(e, e->x, w.wqkv, w.wqkv_h, w.wqkv_l, w.bqkv, nullptr, e->qkv, (int)T,
+                          3 * H, H, EPI_BIAS, st, false))) {
       return rc;
+    }
     {
       const double flop = 0.0;  // attention FLOP are accounted by the caller
       Prof p(e, st, e->prof_kind == AE_KIND_ATTENTION, flop);
@@ -294,35 +347,48 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
         HIPC(ae_launch_attention_f32(e->qkv, e->ctx, e->cu, last_cls ? e->one : nullptr,
                                      last_cls ? 1 : max_len, n, heads, mask_bits, L, st));
       else
-        HIPC(ae_launch_attention_x3(e->qkv, e->ctx, e->cu, last_cls ? e->one : nullptr,
+        HIPC(ae_launch_attention_x3(e->qkv, e->ctx, (pl && !last_cls) ? e->cp : nullptr, e->cu,
+                                    last_cls ? e->one : nullptr,
                                     last_cls ? 1 : max_len, n, heads, mask_bits, L,
                                     e->cfg.precision == AE_PREC_F32X3 ? 3 : 1, st));
     }
-    if (!last_cls) {
+    if (!last_cls && pl) {
+      if ((rc = gemm_pk(e, e->cp, w.wo_p, w.bo, e->x, e->tmp, nullptr, (int)T, H, H,
+                        EPI_BIAS_RESIDUAL, st, false)))
+        return rc;
+      HIPC(ae_launch_layernorm(e->tmp, w.ln1g, w.ln1b, eps, (int)T, e->x, e->xp, e->np, st));
+      if ((rc = gemm_pk(e, e->xp, w.w1_p, w.b1, nullptr, nullptr, e->hp, (int)T, F, H,
+                        EPI_BIAS_GELU, st, true)))
+        return rc;
+      if ((rc = gemm_pk(e, e->hp, w.w2_p, w.b2, e->x, e->tmp, nullptr, (int)T, H, F,
+                        EPI_BIAS_RESIDUAL, st, false)))
+        return rc;
+      HIPC(ae_launch_layernorm(e->tmp, w.ln2g, w.ln2b, eps, (int)T, e->x, e->xp, e->np, st));
+    } else if (!last_cls) {
       if ((rc = gemm(e, e->ctx, w.wo, w.wo_h, w.wo_l, w.bo, e->x, e->tmp, (int)T, H, H, EPI_BIAS_RESIDUAL,
                      st, false)))
         return rc;
-      HIPC(ae_launch_layernorm(e->tmp, w.ln1g, w.ln1b, eps, (int)T, e->x, st));
+      HIPC(ae_launch_layernorm(e->tmp, w.ln1g, w.ln1b, eps, (int)T, e->x, nullptr, 0, st));
       if ((rc = gemm(e, e->x, w.w1, w.w1_h, w.w1_l, w.b1, nullptr, e->h1, (int)T, F, H, EPI_BIAS_GELU, st,
                      true)))
         return rc;
       if ((rc = gemm(e, e->h1, w.w2, w.w2_h, w.w2_l, w.b2, e->x, e->tmp, (int)T, H, F, EPI_BIAS_RESIDUAL,
                      st, false)))
         return rc;
-      HIPC(ae_launch_layernorm(e->tmp, w.ln2g, w.ln2b, eps, (int)T, e->x, st));
+      HIPC(ae_launch_layernorm(e->tmp, w.ln2g, w.ln2b, eps, (int)T, e->x, nullptr, 0, st));
     } else {
       HIPC(ae_launch_gather_cls(e->ctx, e->x, e->cu, n, e->cc, e->xc, st));
       if ((rc = gemm(e, e->cc, w.wo, w.wo_h, w.wo_l, w.bo, e->xc, e->tc, n, H, H, EPI_BIAS_RESIDUAL, st,
                      false)))
         return rc;
-      HIPC(ae_launch_layernorm(e->tc, w.ln1g, w.ln1b, eps, n, e->xc, st));
+      HIPC(ae_launch_layernorm(e->tc, w.ln1g, w.ln1b, eps, n, e->xc, nullptr, 0, st));
       if ((rc = gemm(e, e->xc, w.w1, w.w1_h, w.w1_l, w.b1, nullptr, e->hc, n, F, H, EPI_BIAS_GELU, st,
                      false)))
         return rc;
       if ((rc = gemm(e, e->hc, w.w2, w.w2_h, w.w2_l, w.b2, e->xc, e->tc, n, H, F, EPI_BIAS_RESIDUAL, st,
                      false)))
         return rc;
-      HIPC(ae_launch_layernorm(e->tc, w.ln2g, w.ln2b, eps, n, e->xc, st));
+      HIPC(ae_launch_layernorm(e->tc, w.ln2g, w.ln2b, eps, n, e->xc, nullptr, 0, st));
     }
   }
   return AE_OK;
@@ -359,6 +425,11 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
   e->cfg = *cfg;
   e->device = device;
   if (const char* v = std::getenv("AE_GEMM_VARIANT")) e->gemm_variant = std::atoi(v);
+  // split-precision modes run the full-length GEMMs on bf16 activation planes (gemm_planes.hip);
+  // AE_PLANES=0 keeps the f32-activation kernels (A/B runs)
+  e->planes = cfg->precision != AE_PREC_FP32;
+  if (const char* v = std::getenv("AE_PLANES")) e->planes = e->planes && std::atoi(v) != 0;
+  e->np = cfg->precision == AE_PREC_F32X3 ? 2 : 1;
   WeightTable wt;
   for (int i = 0; i < n_weights; ++i) wt.by_name[weights[i].name] = &weights[i];
   const int64_t H = cfg->hidden, F = cfg->ffn, V = cfg->vocab;
@@ -436,6 +507,21 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
         std::string m = g_err;
         ae_destroy(e);
         return fail(rc, m);
+      }
+      if (lo) {
+        if ((rc = upload_packed(e, hw.data(), 3 * H, H, &w.wqkv_p)) ||
+            (rc = upload_packed(e, vo->data, H, H, &w.wo_p)) ||
+            (rc = upload_packed(e, v1->data, F, H, &w.w1_p)) ||
+            (rc = upload_packed(e, v2->data, H, F, &w.w2_p))) {
+          std::string m = g_err;
+          ae_destroy(e);
+          return fail(rc, m);
+        }
+      } else {
+        w.wqkv_p = w.wqkv_h;
+        w.wo_p = w.wo_h;
+        w.w1_p = w.w1_h;
+        w.w2_p = w.w2_h;
       }
     }
   }
@@ -552,7 +638,8 @@ int ae_mlm_topk(ae_engine* e, const int32_t* ids, int32_t L, int32_t k, float* s
   // lm_head: dense -> gelu -> LN -> decoder (tied word embeddings) + bias
   HIPC(ae_launch_gemm_f32(e->x, e->lm_dw, e->lm_db, nullptr, e->tmp, L, H, H, H, H, H,
                           EPI_BIAS_GELU, nullptr, st));
-  HIPC(ae_launch_layernorm(e->tmp, e->lm_lg, e->lm_lb, e->cfg.ln_eps, L, e->ctx, st));
+  HIPC(ae_launch_layernorm(e->tmp, e->lm_lg, e->lm_lb, e->cfg.ln_eps, L, e->ctx, nullptr, 0,
+                           st));
   HIPC(ae_launch_gemm_f32(e->ctx, e->wemb, e->lm_bias, nullptr, e->logits, L, V, H, H, H, V,
                           EPI_BIAS, nullptr, st));
   HIPC(ae_launch_topk(e->logits, L, V, k, scores_out, ids_out, st));

@@ -1,0 +1,297 @@
+// gemm_planes.hip — packed bf16-plane MFMA GEMM of the split-precision encoder
+// (AE_PREC_BF16 / AE_PREC_F32X3).
+//
+// Operands arrive already split into bf16: the weights at engine creation (W = W_hi + W_lo), the
+// activations by the kernel that produced them (LayerNorm, attention, the FFN1 epilogue), so the
+// main loop moves and multiplies nothing but bf16.  Packed layout ("NP planes per 128-B block"):
+//   NP = 2 (f32x3): row = K/32 blocks of 128 B, block b = [hi of k 32b..32b+31 | lo of the same]
+//   NP = 1 (bf16):  row = K bf16 (the hi plane)
+// so one K-tile of a row is always one full 128-B cache line.  With NP = 2 every product is
+//     a·w ≈ a_hi·w_hi + a_hi·w_lo + a_lo·w_hi          (3 bf16 MFMAs, f32 accumulate)
+// from ONE load of the four planes.
+//
+// gfx950 mapping:
+//   * tile 256 x BN (BN = 256: 8 waves as 2 x 4, wave tile 128 x 64; BN = 128: 4 x 2, 64 x 64),
+//     one 512-thread workgroup per CU, LDS 2 x (256 + BN) x 128 B
+//   * operands reach LDS by LDS-DMA (global_load_lds_dwordx4, one wave instruction = 8 rows x
+//     128 B, lane-linear image); the 16-B chunk of row r is XOR-swizzled by (r >> 1) & 7 on the
+//     SOURCE address, so fragment ds_read_b128s of 16 rows hit 16 different bank slots
+//   * a K-tile's fragments are pulled from LDS into registers as soon as the tile has landed;
+//     once every wave holds them (barrier) the stage is refilled with tile k+2, so TWO K-tiles of
+//     DMA (128 KiB per CU) are in flight behind the MFMAs instead of one — the kernel is bound by
+//     how many bytes a CU keeps in flight, not by LDS size
+//   * the MFMAs of the first half of the tile run between the fragment reads and that barrier,
+//     overlapping the LDS reads of the other waves
+//   * DMA issued from inline asm with hand-counted vmcnt (the compiler's wait-count pass would
+//     otherwise drain it before every fragment read); raw s_barrier; XCD-aware tile order
+//   * epilogues: +bias -> f32, +bias+residual -> f32, +bias -> tanh -> f32, +bias -> GELU -> packed
+//     bf16 planes (the FFN2 operand)
+#include "common.h"
+
+#include <cstdlib>
+
+// m0 is written only by dma16 below; nothing else in these kernels reads it
+#pragma clang diagnostic ignored "-Winline-asm"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+enum { PK_EPI_BIAS = 0, PK_EPI_GELU_PACKED = 1, PK_EPI_RES = 2, PK_EPI_TANH = 3 };
+
+namespace {
+constexpr int PK_BM = 256, PK_ROWB = 128;
+
+// One LDS-DMA wave instruction: 64 lanes x 16 B from per-lane global addresses into
+// lds_base + 16 * lane (SALU write of m0 -> LDS-DMA needs one wait state).
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_base) {
+  asm volatile(
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %0, off"
+      :
+      : "v"(gsrc), "s"(lds_base)
+      : "memory", "m0");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else static_assert(N == 0, "unsupported vmcnt");
+}
+}  // namespace
+
+// element offset of (row, col) in a packed [rows][NP*ld] matrix, plane p
+__device__ __forceinline__ size_t pk_index(int row, int col, int ld, int np, int p) {
+  return (size_t)row * np * ld + (size_t)(col >> 5) * 32 * np + 32 * p + (col & 31);
+}
+
+template <int BN, int NP, int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_pk_kernel(
+    const __bf16* __restrict__ A, const __bf16* __restrict__ W, const float* __restrict__ bias,
+    const float* __restrict__ R, float* __restrict__ C, __bf16* __restrict__ Cp, int M, int N,
+    int K) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char pk_smem[];
+  constexpr int WM = BN == 256 ? 2 : 4, WN = 8 / WM;
+  constexpr int TM = PK_BM / WM / 32, TN = BN / WN / 32;
+  constexpr int A_BYTES = PK_BM * PK_ROWB, W_BYTES = BN * PK_ROWB;
+  constexpr int STAGE = A_BYTES + W_BYTES;
+  constexpr int A_DMA = PK_BM / 64, W_DMA = BN / 64;  // DMA instructions per wave per K-tile
+  constexpr int DMA = A_DMA + W_DMA;
+  constexpr int KB = 64 / NP;                          // k per K-tile
+  constexpr int NS = KB / 16;                          // 16-deep MFMA steps per K-tile
+  constexpr int NS0 = NS / 2;                          // steps multiplied before the refill
+
+  const int tiles_n = (N + BN - 1) / BN;
+  const int tiles_m = (M + PK_BM - 1) / PK_BM;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tm = t / tiles_n, tn = t % tiles_n;
+  const int m0 = tm * PK_BM, n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int li = lane & 31, lh = lane >> 5;
+  const size_t lda = (size_t)NP * K;  // packed row length (elements), A and W
+
+  // ---- per-lane DMA sources at K-tile 0 (instruction u covers rows 8 * (DMA_X * wave + u) + lane/8)
+  const char* a_src[A_DMA];
+  const char* w_src[W_DMA];
+#pragma unroll
+  for (int u = 0; u < A_DMA; ++u) {
+    const int r = 8 * (A_DMA * wave + u) + (lane >> 3);
+    const int cs = (lane & 7) ^ ((r >> 1) & 7);
+    const int gr = m0 + r < M ? m0 + r : M - 1;
+    a_src[u] = reinterpret_cast<const char*>(A + gr * lda) + 16 * cs;
+  }
+#pragma unroll
+  for (int u = 0; u < W_DMA; ++u) {
+    const int r = 8 * (W_DMA * wave + u) + (lane >> 3);
+    const int cs = (lane & 7) ^ ((r >> 1) & 7);
+    const int gr = n0 + r < N ? n0 + r : N - 1;
+    w_src[u] = reinterpret_cast<const char*>(W + gr * lda) + 16 * cs;
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)pk_smem;
+  const int nk = K / KB;
+
+  auto issue = [&](int kt) {
+    const int kb = kt * PK_ROWB;  // byte offset of K-tile kt in a packed row
+    const uint32_t st = lds0 + (kt & 1) * STAGE;
+#pragma unroll
+    for (int u = 0; u < A_DMA; ++u) dma16(a_src[u] + kb, st + (A_DMA * wave + u) * 1024);
+#pragma unroll
+    for (int u = 0; u < W_DMA; ++u) dma16(w_src[u] + kb, st + A_BYTES + (W_DMA * wave + u) * 1024);
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  // fragment rows are 32-aligned + li, so the row swizzle is (li >> 1) & 7
+  const int sw = (li >> 1) & 7;
+  const int a_row0 = (wm * (PK_BM / WM) + li) * PK_ROWB;
+  const int w_row0 = A_BYTES + (wn * (BN / WN) + li) * PK_ROWB;
+
+  auto mfma_step = [&](const bf16x8 (&fa)[NP][TM], const bf16x8 (&fw)[NP][TN]) {
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        if (NP == 2) {
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][a], fw[0][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][a], fw[1][b], acc[a][b], 0, 0, 0);
+        }
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][a], fw[0][b], acc[a][b], 0, 0, 0);
+      }
+  };
+
+  issue(0);
+  if (nk > 1) issue(1);
+  for (int kt = 0; kt < nk; ++kt) {
+    // tile kt landed (this wave's DMA; kt+1 may still be in flight), then visible to all waves
+    if (kt + 1 < nk) wait_vm<DMA>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned char* st = pk_smem + (kt & 1) * STAGE;
+    bf16x8 fa[NS][NP][TM], fw[NS][NP][TN];
+    auto read_step = [&](int s) {
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const int coff = 16 * ((4 * p + 2 * s + lh) ^ sw);
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+          fw[s][p][b] = *reinterpret_cast<const bf16x8*>(st + w_row0 + b * 32 * PK_ROWB + coff);
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+          fa[s][p][a] = *reinterpret_cast<const bf16x8*>(st + a_row0 + a * 32 * PK_ROWB + coff);
+      }
+    };
+#pragma unroll
+    for (int s = 0; s < NS0; ++s) read_step(s);
+    __builtin_amdgcn_sched_barrier(0);
+    // first-half MFMAs interleaved with the second-half fragment reads (<= 15 LDS ops in flight)
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = NS0; s < NS; ++s) read_step(s);
+#pragma unroll
+    for (int s = 0; s < NS0; ++s) mfma_step(fa[s], fw[s]);
+    {
+      constexpr int RD1 = (NS - NS0) * NP * (TM + TN);
+      constexpr int MF0 = NS0 * (NP == 2 ? 3 : 1) * TM * TN;
+      constexpr int PER = MF0 / RD1 > 0 ? MF0 / RD1 : 1;
+#pragma unroll
+      for (int i = 0; i < RD1; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, PER, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);    // DS read
+      }
+      if (MF0 > PER * RD1) __builtin_amdgcn_sched_group_barrier(0x008, MF0 - PER * RD1, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    // every wave holds tile kt in registers: refill its stage with tile kt+2
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 2 < nk) issue(kt + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = NS0; s < NS; ++s) mfma_step(fa[s], fw[s]);
+    __builtin_amdgcn_s_setprio(0);
+  }
+
+  // ---- epilogue straight from the accumulators: lane li owns column li of each 32x32 tile
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int col = n0 + wn * (BN / WN) + b * 32 + li;
+    if (col >= N) continue;
+    const float bv = bias[col];
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * (PK_BM / WM) + a * 32 + mfma32_row(r, lh);
+        if (row >= M) continue;
+        float v = acc[a][b][r] + bv;
+        if (EPI == PK_EPI_GELU_PACKED) {
+          v = gelu_erf(v);
+          const __bf16 h = (__bf16)v;
+          Cp[pk_index(row, col, N, NP, 0)] = h;
+          if (NP == 2) Cp[pk_index(row, col, N, NP, 1)] = (__bf16)(v - (float)h);
+        } else {
+          const size_t o = (size_t)row * N + col;
+          if (EPI == PK_EPI_TANH) v = tanhf(v);
+          if (EPI == PK_EPI_RES) v += R[o];
+          C[o] = v;
+        }
+      }
+    }
+  }
+}
+
+namespace {
+template <int BN, int NP, int EPI>
+hipError_t pk_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R, float* C,
+                     __bf16* Cp, int M, int N, int K, hipStream_t st) {
+  constexpr int lds = 2 * (PK_BM + BN) * PK_ROWB;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_pk_kernel<BN, NP, EPI>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int tiles = ((M + PK_BM - 1) / PK_BM) * ((N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_pk_kernel<BN, NP, EPI>), dim3(tiles), dim3(512), lds, st, A, W, bias,
+                     R, C, Cp, M, N, K);
+  return hipGetLastError();
+}
+
+template <int BN, int NP>
+hipError_t pk_epi(int epi, const __bf16* A, const __bf16* W, const float* bias, const float* R,
+                  float* C, __bf16* Cp, int M, int N, int K, hipStream_t st) {
+  switch (epi) {
+    case PK_EPI_BIAS: return pk_launch<BN, NP, PK_EPI_BIAS>(A, W, bias, R, C, Cp, M, N, K, st);
+    case PK_EPI_GELU_PACKED:
+      return pk_launch<BN, NP, PK_EPI_GELU_PACKED>(A, W, bias, R, C, Cp, M, N, K, st);
+    case PK_EPI_RES: return pk_launch<BN, NP, PK_EPI_RES>(A, W, bias, R, C, Cp, M, N, K, st);
+    default: return pk_launch<BN, NP, PK_EPI_TANH>(A, W, bias, R, C, Cp, M, N, K, st);
+  }
+}
+
+// Tile width per problem: wall time ~ rounds of 256 CUs x per-tile time (256x128 ~0.55 of 256^2)
+int pick_bn(int M, int N) {
+  const char* fv = std::getenv("AE_PL_BN");  // A/B override, read per call (tests flip it)
+  const int force = fv ? std::atoi(fv) : 0;
+  if (force == 128 || force == 256) return force;
+  const long tm = (M + PK_BM - 1) / PK_BM;
+  const long t256 = tm * ((N + 255) / 256), t128 = tm * ((N + 127) / 128);
+  const double c256 = (double)((t256 + 255) / 256), c128 = 0.55 * (double)((t128 + 255) / 256);
+  return c128 < c256 ? 128 : 256;
+}
+}  // namespace
+
+// C = A·W^T (+epilogue) over packed bf16 planes.  A: [M][np*K], W: [N][np*K] packed (see top);
+// f32 output C [M][N] or packed output planes Cp [M][np*N] (GELU epilogue).  np: 2 = split-bf16
+// (f32-class), 1 = plain bf16.  Requires K % 64 == 0.
+extern "C" hipError_t ae_launch_gemm_packed(const unsigned short* A, const unsigned short* W,
+                                            const float* bias, const float* R, float* C,
+                                            unsigned short* Cp, int M, int N, int K, int epi,
+                                            int np, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  if (K % 64 != 0 || (np != 1 && np != 2) || N <= 0) return hipErrorInvalidValue;
+  auto bf = [](const unsigned short* p) { return reinterpret_cast<const __bf16*>(p); };
+  auto bfm = [](unsigned short* p) { return reinterpret_cast<__bf16*>(p); };
+  const int bn = pick_bn(M, N);
+  if (np == 2) {
+    if (bn == 256) return pk_epi<256, 2>(epi, bf(A), bf(W), bias, R, C, bfm(Cp), M, N, K, st);
+    return pk_epi<128, 2>(epi, bf(A), bf(W), bias, R, C, bfm(Cp), M, N, K, st);
+  }
+  if (bn == 256) return pk_epi<256, 1>(epi, bf(A), bf(W), bias, R, C, bfm(Cp), M, N, K, st);
+  return pk_epi<128, 1>(epi, bf(A), bf(W), bias, R, C, bfm(Cp), M, N, K, st);
+}

@@ -52,7 +52,9 @@ __global__ __launch_bounds__(256) void compact_kernel(const int* __restrict__ id
 
 __device__ __forceinline__ void ln_row_store(float (&v)[12], const float* __restrict__ g,
                                              const float* __restrict__ b, float eps,
-                                             float* __restrict__ out, int lane) {
+                                             float* __restrict__ out, int lane,
+                                             unsigned short* __restrict__ op = nullptr,
+                                             int np = 0) {
   float sum = 0.f;
 #pragma unroll
   for (int i = 0; i < 12; ++i) sum += v[i];
@@ -74,6 +76,17 @@ __device__ __forceinline__ void ln_row_store(float (&v)[12], const float* __rest
 #pragma unroll
     for (int e = 0; e < 4; ++e) o[e] = (v[4 * c + e] - mean) * rstd * gg[e] + bb[e];
     *reinterpret_cast<floatx4*>(out + col) = o;
+    if (op) {  // packed bf16 planes for the split-precision GEMMs (gemm_planes.hip): o = hi + lo
+      ushortx4 h, l;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        h[e] = f2bf(o[e]);
+        l[e] = f2bf(o[e] - __builtin_bit_cast(float, (uint32_t)h[e] << 16));
+      }
+      unsigned short* dst = op + (col >> 5) * 32 * np + (col & 31);
+      *reinterpret_cast<ushortx4*>(dst) = h;
+      if (np == 2) *reinterpret_cast<ushortx4*>(dst + 32) = l;
+    }
   }
 }
 
@@ -83,7 +96,8 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(
     const int* __restrict__ tok_ids, const int* __restrict__ tok_pos,
     const float* __restrict__ wemb, const float* __restrict__ pemb,
     const float* __restrict__ temb, const float* __restrict__ g, const float* __restrict__ b,
-    float eps, int T, int max_pos, float* __restrict__ x) {
+    float eps, int T, int max_pos, float* __restrict__ x, unsigned short* __restrict__ xp,
+    int np) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= T) return;
@@ -102,14 +116,16 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[4 * c + e] = (a[e] + t[e]) + bb[e];
   }
-  ln_row_store(v, g, b, eps, x + (size_t)row * AE_HIDDEN, lane);
+  const size_t o = (size_t)row * AE_HIDDEN;
+  ln_row_store(v, g, b, eps, x + o, lane, xp ? xp + o * np : nullptr, np);
 }
 
 // In-place (or out-of-place) LayerNorm of T rows.
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ in,
                                                         const float* __restrict__ g,
                                                         const float* __restrict__ b, float eps,
-                                                        int T, float* __restrict__ out) {
+                                                        int T, float* __restrict__ out,
+                                                        unsigned short* __restrict__ op, int np) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= T) return;
@@ -121,7 +137,8 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[4 * c + e] = a[e];
   }
-  ln_row_store(v, g, b, eps, out + (size_t)row * AE_HIDDEN, lane);
+  const size_t o = (size_t)row * AE_HIDDEN;
+  ln_row_store(v, g, b, eps, out + o, lane, op ? op + o * np : nullptr, np);
 }
 
 // Gather the first (CLS) row of every sequence from two [T,768] matrices into compact [n,768].
@@ -233,16 +250,18 @@ hipError_t ae_launch_compact(const int* ids, const int* pos, const int* cu, int 
 }
 hipError_t ae_launch_embed_ln(const int* tok_ids, const int* tok_pos, const float* wemb,
                               const float* pemb, const float* temb, const float* g, const float* b,
-                              float eps, int T, int max_pos, float* x, hipStream_t st) {
+                              float eps, int T, int max_pos, float* x, unsigned short* xp,
+                              int np, hipStream_t st) {
   if (T <= 0) return hipSuccess;
   hipLaunchKernelGGL(embed_ln_kernel, dim3((T + 3) / 4), dim3(256), 0, st, tok_ids, tok_pos, wemb,
-                     pemb, temb, g, b, eps, T, max_pos, x);
+                     pemb, temb, g, b, eps, T, max_pos, x, xp, np);
   return hipGetLastError();
 }
 hipError_t ae_launch_layernorm(const float* in, const float* g, const float* b, float eps, int T,
-                               float* out, hipStream_t st) {
+                               float* out, unsigned short* op, int np, hipStream_t st) {
   if (T <= 0) return hipSuccess;
-  hipLaunchKernelGGL(layernorm_kernel, dim3((T + 3) / 4), dim3(256), 0, st, in, g, b, eps, T, out);
+  hipLaunchKernelGGL(layernorm_kernel, dim3((T + 3) / 4), dim3(256), 0, st, in, g, b, eps, T, out,
+                     op, np);
   return hipGetLastError();
 }
 hipError_t ae_launch_gather_cls(const float* a, const float* b, const int* cu, int n, float* ac,

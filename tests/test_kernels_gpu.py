@@ -1,0 +1,102 @@
+"""GPU unit tests of individual kernels called through their extern "C" launchers in
+lib/libalert_engine.so (not part of the public C-ABI; the engine tests cover them end to end).
+
+Packed-plane GEMM (gemm_planes.hip): C = A·W^T over packed bf16 planes must equal the float64 sum
+of the split products A_hi·W_hi + A_hi·W_lo + A_lo·W_hi (f32 accumulation: |Δ| ≤ 1e-5·Σ|a||w|), for
+ragged M, both tile widths, both plane counts and every epilogue."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    from apmc_amd.engine import load_library
+    lib = load_library()
+    vp, i32 = ctypes.c_void_p, ctypes.c_int32
+    lib.ae_launch_gemm_packed.argtypes = [vp] * 6 + [i32] * 5 + [vp]
+    lib.ae_launch_gemm_packed.restype = ctypes.c_int
+    return lib
+
+
+def _split(x):
+    """f32 tensor -> (hi, lo) bf16 planes."""
+    hi = x.to(torch.bfloat16)
+    lo = (x - hi.float()).to(torch.bfloat16)
+    return hi, lo
+
+
+def _pack(hi, lo, np_):
+    """[R, K] planes -> packed [R, np*K] (np = 2: K/32 blocks of [hi 32 | lo 32])."""
+    if np_ == 1:
+        return hi.contiguous()
+    R, K = hi.shape
+    return torch.stack([hi.reshape(R, K // 32, 32), lo.reshape(R, K // 32, 32)], 2).reshape(R, 2 * K)
+
+
+def _unpack(p, np_, N):
+    R = p.shape[0]
+    if np_ == 1:
+        return p.double()
+    b = p.reshape(R, N // 32, 2, 32).double()
+    return (b[:, :, 0] + b[:, :, 1]).reshape(R, N)
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(None)
+
+
+@pytest.mark.parametrize("M,N,K,np_,epi,bn", [
+    (300, 256, 128, 2, 0, "256"),
+    (512, 768, 768, 2, 2, "128"),
+    (257, 512, 192, 2, 1, "256"),
+    (1000, 384, 64, 1, 3, "128"),
+    (700, 256, 256, 1, 1, "256"),
+    (64, 2304, 768, 2, 0, ""),
+])
+def test_gemm_packed_matches_split_products(gpu, monkeypatch, M, N, K, np_, epi, bn):
+    if bn:
+        monkeypatch.setenv("AE_PL_BN", bn)
+    lib = _lib()
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g) * 0.7
+    W = torch.randn(N, K, generator=g) * 0.05
+    bias = torch.randn(N, generator=g)
+    R = torch.randn(M, N, generator=g)
+    Ah, Al = _split(A)
+    Wh, Wl = _split(W)
+    ref = Ah.double() @ Wh.double().T
+    if np_ == 2:
+        ref = ref + Ah.double() @ Wl.double().T + Al.double() @ Wh.double().T
+    ref = ref + bias.double()
+    scale = A.abs().double() @ W.abs().double().T
+    if epi == 1:
+        ref = torch.nn.functional.gelu(ref)
+    elif epi == 2:
+        ref = ref + R.double()
+    elif epi == 3:
+        ref = torch.tanh(ref)
+    dA = _pack(Ah, Al, np_).cuda()
+    dW = _pack(Wh, Wl, np_).cuda()
+    db, dR = bias.cuda(), R.cuda()
+    C = torch.full((M, N), float("nan"), device="cuda")
+    Cp = torch.zeros((M, np_ * N), dtype=torch.bfloat16, device="cuda")
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    rc = lib.ae_launch_gemm_packed(_p(dA), _p(dW), _p(db), _p(dR), _p(C), _p(Cp), M, N, K, epi,
+                                   np_, st)
+    assert rc == 0
+    torch.cuda.synchronize()
+    if epi == 1:
+        got = _unpack(Cp.cpu(), np_, N)
+        # the packed planes hold the GELU output to ~2^-17 relative (np 2) / 2^-9 (np 1)
+        rel = 2e-5 if np_ == 2 else 5e-3
+        tol = 1e-5 * scale + rel * ref.abs() + 1e-6
+    else:
+        got = C.double().cpu()
+        tol = 1e-5 * scale + 1e-6
+    assert torch.isfinite(got).all()
+    err = (got - ref).abs()
+    assert (err <= tol).all(), float((err - tol).max())
