@@ -70,7 +70,7 @@ template <int BN, int NP, int EPI>
 __global__ __launch_bounds__(512, 1) void gemm_pk_kernel(
     const __bf16* __restrict__ A, const __bf16* __restrict__ W, const float* __restrict__ bias,
     const float* __restrict__ R, float* __restrict__ C, __bf16* __restrict__ Cp, int M, int N,
-    int K) {
+    int K, int group_m, int diag) {
   extern __shared__ __attribute__((aligned(16))) unsigned char pk_smem[];
   constexpr int WM = BN == 256 ? 2 : 4, WN = 8 / WM;
   constexpr int TM = PK_BM / WM / 32, TN = BN / WN / 32;
@@ -84,8 +84,13 @@ __global__ __launch_bounds__(512, 1) void gemm_pk_kernel(
 
   const int tiles_n = (N + BN - 1) / BN;
   const int tiles_m = (M + PK_BM - 1) / PK_BM;
+  // XCD-contiguous tile order, then grouped: group_m M-tiles sweep the N-tiles together, so the
+  // ~32 tiles an XCD runs at once share both their A rows and their W rows in its L2
   const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tm = t / tiles_n, tn = t % tiles_n;
+  const int per_group = group_m * tiles_n;
+  const int g = t / per_group, first_m = g * group_m;
+  const int gsize = min(tiles_m - first_m, group_m);
+  const int tm = first_m + (t - g * per_group) % gsize, tn = (t - g * per_group) / gsize;
   const int m0 = tm * PK_BM, n0 = tn * BN;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -112,7 +117,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pk_kernel(
     w_src[u] = reinterpret_cast<const char*>(W + gr * lda) + 16 * cs;
   }
   const uint32_t lds0 = (uint32_t)(uintptr_t)pk_smem;
-  const int nk = K / KB;
+  const int nk = diag == 6 ? 0 : K / KB;
 
   auto issue = [&](int kt) {
     const int kb = kt * PK_ROWB;  // byte offset of K-tile kt in a packed row
@@ -149,16 +154,16 @@ __global__ __launch_bounds__(512, 1) void gemm_pk_kernel(
       }
   };
 
-  issue(0);
+  bf16x8 fa[NS][NP][TM], fw[NS][NP][TN];
+  if (nk > 0) issue(0);
   if (nk > 1) issue(1);
   for (int kt = 0; kt < nk; ++kt) {
     // tile kt landed (this wave's DMA; kt+1 may still be in flight), then visible to all waves
     if (kt + 1 < nk) wait_vm<DMA>();
     else wait_vm<0>();
-    __builtin_amdgcn_s_barrier();
+    if (diag != 3) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     const unsigned char* st = pk_smem + (kt & 1) * STAGE;
-    bf16x8 fa[NS][NP][TM], fw[NS][NP][TN];
     auto read_step = [&](int s) {
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
@@ -172,14 +177,17 @@ __global__ __launch_bounds__(512, 1) void gemm_pk_kernel(
       }
     };
 #pragma unroll
-    for (int s = 0; s < NS0; ++s) read_step(s);
+    for (int s = 0; s < NS0; ++s)
+      if (diag != 4 || kt == 0) read_step(s);
     __builtin_amdgcn_sched_barrier(0);
     // first-half MFMAs interleaved with the second-half fragment reads (<= 15 LDS ops in flight)
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int s = NS0; s < NS; ++s) read_step(s);
+    for (int s = NS0; s < NS; ++s)
+      if (diag != 4 || kt == 0) read_step(s);
 #pragma unroll
-    for (int s = 0; s < NS0; ++s) mfma_step(fa[s], fw[s]);
+    for (int s = 0; s < NS0; ++s)
+      if (diag != 5) mfma_step(fa[s], fw[s]);
     {
       constexpr int RD1 = (NS - NS0) * NP * (TM + TN);
       constexpr int MF0 = NS0 * (NP == 2 ? 3 : 1) * TM * TN;
@@ -195,41 +203,78 @@ __global__ __launch_bounds__(512, 1) void gemm_pk_kernel(
     __builtin_amdgcn_sched_barrier(0);
     // every wave holds tile kt in registers: refill its stage with tile kt+2
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if (diag != 2 && diag != 3) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (kt + 2 < nk) issue(kt + 2);
+    if (kt + 2 < nk && diag != 1) issue(kt + 2);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int s = NS0; s < NS; ++s) mfma_step(fa[s], fw[s]);
+    for (int s = NS0; s < NS; ++s)
+      if (diag != 5) mfma_step(fa[s], fw[s]);
     __builtin_amdgcn_s_setprio(0);
   }
 
-  // ---- epilogue straight from the accumulators: lane li owns column li of each 32x32 tile
+  // ---- epilogue through LDS: each 32x32 accumulator tile is transposed through a private
+  // 32 x 33-float LDS slab so that every global access is a 16-byte-per-lane row segment
+  // (4 floats of C / R, or 8 hi + 8 lo bf16 of a packed block) instead of one element per lane
+  __syncthreads();  // the stages are reused as scratch: every wave has finished the main loop
+  float* slab = reinterpret_cast<float*>(pk_smem) + wave * 32 * 33;
 #pragma unroll
   for (int b = 0; b < TN; ++b) {
-    const int col = n0 + wn * (BN / WN) + b * 32 + li;
-    if (col >= N) continue;
-    const float bv = bias[col];
+    const int cb = n0 + wn * (BN / WN) + b * 32;  // first column of the tile (N % 32 == 0)
 #pragma unroll
     for (int a = 0; a < TM; ++a) {
+      const int rb = m0 + wm * (PK_BM / WM) + a * 32;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * (PK_BM / WM) + a * 32 + mfma32_row(r, lh);
-        if (row >= M) continue;
-        float v = acc[a][b][r] + bv;
+      for (int r = 0; r < 16; ++r) slab[mfma32_row(r, lh) * 33 + li] = acc[a][b][r];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slab is written before it is read
+      if (cb < N) {
         if (EPI == PK_EPI_GELU_PACKED) {
-          v = gelu_erf(v);
-          const __bf16 h = (__bf16)v;
-          Cp[pk_index(row, col, N, NP, 0)] = h;
-          if (NP == 2) Cp[pk_index(row, col, N, NP, 1)] = (__bf16)(v - (float)h);
+          // lane -> row (lane >> 2) + 16 pass, 8 columns c8 = 8 * (lane & 3)
+          const int c8 = 8 * (lane & 3);
+          floatx4 b0 = *reinterpret_cast<const floatx4*>(bias + cb + c8);
+          floatx4 b1 = *reinterpret_cast<const floatx4*>(bias + cb + c8 + 4);
+#pragma unroll
+          for (int pass = 0; pass < 2; ++pass) {
+            const int rr = 16 * pass + (lane >> 2);
+            const int row = rb + rr;
+            bf16x8 h, l;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float v = gelu_erf(slab[rr * 33 + c8 + e] + (e < 4 ? b0[e] : b1[e - 4]));
+              const __bf16 hv = (__bf16)v;
+              h[e] = hv;
+              l[e] = (__bf16)(v - (float)hv);
+            }
+            if (row < M) {
+              __bf16* dst = Cp + (size_t)row * NP * N + (size_t)(cb >> 5) * 32 * NP + c8;
+              *reinterpret_cast<bf16x8*>(dst) = h;
+              if (NP == 2) *reinterpret_cast<bf16x8*>(dst + 32) = l;
+            }
+          }
         } else {
-          const size_t o = (size_t)row * N + col;
-          if (EPI == PK_EPI_TANH) v = tanhf(v);
-          if (EPI == PK_EPI_RES) v += R[o];
-          C[o] = v;
+          // lane -> row (lane >> 3) + 8 pass, 4 columns c4 = 4 * (lane & 7)
+          const int c4 = 4 * (lane & 7);
+          const floatx4 bv = *reinterpret_cast<const floatx4*>(bias + cb + c4);
+#pragma unroll
+          for (int pass = 0; pass < 4; ++pass) {
+            const int rr = 8 * pass + (lane >> 3);
+            const int row = rb + rr;
+            if (row < M) {
+              const size_t o = (size_t)row * N + cb + c4;
+              floatx4 v;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = slab[rr * 33 + c4 + e] + bv[e];
+              if (EPI == PK_EPI_TANH)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
+              if (EPI == PK_EPI_RES) v += *reinterpret_cast<const floatx4*>(R + o);
+              *reinterpret_cast<floatx4*>(C + o) = v;
+            }
+          }
         }
       }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slab reads done before the next tile overwrites it
     }
   }
 }
@@ -247,8 +292,15 @@ hipError_t pk_launch(const __bf16* A, const __bf16* W, const float* bias, const 
     attr_set = true;
   }
   const int tiles = ((M + PK_BM - 1) / PK_BM) * ((N + BN - 1) / BN);
+  const char* gv = std::getenv("AE_PK_GROUP");
+  const int group_m = gv && std::atoi(gv) > 0 ? std::atoi(gv) : 8;
+  // AE_PK_DIAG (timing experiments only, results WRONG): 1 = no refill DMA after the first two
+  // K-tiles, 2 = no post-read barrier, 3 = no barriers at all, 4 = no fragment reads after the
+  // first K-tile, 5 = no MFMAs, 6 = epilogue only
+  const char* dv = std::getenv("AE_PK_DIAG");
+  const int diag = dv ? std::atoi(dv) : 0;
   hipLaunchKernelGGL((gemm_pk_kernel<BN, NP, EPI>), dim3(tiles), dim3(512), lds, st, A, W, bias,
-                     R, C, Cp, M, N, K);
+                     R, C, Cp, M, N, K, group_m, diag);
   return hipGetLastError();
 }
 
@@ -278,13 +330,13 @@ int pick_bn(int M, int N) {
 
 // C = A·W^T (+epilogue) over packed bf16 planes.  A: [M][np*K], W: [N][np*K] packed (see top);
 // f32 output C [M][N] or packed output planes Cp [M][np*N] (GELU epilogue).  np: 2 = split-bf16
-// (f32-class), 1 = plain bf16.  Requires K % 64 == 0.
+// (f32-class), 1 = plain bf16.  Requires K % 64 == 0 and N % 32 == 0.
 extern "C" hipError_t ae_launch_gemm_packed(const unsigned short* A, const unsigned short* W,
                                             const float* bias, const float* R, float* C,
                                             unsigned short* Cp, int M, int N, int K, int epi,
                                             int np, hipStream_t st) {
   if (M <= 0) return hipSuccess;
-  if (K % 64 != 0 || (np != 1 && np != 2) || N <= 0) return hipErrorInvalidValue;
+  if (K % 64 != 0 || N % 32 != 0 || (np != 1 && np != 2) || N <= 0) return hipErrorInvalidValue;
   auto bf = [](const unsigned short* p) { return reinterpret_cast<const __bf16*>(p); };
   auto bfm = [](unsigned short* p) { return reinterpret_cast<__bf16*>(p); };
   const int bn = pick_bn(M, N);

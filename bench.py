@@ -38,13 +38,14 @@ def flops_per_query(L, C=1):
     return 12 * (L * per_tok + 4 * L * L * 768) + 2 * 768 * 768 + 2 * 768 * C
 
 
-def pmc_traffic_per_launch():
-    """HBM bytes per FFN1 launch from the committed rocprofv3 PMC summary (profiles/*pmc*.json),
-    or None."""
+def pmc_traffic_per_launch(precision):
+    """HBM bytes per FFN1 launch of this precision's kernel from the committed rocprofv3 PMC
+    summary (profiles/*pmc_ffn1.json, newest first), or None."""
     for f in sorted(glob.glob(str(ROOT / "profiles" / "*pmc*ffn1*.json")), reverse=True):
         try:
             d = json.load(open(f))
-            return float(d["hbm_bytes_per_launch"])
+            if d.get("precision", "fp32") == precision:
+                return float(d["hbm_bytes_per_launch"])
         except Exception:
             continue
     return None
@@ -73,7 +74,7 @@ def cpu_baseline(L, seconds, threads):
                       f"oracle/roberta_cpu.py fp32 eager, torch threads={threads}"}
 
 
-def attack_leg(dev, seconds, rank, world):
+def attack_leg(dev, seconds, rank, world, precision):
     """End-to-end config-2 workload: greedy -> GA attack (gi_attack.py --use_ga) over the
     test_subs_0_400 fixture, examples pulled in order from a shared queue until the time budget is
     spent; victim queries/s and attacked examples/min over the whole job."""
@@ -82,7 +83,8 @@ def attack_leg(dev, seconds, rank, world):
     from apmc_amd.weights import synthetic_state_dict
 
     codes, subs, labels = load_fixture(ROOT / "data" / "devign" / "test_subs_0_400.jsonl")
-    model = Model(synthetic_state_dict(seed=0, head="sigmoid1"), task="devign", device=dev.index)
+    model = Model(synthetic_state_dict(seed=0, head="sigmoid1"), task="devign",
+                  precision=precision, device=dev.index)
     args = AttackArgs(block_size=512, eval_batch_size=64, seed=123456, rng="per_example")
     from apmc_amd.dist import DynamicQueue
 
@@ -109,6 +111,7 @@ def attack_leg(dev, seconds, rank, world):
     ga = sum(r["attack_type"] == "GA" for r in out["records"])
     return {"workload": "CodeBERT Devign greedy->GA attack (gi_attack --use_ga), "
                         "test_subs_0_400.jsonl in order, block 512, eval_batch_size 64",
+            "precision": precision,
             "examples": int(ex), "correctly_classified": int(cnt), "successes": int(suc),
             "success_rate": round(suc / cnt, 4) if cnt else None, "victim_queries": int(q),
             "wall_s": round(wall, 2), "victim_queries_per_s": round(q / wall, 2),
@@ -124,7 +127,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--seq", type=int, default=512)
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "f32x3", "bf16"])
+    ap.add_argument("--precision", default="f32x3", choices=["fp32", "f32x3", "bf16"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--attack-seconds", type=float, default=90.0,
@@ -213,7 +216,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": {"fp32": "fp32", "f32x3": "fp32 (split-bf16 x3 MFMA, f32 accumulate)",
+        "dtype": {"fp32": "fp32", "f32x3": "f32x3 (fp32 operands as bf16 hi+lo, 3 bf16 MFMAs "
+                                           "per product, f32 accumulate; |dp| vs fp32 <= 1e-4)",
                   "bf16": "bf16 (f32 accumulate / residual)"}[args.precision],
         "precision_mode": args.precision,
         "max_abs_dprob_vs_fp32_mode": parity,
@@ -223,13 +227,15 @@ def main():
                    "global_batch": B * world, "seq_len": L, "parallelism": f"dp{world} (example shards)"},
         "roofline": {
             "bound": "mfma",
-            "kernel": ("gemm_f32_nt_kernel<EPI_BIAS_GELU>" if args.precision == "fp32" else
-                       "gemm_x3_kernel<256,256,...,EPI_GELU>") + " (FFN1 [T,768]x[768,3072])",
+            "kernel": {"fp32": "gemm_f32_nt_kernel<EPI_BIAS_GELU>",
+                       "f32x3": "gemm_pk_kernel<256, 2, EPI_GELU_PACKED>",
+                       "bf16": "gemm_pk_kernel<256, 1, EPI_GELU_PACKED>"}[args.precision]
+                      + " (FFN1 [T,768]x[768,3072])",
             "achieved": round(achieved, 3) if achieved else None,
             "peak": peak,
             "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4) if achieved else None,
-            "traffic": pmc_traffic_per_launch(),
+            "traffic": pmc_traffic_per_launch(args.precision),
             "launches": k_n,
             "avg_launch_us": round(per_launch_s * 1e6, 2),
             "flop_per_launch": (k_flop / k_n) if k_n else None,
@@ -239,7 +245,7 @@ def main():
         "probs_checksum": float(np.round(probs.astype(np.float64).sum(), 6)),
     }
     if args.attack_seconds > 0:
-        res["attack"] = attack_leg(dev, args.attack_seconds, rank, world)
+        res["attack"] = attack_leg(dev, args.attack_seconds, rank, world, args.precision)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
         res["cpu_baseline"] = cpu_baseline(L, args.cpu_seconds, threads)

@@ -7,7 +7,7 @@ FETCH_SIZE reports half the bytes of wide coalesced streaming reads, so read byt
 FETCH_SIZE x 1024; WRITE_SIZE is exact for 16-B-per-lane stores (our epilogue stores are 4-B
 per lane, so WRITE_SIZE is reported uncorrected and flagged uncalibrated).
 
-Usage: python tools/summarize_profile.py gpurun_out/prof_r1 r1
+Usage: python tools/summarize_profile.py gpurun_out/prof_r1 r1 [fp32|f32x3|bf16]
 """
 import csv
 import json
@@ -17,9 +17,16 @@ import statistics
 import sys
 
 ROOT = pathlib.Path(__file__).resolve().parents[1]
-FFN1 = "gemm_f32_nt_kernel<1>"
 T, H, F = 64 * 512, 768, 3072
-ALGO_BYTES = 4 * (T * H + F * H + F + T * F)  # A + W + bias read, C written (fp32)
+# FFN1 kernel per precision: (name substring, min grid size in threads, bytes per operand element)
+KERNELS = {
+    "fp32": ("gemm_f32_nt_kernel<1>", 256 * 24 * 256, 4),
+    "f32x3": ("gemm_pk_kernel<256, 2, 1>", 128 * 12 * 512, 4),   # packed hi+lo = 4 B / element
+    "bf16": ("gemm_pk_kernel<256, 1, 1>", 128 * 12 * 512, 2),
+}
+PREC = sys.argv[3] if len(sys.argv) > 3 else "fp32"
+FFN1, MIN_GRID, EB = KERNELS[PREC]
+ALGO_BYTES = EB * (T * H + F * H + T * F) + 4 * F  # A + W read, C written, f32 bias
 
 
 def ffn1_rows(path, counter):
@@ -28,7 +35,7 @@ def ffn1_rows(path, counter):
         for r in csv.DictReader(f):
             if FFN1 in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 # full-size launches only (grid = 256 rows/tile-blocks x 24 col tiles x 256 thr)
-                if int(r["Grid_Size"]) >= 256 * 24 * 256:
+                if int(r["Grid_Size"]) >= MIN_GRID:
                     vals.append(float(r["Counter_Value"]))
     return vals
 
@@ -37,7 +44,7 @@ def durations(path):
     out = []
     with open(path) as f:
         for r in csv.DictReader(f):
-            if FFN1 in r["Kernel_Name"] and int(r["Grid_Size_X"]) >= 256 * 24 * 256:
+            if FFN1 in r["Kernel_Name"] and int(r["Grid_Size_X"]) >= MIN_GRID:
                 out.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     return out
 
@@ -55,6 +62,7 @@ def main():
     write_b = statistics.mean(write) * 1024 if write else None
     res = {
         "kernel": FFN1 + " (FFN1 [32768,768]x[768,3072] + bias + GELU, B=64 x L=512)",
+        "precision": PREC,
         "dispatches": len(fetch),
         "avg_duration_us_trace": statistics.mean(durs) / 1e3 if durs else None,
         "fetch_size_kib_mean_raw": statistics.mean(fetch) if fetch else None,
@@ -65,8 +73,10 @@ def main():
         "algorithmic_bytes_per_launch": ALGO_BYTES,
         "traffic_over_algorithmic": ((fetch_b or 0) + (write_b or 0)) / ALGO_BYTES,
         "notes": "read bytes = 2 x FETCH_SIZE (gfx950 half-count on wide streaming reads); "
-                 "WRITE_SIZE uncalibrated for 4-B-per-lane stores; Infinity Cache hits are "
-                 "counted by FETCH_SIZE, so A/W re-reads served on-die appear here",
+                 + ("WRITE_SIZE uncalibrated for 4-B-per-lane stores; " if PREC == "fp32" else
+                    "WRITE_SIZE exact for the 16-B-per-lane epilogue stores; ")
+                 + "Infinity Cache hits are counted by FETCH_SIZE, so A/W re-reads served "
+                 "on-die appear here",
     }
     (out / f"{name}_pmc_ffn1.json").write_text(json.dumps(res, indent=1))
     print(json.dumps(res, indent=1))
