@@ -35,16 +35,13 @@ def convert_code_to_features(code, tokenizer, label, args):
 
 
 def get_identifiers(code, lang):
-    """run_parser.py:272-281 — returns (identifiers, code_tokens).  Only the code tokens feed the
-    attacks; the DFG identifier list is produced by apmc_amd.dataflow when available."""
+    """run_parser.py:272-281 — (identifiers as [[name]], code_tokens): the unique valid names of
+    the data-flow graph (C; host/dfg.cpp) and the comment-stripped leaves."""
+    from .utils import is_valid_variable_name
+
     ex = Example(code, lang)
     toks = ex.leaves(identifiers=True)
-    try:
-        from .dataflow import dfg_identifiers
-
-        idents = [[i] for i in dfg_identifiers(code, lang)]
-    except Exception:
-        idents = None
+    idents = [[n] for n in ex.dfg_names() if is_valid_variable_name(n, lang)]
     return idents, toks
 
 

@@ -222,4 +222,52 @@ int32_t ah_example_word_table(ah_example* e, int32_t* word_tok, int32_t cap_tok,
   return nt;
 }
 
+int32_t ah_example_identifiers(ah_example* e, char* buf, int32_t cap) {
+  if (!e) return fail("null example");
+  const std::vector<std::string> names = ah::dfg_names(e->ex.id_leaves, e->ex.lang);
+  size_t need = 0;
+  for (auto& s : names) need += s.size() + 1;
+  if (buf && (size_t)cap >= need) {
+    size_t p = 0;
+    for (auto& s : names) {
+      std::memcpy(buf + p, s.data(), s.size());
+      p += s.size();
+      buf[p++] = 0;
+    }
+  }
+  return (int32_t)need;
+}
+
+int32_t ah_example_dfg(ah_example* e, int32_t* rows, int32_t cap_rows, int32_t* from_idx,
+                       int32_t cap_from) {
+  if (!e) return fail("null example");
+  if (e->ex.lang != ah::LANG_C) return fail("data-flow graph: only C is built");
+  const std::vector<ah::DfgEdge> d = ah::dfg_c(e->ex.id_leaves);
+  int32_t nf = 0;
+  for (auto& x : d) nf += (int32_t)x.from_idx.size();
+  if (rows && cap_rows >= (int32_t)d.size() && from_idx && cap_from >= nf) {
+    int32_t f = 0;
+    for (size_t i = 0; i < d.size(); ++i) {
+      rows[4 * i + 0] = d[i].idx;
+      rows[4 * i + 1] = d[i].computed ? 1 : 0;
+      rows[4 * i + 2] = f;
+      rows[4 * i + 3] = (int32_t)d[i].from_idx.size();
+      for (int k : d[i].from_idx) from_idx[f++] = k;
+    }
+  }
+  if (cap_from < nf && rows) return -nf - 1;
+  return (int32_t)d.size();
+}
+
+int32_t ah_remove_comments(const char* code, char* out, int32_t cap) {
+  if (!code) return fail("null argument");
+  const std::string s = ah::remove_comments(code);
+  if (out && cap > 0) {
+    const int32_t m = std::min<int32_t>(cap - 1, (int32_t)s.size());
+    std::memcpy(out, s.data(), m);
+    out[m] = 0;
+  }
+  return (int32_t)s.size() + 1;
+}
+
 }  // extern "C"

@@ -82,6 +82,21 @@ std::string get_example(const Example& ex, const std::string& tgt, const std::st
 std::string get_example_batch(const Example& ex, const std::vector<std::string>& tgts,
                               const std::vector<std::string>& subs);
 
+// ------------------------------------------------------------------------------------ DFG
+// One DFG_c entry (python_parser/parser_folder/DFG_c.py): (code, idx, 'comesFrom' |
+// 'computedFrom', [from codes], [from idxs]); idx = leaf index.
+struct DfgEdge {
+  std::string code;
+  int idx;
+  bool computed;  // 'computedFrom' (update_expression) vs 'comesFrom'
+  std::vector<std::string> from_code;
+  std::vector<int> from_idx;
+};
+// DFG of C leaves (dfg.cpp), sorted by idx as extract_dataflow returns it (run_parser.py:213)
+std::vector<DfgEdge> dfg_c(const std::vector<Leaf>& leaves);
+// unique DFG names in graph order (get_identifiers before the validity filter, run_parser.py:272)
+std::vector<std::string> dfg_names(const std::vector<Leaf>& leaves, Lang lang);
+
 // ' '.join(code.split()) words
 std::vector<std::string> py_split(const std::string& s);
 

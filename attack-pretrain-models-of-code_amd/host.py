@@ -41,8 +41,12 @@ def load_host_library(path=None) -> ctypes.CDLL:
     lib.ah_example_mutants.argtypes = [vp, vp, i32, i32, vp, pp, pp, i32, vp, vp]
     lib.ah_example_mutant_words.argtypes = [vp, vp, i32, i32, vp, pp, pp, i32, vp, i32, vp, vp]
     lib.ah_example_word_table.argtypes = [vp, vp, i32, vp, i32, ctypes.POINTER(i32)]
+    lib.ah_example_identifiers.argtypes = [vp, vp, i32]
+    lib.ah_example_dfg.argtypes = [vp, vp, i32, vp, i32]
+    lib.ah_remove_comments.argtypes = [cp, vp, i32]
     lib.ah_last_error.restype = ctypes.c_char_p
-    for f in ("ah_tokenizer_special", "ah_tokenize", "ah_decode", "ah_featurize_batch",
+    for f in ("ah_example_identifiers", "ah_example_dfg", "ah_remove_comments",
+              "ah_tokenizer_special", "ah_tokenize", "ah_decode", "ah_featurize_batch",
               "ah_example_num_leaves", "ah_example_leaves", "ah_example_mutant_text",
               "ah_example_mutants", "ah_example_mutant_words", "ah_example_word_table"):
         getattr(lib, f).restype = i32
@@ -63,6 +67,16 @@ def _cstrs(strs):
 
 def _i32p(a: np.ndarray):
     return ctypes.c_void_p(a.ctypes.data)
+
+
+def remove_comments(code: str) -> str:
+    """remove_comments_and_docstrings(code, 'c' | 'java') (parser_folder/utils.py:30-87)."""
+    lib = load_host_library()
+    b = code.encode("utf-8")
+    need = lib.ah_remove_comments(b, None, 0)
+    buf = ctypes.create_string_buffer(need)
+    lib.ah_remove_comments(b, buf, need)
+    return buf.raw[:need - 1].decode("utf-8")
 
 
 class Tokenizer:
@@ -140,6 +154,32 @@ class Example:
         n = self.lib.ah_example_num_leaves(self.h, w)
         parts = buf.raw[:need].split(b"\0")[:n]
         return [p.decode("utf-8") for p in parts]
+
+    def dfg_names(self) -> list[str]:
+        """Unique data-flow-graph names in graph order (get_identifiers before its validity
+        filter, run_parser.py:272-281).  C only; other languages return []."""
+        need = self.lib.ah_example_identifiers(self.h, None, 0)
+        if need < 0:
+            _err("ah_example_identifiers")
+        buf = ctypes.create_string_buffer(max(need, 1))
+        self.lib.ah_example_identifiers(self.h, buf, need)
+        return [p.decode("utf-8") for p in buf.raw[:need].split(b"\0")[:-1]] if need else []
+
+    def dfg(self):
+        """extract_dataflow(code, lang)[0] as (idx, computed, from_idx list) per entry, sorted by
+        leaf index (run_parser.py:190-216, DFG_c.py:10-191).  The entry's code is leaves(True)[idx]."""
+        n = self.lib.ah_example_dfg(self.h, None, 0, None, 0)
+        if n < 0:
+            _err("ah_example_dfg")
+        rows = np.zeros((max(n, 1), 4), dtype=np.int32)
+        cap = 16
+        while True:
+            fr = np.zeros((cap,), dtype=np.int32)
+            r = self.lib.ah_example_dfg(self.h, _i32p(rows), n, _i32p(fr), cap)
+            if r >= 0:
+                break
+            cap = -r - 1
+        return [(int(a), bool(b), fr[o:o + c].tolist()) for a, b, o, c in rows[:n]]
 
     def mutant_text(self, pairs: list[tuple[str, str]], mode: int = MODE_BATCH) -> str:
         tg, sb = _cstrs([p[0] for p in pairs]), _cstrs([p[1] for p in pairs])

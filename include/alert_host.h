@@ -14,6 +14,9 @@
  *   ah_example_mutant_text    <- get_example / get_example_batch (run_parser.py:218-266)
  *   ah_example_mutants        <- convert_code_to_features(map_chromesome(...)) for a population
  *   ah_example_mutant_words   <- the same, as word-id sequences for the device splice (ae_splice)
+ *   ah_example_identifiers    <- get_identifiers(code, lang)[0] (run_parser.py:272-281)
+ *   ah_example_dfg            <- extract_dataflow(code, lang)[0] (run_parser.py:190-216, DFG_c.py)
+ *   ah_remove_comments        <- remove_comments_and_docstrings (parser_folder/utils.py:30-87)
  * All strings are UTF-8, NUL-terminated.  Functions return >= 0 on success (a count) or a
  * negative code; ah_last_error() describes the last failure of the calling thread.
  */
@@ -74,6 +77,20 @@ int32_t ah_example_mutant_words(ah_example *ex, ah_tokenizer *tok, int32_t mode,
  * *n_words_out = number of words (word_off needs n_words+1). */
 int32_t ah_example_word_table(ah_example *ex, int32_t *word_tok, int32_t cap_tok,
                               int32_t *word_off, int32_t cap_off, int32_t *n_words_out);
+
+/* get_identifiers(code, lang) before its validity filter (python_parser/run_parser.py:272-281):
+ * the unique names of the data-flow graph in graph order, over the comment-stripped leaves
+ * (which = 1).  NUL-separated; returns bytes needed.  C only (other languages: empty). */
+int32_t ah_example_identifiers(ah_example *ex, char *buf, int32_t cap);
+/* extract_dataflow(code, lang)[0] (run_parser.py:190-216 + DFG_c.py:10-191), sorted by leaf
+ * index.  rows [n, 4] = (leaf idx, 1 if computedFrom else 0, offset, count) into from_idx.
+ * Returns n (call with NULL buffers to size them; -(n_from)-1 if cap_from is too small).
+ * C only (other languages return an error). */
+int32_t ah_example_dfg(ah_example *ex, int32_t *rows, int32_t cap_rows, int32_t *from_idx,
+                       int32_t cap_from);
+/* remove_comments_and_docstrings(code, 'c'|'java') (parser_folder/utils.py:30-87); returns
+ * bytes needed incl. NUL. */
+int32_t ah_remove_comments(const char *code, char *out, int32_t cap);
 
 const char *ah_last_error(void);
 
