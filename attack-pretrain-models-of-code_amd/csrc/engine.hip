@@ -35,8 +35,8 @@ hipError_t ae_launch_attention_x3(const float*, float*, unsigned short*, const i
 hipError_t ae_launch_gemm_packed(const unsigned short*, const unsigned short*, const float*,
                                  const float*, float*, unsigned short*, int, int, int, int, int,
                                  hipStream_t);
-hipError_t ae_launch_compact(const int*, const int*, const int*, int, int, int, int*, int*, int*,
-                             hipStream_t);
+hipError_t ae_launch_compact(const int*, const int*, const int*, int, int, int, int, int*, int*,
+                             int*, hipStream_t);
 hipError_t ae_launch_embed_ln(const int*, const int*, const float*, const float*, const float*,
                               const float*, const float*, float, int, int, float*, unsigned short*,
                               int, hipStream_t);
@@ -51,8 +51,9 @@ hipError_t ae_launch_splice(const int*, const int*, const int*, const int*, int,
 hipError_t ae_launch_topk(const float*, int, int, int, float*, int*, hipStream_t);
 hipError_t ae_launch_cosine_rank(const float*, const float*, int, int, int, float, float*,
                                  hipStream_t);
-hipError_t ae_launch_scatter_rows(const float*, const int*, const int*, int, int, int, float*,
-                                  hipStream_t);
+hipError_t ae_launch_scatter_rows(const float*, const int*, const int*, int, int, int, int,
+                                  float*, hipStream_t);
+hipError_t ae_launch_nll_rows(const float*, const int*, int, int, float*, hipStream_t);
 }
 
 namespace {
@@ -320,10 +321,12 @@ int gemm_pk(ae_engine* e, const unsigned short* A, const unsigned short* Wp, con
 // Runs the encoder over compacted tokens; on return the last-layer CLS rows are in e->xc
 // (cls_only) or all rows in e->x.
 int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint32_t* mask_bits,
-                int n, int L, int64_t T, int max_len, bool cls_only, hipStream_t st) {
+                int n, int L, int64_t T, int max_len, bool cls_only, hipStream_t st,
+                int keep_all = 0) {
   const int H = e->cfg.hidden, F = e->cfg.ffn, NL = e->cfg.layers, heads = e->cfg.heads;
   const float eps = e->cfg.ln_eps;
-  HIPC(ae_launch_compact(ids, pos, e->cu, n, L, e->cfg.pad_id, e->tok_ids, e->tok_pos, e->src_col,
+  HIPC(ae_launch_compact(ids, pos, e->cu, n, L, e->cfg.pad_id, keep_all, e->tok_ids, e->tok_pos,
+                         e->src_col,
                          st));
   const bool pl = e->planes;
   HIPC(ae_launch_embed_ln(e->tok_ids, e->tok_pos, e->wemb, e->pemb, e->temb, e->eg, e->eb, eps,
@@ -597,11 +600,13 @@ int ae_score(ae_engine* e, const int32_t* ids, const int32_t* lens, const int32_
   return AE_OK;
 }
 
-int ae_encode(ae_engine* e, const int32_t* ids, const int32_t* lens, int32_t n, int32_t L,
-              float* hidden_out, void* stream) {
+int ae_encode_ex(ae_engine* e, const int32_t* ids, const int32_t* lens, int32_t n, int32_t L,
+                 int32_t flags, int32_t row0, int32_t nrows, float* hidden_out, void* stream) {
   int rc = check_common(e, ids, lens, n, L);
   if (rc) return rc;
   if (!hidden_out) return fail(AE_EINVAL, "null hidden_out");
+  if (row0 < 0 || nrows < 1 || row0 + nrows > L) return fail(AE_EINVAL, "bad row window");
+  if (flags & ~AE_ENC_ATTEND_PAD) return fail(AE_EINVAL, "unknown flags");
   if (n == 0) return AE_OK;
   HIPC(hipSetDevice(e->device));
   hipStream_t st = (hipStream_t)stream;
@@ -610,10 +615,43 @@ int ae_encode(ae_engine* e, const int32_t* ids, const int32_t* lens, int32_t n, 
   if ((rc = upload_cu(e, lens, n, L, st, &T))) return rc;
   int max_len = 0;
   for (int i = 0; i < n; ++i) max_len = lens[i] > max_len ? lens[i] : max_len;
-  if ((rc = run_encoder(e, ids, nullptr, nullptr, n, L, T, max_len, false, st))) return rc;
-  HIPC(ae_launch_scatter_rows(e->x, e->cu, e->src_col, n, L, (int)T, hidden_out, st));
+  if ((rc = run_encoder(e, ids, nullptr, nullptr, n, L, T, max_len, false, st,
+                        (flags & AE_ENC_ATTEND_PAD) ? 1 : 0)))
+    return rc;
+  HIPC(ae_launch_scatter_rows(e->x, e->cu, e->src_col, n, row0, nrows, (int)T, hidden_out, st));
   return AE_OK;
 }
+
+int ae_encode(ae_engine* e, const int32_t* ids, const int32_t* lens, int32_t n, int32_t L,
+              float* hidden_out, void* stream) {
+  return ae_encode_ex(e, ids, lens, n, L, 0, 0, L, hidden_out, stream);
+}
+
+}  // extern "C"
+
+namespace {
+// lm_head over the T encoder rows in e->x: dense -> gelu -> LN -> decoder (tied word embeddings)
+// + bias, into e->logits [T, V] (RobertaLMHead, reached from get_substitutes.py:62)
+int mlm_logits(ae_engine* e, int64_t T, hipStream_t st) {
+  const int V = e->cfg.vocab, H = e->cfg.hidden;
+  int rc;
+  if ((size_t)T * V > e->cap_logits) {
+    HIPC(hipDeviceSynchronize());
+    dev_free(e, e->logits);
+    if ((rc = dev_alloc(e, (void**)&e->logits, (size_t)T * V * 4))) return rc;
+    e->cap_logits = (size_t)T * V;
+  }
+  HIPC(ae_launch_gemm_f32(e->x, e->lm_dw, e->lm_db, nullptr, e->tmp, (int)T, H, H, H, H, H,
+                          EPI_BIAS_GELU, nullptr, st));
+  HIPC(ae_launch_layernorm(e->tmp, e->lm_lg, e->lm_lb, e->cfg.ln_eps, (int)T, e->ctx, nullptr, 0,
+                           st));
+  HIPC(ae_launch_gemm_f32(e->ctx, e->wemb, e->lm_bias, nullptr, e->logits, (int)T, V, H, H, H, V,
+                          EPI_BIAS, nullptr, st));
+  return AE_OK;
+}
+}  // namespace
+
+extern "C" {
 
 int ae_mlm_topk(ae_engine* e, const int32_t* ids, int32_t L, int32_t k, float* scores_out,
                 int32_t* ids_out, void* stream) {
@@ -627,22 +665,31 @@ int ae_mlm_topk(ae_engine* e, const int32_t* ids, int32_t L, int32_t k, float* s
   const int32_t lens[1] = {L};
   int64_t T = 0;
   if ((rc = upload_cu(e, lens, 1, L, st, &T))) return rc;
-  if ((rc = run_encoder(e, ids, nullptr, nullptr, 1, L, T, L, false, st))) return rc;
-  const int V = e->cfg.vocab, H = e->cfg.hidden;
-  if ((size_t)L * V > e->cap_logits) {
-    HIPC(hipDeviceSynchronize());
-    dev_free(e, e->logits);
-    if ((rc = dev_alloc(e, (void**)&e->logits, (size_t)L * V * 4))) return rc;
-    e->cap_logits = (size_t)L * V;
-  }
-  // lm_head: dense -> gelu -> LN -> decoder (tied word embeddings) + bias
-  HIPC(ae_launch_gemm_f32(e->x, e->lm_dw, e->lm_db, nullptr, e->tmp, L, H, H, H, H, H,
-                          EPI_BIAS_GELU, nullptr, st));
-  HIPC(ae_launch_layernorm(e->tmp, e->lm_lg, e->lm_lb, e->cfg.ln_eps, L, e->ctx, nullptr, 0,
-                           st));
-  HIPC(ae_launch_gemm_f32(e->ctx, e->wemb, e->lm_bias, nullptr, e->logits, L, V, H, H, H, V,
-                          EPI_BIAS, nullptr, st));
-  HIPC(ae_launch_topk(e->logits, L, V, k, scores_out, ids_out, st));
+  // codebert_mlm(input_ids_) is called without attention_mask: every id is attended
+  if ((rc = run_encoder(e, ids, nullptr, nullptr, 1, L, T, L, false, st, 1))) return rc;
+  if ((rc = mlm_logits(e, T, st))) return rc;
+  HIPC(ae_launch_topk(e->logits, L, e->cfg.vocab, k, scores_out, ids_out, st));
+  return AE_OK;
+}
+
+int ae_mlm_nll(ae_engine* e, const int32_t* ids, int32_t n, int32_t L, float* nll_out,
+               void* stream) {
+  if (!e || !ids || !nll_out) return fail(AE_EINVAL, "null argument");
+  if (!e->lm_dw) return fail(AE_EINVAL, "engine created without the MLM head (with_mlm=0)");
+  if (n < 0 || L < 1 || L > 4096) return fail(AE_EINVAL, "bad n/L");
+  if (n == 0) return AE_OK;
+  HIPC(hipSetDevice(e->device));
+  hipStream_t st = (hipStream_t)stream;
+  int rc;
+  if ((rc = ensure_workspace(e, (size_t)n * L, n))) return rc;
+  std::vector<int32_t> lens((size_t)n, L);
+  int64_t T = 0;
+  if ((rc = upload_cu(e, lens.data(), n, L, st, &T))) return rc;
+  // mlm_model(all_substitutes) without attention_mask (utils.py:237): every id is attended;
+  // with all rows full the compact token order is row-major [n, L]
+  if ((rc = run_encoder(e, ids, nullptr, nullptr, n, L, T, L, false, st, 1))) return rc;
+  if ((rc = mlm_logits(e, T, st))) return rc;
+  HIPC(ae_launch_nll_rows(e->logits, e->tok_ids, (int)T, e->cfg.vocab, nll_out, st));
   return AE_OK;
 }
 

@@ -13,39 +13,56 @@
 // ---------------------------------------------------------------------------------------------
 // Pad compaction: one workgroup per sequence.  Writes the non-pad ids of row s, in order, to
 // tok_ids[cu[s] + j] and their position ids (explicit `pos` row, or the RoBERTa rule pad+1+j).
+// keep_all (a model called without attention_mask, e.g. get_substitutes.py:62,73,105): the first
+// cu[s+1]-cu[s] ids of the row are all kept — a pad id is then an ordinary, attended token whose
+// position is `pad`, and only non-pad tokens advance the position counter (HF
+// create_position_ids_from_input_ids).
 // Also records where each compacted token came from (src_col) for ae_encode scatter-back.
 __global__ __launch_bounds__(256) void compact_kernel(const int* __restrict__ ids,
                                                       const int* __restrict__ pos,
                                                       const int* __restrict__ cu, int L, int pad,
+                                                      int keep_all,
                                                       int* __restrict__ tok_ids,
                                                       int* __restrict__ tok_pos,
                                                       int* __restrict__ src_col) {
-  __shared__ int wave_tot[4];
-  __shared__ int carry;
+  __shared__ int wave_tot[4], wave_np[4];
+  __shared__ int carry, carry_np;
   const int s = blockIdx.x;
   const int base = cu[s];
+  const int len = cu[s + 1] - base;
   const int* row = ids + (size_t)s * L;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) carry = 0;
+  if (tid == 0) carry = carry_np = 0;
   __syncthreads();
   for (int c0 = 0; c0 < L; c0 += 256) {
     const int c = c0 + tid;
     const int id = c < L ? row[c] : pad;
-    const int keep = id != pad;
-    const unsigned long long bal = __ballot(keep);
-    const int before = __popcll(bal & ((1ull << lane) - 1ull));
-    if (lane == 0) wave_tot[wave] = __popcll(bal);
+    const int nonpad = c < L && id != pad;
+    const int keep = keep_all ? c < len : nonpad;
+    const unsigned long long bal = __ballot(keep), bnp = __ballot(nonpad);
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const int before = __popcll(bal & below), np_before = __popcll(bnp & below);
+    if (lane == 0) {
+      wave_tot[wave] = __popcll(bal);
+      wave_np[wave] = __popcll(bnp);
+    }
     __syncthreads();
-    int off = carry;
-    for (int w = 0; w < wave; ++w) off += wave_tot[w];
+    int off = carry, off_np = carry_np;
+    for (int w = 0; w < wave; ++w) {
+      off += wave_tot[w];
+      off_np += wave_np[w];
+    }
     if (keep) {
       const int j = off + before;
       tok_ids[base + j] = id;
-      tok_pos[base + j] = pos ? pos[(size_t)s * L + c] : pad + 1 + j;
+      tok_pos[base + j] = pos ? pos[(size_t)s * L + c] : (nonpad ? pad + 1 + off_np + np_before : pad);
       if (src_col) src_col[base + j] = c;
     }
     __syncthreads();
-    if (tid == 0) carry += wave_tot[0] + wave_tot[1] + wave_tot[2] + wave_tot[3];
+    if (tid == 0) {
+      carry += wave_tot[0] + wave_tot[1] + wave_tot[2] + wave_tot[3];
+      carry_np += wave_np[0] + wave_np[1] + wave_np[2] + wave_np[3];
+    }
     __syncthreads();
   }
 }
@@ -210,42 +227,94 @@ __global__ __launch_bounds__(256) void head_out_kernel(const float* __restrict__
   for (int c = lane; c < C; c += 64) out[(size_t)row * C + c] = expf(logit[wave][c] - mx) / sm;
 }
 
-// Scatter compacted rows back to the padded [n, L, 768] layout (ae_encode).
+// Scatter compacted rows back to the padded layout (ae_encode): token t of sequence s, from
+// column c = src_col[t], goes to out[s, c - row0] when row0 <= c < row0 + nrows (out [n, nrows, 768]).
 __global__ __launch_bounds__(256) void scatter_rows_kernel(const float* __restrict__ x,
                                                            const int* __restrict__ cu,
                                                            const int* __restrict__ src_col, int n,
-                                                           int L, int T, float* __restrict__ out) {
+                                                           int row0, int nrows, int T,
+                                                           float* __restrict__ out) {
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (t >= T) return;
+  const int c = src_col[t] - row0;
+  if (c < 0 || c >= nrows) return;
   int lo = 0, hi = n;  // find s with cu[s] <= t < cu[s+1]
   while (hi - lo > 1) {
     const int mid = (lo + hi) >> 1;
     if (cu[mid] <= t) lo = mid; else hi = mid;
   }
-  const size_t dst = ((size_t)lo * L + src_col[t]) * AE_HIDDEN;
+  const size_t dst = ((size_t)lo * nrows + c) * AE_HIDDEN;
 #pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    const int col = c * 256 + lane * 4;
+  for (int k = 0; k < 3; ++k) {
+    const int col = k * 256 + lane * 4;
     *reinterpret_cast<floatx4*>(out + dst + col) =
         *reinterpret_cast<const floatx4*>(x + (size_t)t * AE_HIDDEN + col);
   }
 }
 
+// Token negative log-likelihood of the MLM logits (CrossEntropyLoss(reduction='none') of
+// utils.py:238-239): nll[t] = logsumexp(logits[t, :]) - logits[t, target[t]].  One 256-thread
+// workgroup per row; the 50265-wide row is read once (online max / rescaled sum per lane).
+__global__ __launch_bounds__(256) void nll_rows_kernel(const float* __restrict__ logits,
+                                                       const int* __restrict__ target, int V,
+                                                       float* __restrict__ nll) {
+  __shared__ float sm_m[4], sm_s[4];
+  const int t = blockIdx.x;
+  const float* row = logits + (size_t)t * V;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float m = -INFINITY, sum = 0.f;
+  for (int c = tid; c < V; c += 256) {
+    const float v = row[c];
+    if (v > m) {
+      sum = sum * expf(m - v) + 1.f;
+      m = v;
+    } else {
+      sum += expf(v - m);
+    }
+  }
+  // wave reduce (m, sum)
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o), s2 = __shfl_xor(sum, o);
+    const float mm = fmaxf(m, m2);
+    sum = (m == -INFINITY ? 0.f : sum * expf(m - mm)) + (m2 == -INFINITY ? 0.f : s2 * expf(m2 - mm));
+    m = mm;
+  }
+  if (lane == 0) {
+    sm_m[wave] = m;
+    sm_s[wave] = sum;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float M = sm_m[0];
+    for (int w = 1; w < 4; ++w) M = fmaxf(M, sm_m[w]);
+    float S = 0.f;
+    for (int w = 0; w < 4; ++w) S += sm_s[w] * expf(sm_m[w] - M);
+    nll[t] = logf(S) + M - row[target[t]];
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 extern "C" {
-hipError_t ae_launch_scatter_rows(const float* x, const int* cu, const int* src_col, int n, int L,
-                                  int T, float* out, hipStream_t st) {
+hipError_t ae_launch_scatter_rows(const float* x, const int* cu, const int* src_col, int n,
+                                  int row0, int nrows, int T, float* out, hipStream_t st) {
   if (T <= 0) return hipSuccess;
   hipLaunchKernelGGL(scatter_rows_kernel, dim3((T + 3) / 4), dim3(256), 0, st, x, cu, src_col, n,
-                     L, T, out);
+                     row0, nrows, T, out);
   return hipGetLastError();
 }
 hipError_t ae_launch_compact(const int* ids, const int* pos, const int* cu, int n, int L, int pad,
-                             int* tok_ids, int* tok_pos, int* src_col, hipStream_t st) {
+                             int keep_all, int* tok_ids, int* tok_pos, int* src_col,
+                             hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(compact_kernel, dim3(n), dim3(256), 0, st, ids, pos, cu, L, pad, tok_ids,
-                     tok_pos, src_col);
+  hipLaunchKernelGGL(compact_kernel, dim3(n), dim3(256), 0, st, ids, pos, cu, L, pad, keep_all,
+                     tok_ids, tok_pos, src_col);
+  return hipGetLastError();
+}
+hipError_t ae_launch_nll_rows(const float* logits, const int* target, int T, int V, float* nll,
+                              hipStream_t st) {
+  if (T <= 0) return hipSuccess;
+  hipLaunchKernelGGL(nll_rows_kernel, dim3(T), dim3(256), 0, st, logits, target, V, nll);
   return hipGetLastError();
 }
 hipError_t ae_launch_embed_ln(const int* tok_ids, const int* tok_pos, const float* wemb,

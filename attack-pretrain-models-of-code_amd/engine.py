@@ -33,7 +33,8 @@ class AeWeightView(ctypes.Structure):
 
 
 # every symbol include/alert_engine.h declares (checked by tests/test_abi.py)
-EXPORTS = ("ae_create", "ae_destroy", "ae_score", "ae_encode", "ae_mlm_topk", "ae_splice",
+EXPORTS = ("ae_create", "ae_destroy", "ae_score", "ae_encode", "ae_encode_ex", "ae_mlm_topk",
+           "ae_mlm_nll", "ae_splice",
            "ae_topk", "ae_cosine_rank", "ae_set_profiling", "ae_kernel_time", "ae_last_error",
            "ae_version")
 
@@ -59,7 +60,9 @@ def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     lib.ae_destroy.argtypes = [vp]
     lib.ae_score.argtypes = [vp, vp, vp, vp, vp, i32, i32, vp, vp]
     lib.ae_encode.argtypes = [vp, vp, vp, i32, i32, vp, vp]
+    lib.ae_encode_ex.argtypes = [vp, vp, vp, i32, i32, i32, i32, i32, vp, vp]
     lib.ae_mlm_topk.argtypes = [vp, vp, i32, i32, vp, vp, vp]
+    lib.ae_mlm_nll.argtypes = [vp, vp, i32, i32, vp, vp]
     lib.ae_splice.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp]
     lib.ae_topk.argtypes = [vp, i32, i32, i32, vp, vp, vp]
     lib.ae_cosine_rank.argtypes = [vp, vp, i32, i32, i32, ctypes.c_float, vp, vp]
@@ -154,14 +157,32 @@ class Engine:
                "ae_score")
         return out
 
-    def encode(self, ids, lens: np.ndarray, stream=None):
+    def encode(self, ids, lens: np.ndarray, attend_pad: bool = False, row0: int = 0,
+               nrows: int | None = None, stream=None):
+        """Hidden states [n, nrows, hidden] of rows [row0, row0+nrows) (default all L rows).
+        attend_pad: the model is called without attention_mask (every id of the first lens[i]
+        is attended, pad included)."""
         import torch
 
         n, L = ids.shape
+        assert ids.dtype == torch.int32 and ids.is_cuda and ids.is_contiguous()
+        nrows = L - row0 if nrows is None else nrows
         lens = np.ascontiguousarray(lens, dtype=np.int32)
-        out = torch.zeros((n, L, self.shape.hidden), dtype=torch.float32, device=ids.device)
-        _check(self.lib.ae_encode(self.handle, _ptr(ids), ctypes.c_void_p(lens.ctypes.data), n, L,
-                                  _ptr(out), _stream(stream)), "ae_encode")
+        out = torch.zeros((n, nrows, self.shape.hidden), dtype=torch.float32, device=ids.device)
+        _check(self.lib.ae_encode_ex(self.handle, _ptr(ids), ctypes.c_void_p(lens.ctypes.data),
+                                     n, L, 1 if attend_pad else 0, row0, nrows, _ptr(out),
+                                     _stream(stream)), "ae_encode_ex")
+        return out
+
+    def mlm_nll(self, ids, stream=None):
+        """Per-token MLM cross entropy of full rows ids [n, L] (no attention_mask)."""
+        import torch
+
+        n, L = ids.shape
+        assert ids.dtype == torch.int32 and ids.is_cuda and ids.is_contiguous()
+        out = torch.empty((n, L), dtype=torch.float32, device=ids.device)
+        _check(self.lib.ae_mlm_nll(self.handle, _ptr(ids), n, L, _ptr(out), _stream(stream)),
+               "ae_mlm_nll")
         return out
 
     def mlm_topk(self, ids, k: int, stream=None):

@@ -24,7 +24,10 @@
  *                    expressed on token ids: word-id sequences -> padded [n, L] ids.
  *   ae_mlm_topk   <- codebert_mlm(input_ids)[0] + torch.topk(., 60, -1)
  *                    (CodeXGLUE/Defect-detection/preprocess/get_substitutes.py:62-63)
- *   ae_encode     <- codebert_mlm.roberta(ids)[0] (get_substitutes.py:73,105)
+ *   ae_encode     <- codebert_mlm.roberta(ids)[0] (get_substitutes.py:73,105); ae_encode_ex adds
+ *                    the no-attention_mask call form and a row window (the cosine span)
+ *   ae_mlm_nll    <- mlm_model(all_substitutes)[0] + CrossEntropyLoss(reduction='none')
+ *                    (utils.py:237-239 get_bpe_substitues)
  *   ae_cosine_rank<- CosineSimilarity(dim=1) summed over the sub-word span / L_sub
  *                    (get_substitutes.py:75,108)
  *
@@ -114,7 +117,25 @@ int ae_score(ae_engine *eng, const int32_t *ids, const int32_t *lens, const int3
 int ae_encode(ae_engine *eng, const int32_t *ids, const int32_t *lens, int32_t n, int32_t L,
               float *hidden_out, void *stream);
 
-/* Masked-LM logits + top-k over the vocabulary for ONE sequence (no pad):
+/* ae_encode with options.
+ *   flags     AE_ENC_ATTEND_PAD: the model is called without attention_mask (get_substitutes.py
+ *             :73,105 codebert_mlm.roberta(ids)): the first lens[i] ids of row i are all attended,
+ *             a pad id included (position = pad_id, only non-pad ids advance positions)
+ *   row0/nrows  only rows [row0, row0 + nrows) of each sequence are written:
+ *             hidden_out device float [n, nrows, hidden] */
+#define AE_ENC_ATTEND_PAD 1
+int ae_encode_ex(ae_engine *eng, const int32_t *ids, const int32_t *lens, int32_t n, int32_t L,
+                 int32_t flags, int32_t row0, int32_t nrows, float *hidden_out, void *stream);
+
+/* Per-token masked-LM negative log-likelihood of n full rows (no attention_mask: every id is
+ * attended):  nll_out[i, t] = logsumexp(logits[i, t, :]) - logits[i, t, ids[i, t]]
+ * (CrossEntropyLoss(reduction='none') of utils.py:238, the BPE-substitute perplexity).
+ *   ids device int32 [n, L];  nll_out device float [n, L]. */
+int ae_mlm_nll(ae_engine *eng, const int32_t *ids, int32_t n, int32_t L, float *nll_out,
+               void *stream);
+
+/* Masked-LM logits + top-k over the vocabulary for ONE sequence (no attention_mask: every id is
+ * attended, as codebert_mlm(input_ids_) in get_substitutes.py:62):
  *   scores_out device float [L, k], ids_out device int32 [L, k] (descending, ties by lower id). */
 int ae_mlm_topk(ae_engine *eng, const int32_t *ids, int32_t L, int32_t k, float *scores_out,
                 int32_t *ids_out, void *stream);

@@ -42,10 +42,13 @@ def position_ids(ids: torch.Tensor, pad: int = 1) -> torch.Tensor:
 
 @torch.no_grad()
 def encoder_forward(sd, ids, pos=None, attn_mask=None, layers: int = 12, heads: int = 12,
-                    pad: int = 1, eps: float = 1e-5, inputs_embeds=None) -> torch.Tensor:
+                    pad: int = 1, eps: float = 1e-5, inputs_embeds=None,
+                    no_mask: bool = False) -> torch.Tensor:
     """Last hidden state [n, L, 768] of RoBERTa for int ids [n, L].
 
     attn_mask: None -> key padding mask ids != pad; else bool [n, L, L] (True = may attend).
+    no_mask: the model is called without attention_mask (HF then attends every id, pad included;
+    positions still follow the pad rule) — the MLM call sites of get_substitutes.py:62,73,105.
     """
     ids = torch.as_tensor(np.asarray(ids), dtype=torch.long)
     n, L = ids.shape
@@ -61,7 +64,9 @@ def encoder_forward(sd, ids, pos=None, attn_mask=None, layers: int = 12, heads: 
     x = x + _t(sd, "embeddings.position_embeddings.weight")[pos]
     x = _ln(x, _t(sd, "embeddings.LayerNorm.weight"), _t(sd, "embeddings.LayerNorm.bias"), eps)
     neg = torch.finfo(torch.float32).min
-    if attn_mask is None:
+    if no_mask:
+        add = torch.zeros((n, 1, 1, L), dtype=torch.float32)
+    elif attn_mask is None:
         add = torch.zeros((n, 1, 1, L), dtype=torch.float32)
         add.masked_fill_(~ids.ne(pad)[:, None, None, :], neg)
     else:
@@ -115,9 +120,9 @@ def score(sd, ids, kind: str = "sigmoid1", layers: int = 12, pos=None, attn_mask
 
 
 @torch.no_grad()
-def mlm_logits(sd, ids, layers: int = 12) -> torch.Tensor:
+def mlm_logits(sd, ids, layers: int = 12, no_mask: bool = False) -> torch.Tensor:
     """RobertaForMaskedLM logits [n, L, V] (lm_head: dense -> gelu -> LN -> tied decoder + bias)."""
-    h = encoder_forward(sd, ids, layers=layers)
+    h = encoder_forward(sd, ids, layers=layers, no_mask=no_mask)
     x = torch.nn.functional.linear(h, _t(sd, "lm_head.dense.weight"), _t(sd, "lm_head.dense.bias"))
     x = torch.nn.functional.gelu(x)
     x = _ln(x, _t(sd, "lm_head.layer_norm.weight"), _t(sd, "lm_head.layer_norm.bias"), 1e-5)
