@@ -107,3 +107,40 @@ def run_sharded_gi_attack(model, codes, subs, labels, args, device=None, tok=Non
                wall_s=float(st[:, 4].max()), per_rank=st.tolist())
     tot["success_rate"] = tot["success"] / tot["total_cnt"] if tot["total_cnt"] else 0.0
     return recs, tot
+
+
+def run_sharded_substitutes(gen, in_path, out_path, start=0, end=None, device=None,
+                            deadline: float | None = None):
+    """get_substitutes.py over all ranks (examples across ranks, jsonl merged by
+    index): every rank pulls item indices from the shared queue and writes its shard
+    `<out_path>.rank<r>`; rank 0 merges the shards into `out_path` in input order.  Returns the
+    job totals (all-gathered)."""
+    import torch.distributed as dist
+
+    from .substitutes import generate_file, merge_shards
+
+    on = dist.is_available() and dist.is_initialized()
+    rank, world = (dist.get_rank(), dist.get_world_size()) if on else (0, 1)
+    n_items = 0
+    with open(in_path) as f:
+        for i, _ in enumerate(f):
+            if i >= start and (end is None or i < end):
+                n_items += 1
+    q = DynamicQueue(n_items, key="apmc_subs_queue", deadline=deadline)
+    shard = f"{out_path}.rank{rank}"
+    t0 = time.time()
+    out = generate_file(gen, in_path, shard, start, end, queue=q)
+    wall = time.time() - t0
+    st = gather_stats([out["items"], out["occurrences"], out["encoded_seqs"],
+                       out["encoded_tokens"], wall], device=device)
+    if on:
+        dist.barrier()
+    if rank == 0:
+        merge_shards([f"{out_path}.rank{r}" for r in range(world)], out_path)
+        for r in range(world):
+            os.remove(f"{out_path}.rank{r}")
+    if on:
+        dist.barrier()
+    return dict(items=int(st[:, 0].sum()), occurrences=int(st[:, 1].sum()),
+                encoded_seqs=int(st[:, 2].sum()), encoded_tokens=int(st[:, 3].sum()),
+                wall_s=float(st[:, 4].max()), per_rank=st.tolist())

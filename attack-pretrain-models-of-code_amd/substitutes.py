@@ -44,8 +44,15 @@ class SubstituteGenerator:
         self.tok = tokenizer or Tokenizer()
         self.block_size = block_size
         self.lang = lang
+        self.tokens_per_call = 1 << 18  # candidate tokens per re-encode call (workspace bound)
         self.stats = {"examples": 0, "occurrences": 0, "encoded_seqs": 0, "encoded_tokens": 0,
-                      "bpe_batches": 0}
+                      "bpe_batches": 0, "encoder_flop": 0.0}
+
+    def _enc_flop(self, L: int) -> float:
+        """Algorithmic FLOP of one encoder pass over L tokens (SURVEY §8(d) F_enc)."""
+        sh = self.engine.shape
+        per_tok = 2 * (4 * sh.hidden * sh.hidden + 2 * sh.hidden * sh.ffn)
+        return sh.layers * (L * per_tok + 4 * L * L * sh.hidden)
 
     # ------------------------------------------------------------------------------------------
     def _bpe_words(self, substitutes: np.ndarray, trace=None) -> list[str]:
@@ -81,9 +88,7 @@ class SubstituteGenerator:
     # ------------------------------------------------------------------------------------------
     def generate(self, func: str, trace=None) -> dict[str, list[str]]:
         """`item["substitutes"]` for one function (get_substitutes.py:54-137)."""
-        import torch
-
-        lang, tok = self.lang, self.tok
+        lang = self.lang
         identifiers, code_tokens = get_identifiers(remove_comments(func), lang)
         variable_names = [name[0] for name in identifiers if " " not in name[0].strip()]
         return self.generate_from_tokens(code_tokens, variable_names, trace)
@@ -111,35 +116,54 @@ class SubstituteGenerator:
         from .engine import cosine_rank
 
         positions = get_identifier_posistions_from_code(words, variable_names)
-        result: dict[str, list[str]] = {}
+        # every (word, occurrence) that reaches the cosine filter, in the reference's loop order
+        occ = []
         for tgt_word, tgt_positions in positions.items():
             if not is_valid_variable_name(tgt_word, self.lang):
                 continue
-            all_subs: list[str] = []
             for one_pos in tgt_positions:
                 k0, k1 = keys[one_pos]
-                if k0 >= n_pred:
-                    continue
-                k1e = min(k1, n_pred)  # slices clip at the prediction rows (L - 1)
-                span = k1e - k0
-                cand_ids = preds[k0:k1e]  # [span, 60]
-                batch = np.repeat(ids_np[None], K_TOP, axis=0)
-                batch[:, k0 + 1:k1e + 1] = cand_ids.T
-                bdev = torch.from_numpy(batch).to(dev)
-                hid = self.engine.encode(bdev, np.full((K_TOP,), L, np.int32), attend_pad=True,
-                                         row0=k0 + 1, nrows=span)
-                sims = cosine_rank(orig[k0 + 1:k1e + 1].contiguous(), hid, eps=1e-6)
-                sims = sims.cpu().numpy()
-                self.stats["occurrences"] += 1
-                self.stats["encoded_seqs"] += K_TOP
-                self.stats["encoded_tokens"] += K_TOP * L
-                if trace is not None:
-                    trace["sims"].append((tgt_word, one_pos, [float(v) for v in sims]))
-                # sorted(sims, key=sim, reverse=True): stable, ties keep candidate order
-                order = sorted(range(K_TOP), key=lambda i: sims[i], reverse=True)[:K_TOP // 2]
-                similar = cand_ids[:, order]
-                all_subs += self._words(similar, trace)
-            for s in set(all_subs):
+                if k0 < n_pred:
+                    occ.append((tgt_word, one_pos, k0, min(k1, n_pred)))  # slices clip at L - 1
+        # re-encode the 60 candidates of several occurrences per device call (rows of a batch are
+        # independent, so batching changes nothing but float rounding); one host sync per chunk
+        per_call = max(1, min(16, self.tokens_per_call // (K_TOP * L)))
+        sims_of = {}
+        for c0 in range(0, len(occ), per_call):
+            chunk = occ[c0:c0 + per_call]
+            r_lo = min(k0 for _, _, k0, _ in chunk) + 1
+            r_hi = max(k1e for _, _, _, k1e in chunk) + 1
+            batch = np.repeat(ids_np[None], K_TOP * len(chunk), axis=0)
+            for j, (_, _, k0, k1e) in enumerate(chunk):
+                batch[j * K_TOP:(j + 1) * K_TOP, k0 + 1:k1e + 1] = preds[k0:k1e].T
+            bdev = torch.from_numpy(batch).to(dev)
+            hid = self.engine.encode(bdev, np.full((len(batch),), L, np.int32), attend_pad=True,
+                                     row0=r_lo, nrows=r_hi - r_lo)
+            sims = torch.empty((len(chunk), K_TOP), dtype=torch.float32, device=dev)
+            for j, (_, _, k0, k1e) in enumerate(chunk):
+                cand = hid[j * K_TOP:(j + 1) * K_TOP, k0 + 1 - r_lo:k1e + 1 - r_lo].contiguous()
+                sims[j] = cosine_rank(orig[k0 + 1:k1e + 1].contiguous(), cand, eps=1e-6)
+            sims = sims.cpu().numpy()
+            for j, o in enumerate(chunk):
+                sims_of[o] = sims[j]
+            self.stats["occurrences"] += len(chunk)
+            self.stats["encoded_seqs"] += len(batch)
+            self.stats["encoded_tokens"] += len(batch) * L
+            self.stats["encoder_flop"] += len(batch) * self._enc_flop(L)
+        result: dict[str, list[str]] = {}
+        all_subs: dict[str, list[str]] = {}
+        for o in occ:
+            tgt_word, one_pos, k0, k1e = o
+            sims = sims_of[o]
+            cand_ids = preds[k0:k1e]  # [span, 60]
+            if trace is not None:
+                trace["sims"].append((tgt_word, one_pos, [float(v) for v in sims],
+                                      [tuple(int(x) for x in c) for c in cand_ids.T]))
+            # sorted(sims, key=sim, reverse=True): stable, ties keep candidate order
+            order = sorted(range(K_TOP), key=lambda i: sims[i], reverse=True)[:K_TOP // 2]
+            all_subs.setdefault(tgt_word, []).extend(self._words(cand_ids[:, order], trace))
+        for tgt_word, subs in all_subs.items():
+            for s in set(subs):
                 if s.strip() in variable_names:
                     continue
                 if not is_valid_substitue(s.strip(), tgt_word, self.lang):

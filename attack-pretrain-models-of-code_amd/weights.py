@@ -140,3 +140,32 @@ def to_hf_state_dict(sd: dict[str, np.ndarray], arch: str = "seqcls") -> dict:
         out["lm_head.decoder.weight"] = out["roberta.embeddings.word_embeddings.weight"]
         out["lm_head.decoder.bias"] = out["lm_head.bias"]
     return out
+
+
+def load_checkpoint(path) -> dict[str, np.ndarray]:
+    """Engine state dict from a local HF model directory or a reference `model.bin`.
+
+    Accepts a directory holding model.safetensors or pytorch_model.bin (the from_pretrained
+    layout the reference loads, gi_attack.py:122-152) or a single .bin / .safetensors file (the
+    fine-tuned `model.bin` the attack scripts load_state_dict, gi_attack.py:138-146).  Loaded only
+    with loaders that execute nothing from the file (safetensors, torch.load(weights_only=True)).
+    """
+    import pathlib
+
+    p = pathlib.Path(path)
+    if p.is_dir():
+        for name in ("model.safetensors", "pytorch_model.bin", "model.bin"):
+            if (p / name).exists():
+                p = p / name
+                break
+        else:
+            raise FileNotFoundError(f"no model.safetensors / pytorch_model.bin under {path}")
+    if p.suffix == ".safetensors":
+        from safetensors.numpy import load_file
+
+        raw = load_file(str(p))
+    else:
+        import torch
+
+        raw = torch.load(str(p), map_location="cpu", weights_only=True)
+    return normalize_state_dict(raw)

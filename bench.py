@@ -120,6 +120,60 @@ def attack_leg(dev, seconds, rank, world, precision):
             "sharding": "dynamic queue (torch.distributed store counter)"}
 
 
+def subs_leg(dev, seconds, rank, world, precision):
+    """Config-3 workload: masked-LM substitute generation (get_substitutes.py) over the Devign
+    fixture functions in order (12-layer codebert-shaped MLM, synthetic weights), items pulled
+    from a shared queue until the time budget is spent."""
+    from apmc_amd.dist import DynamicQueue
+    from apmc_amd.engine import Engine
+    from apmc_amd.host import Tokenizer
+    from apmc_amd.substitutes import SubstituteGenerator
+    from apmc_amd.weights import synthetic_state_dict
+
+    eng = Engine(synthetic_state_dict(seed=0, head="none", with_mlm=True), head="none",
+                 with_mlm=True, precision=precision, device=dev.index)
+    gen = SubstituteGenerator(eng, Tokenizer(), block_size=512)
+    codes = [json.loads(line)["func"] for line in
+             open(ROOT / "data" / "devign" / "test_subs_0_400.jsonl")]
+    gen.generate(codes[0])  # warm-up (workspaces, logits buffer)
+    gen.stats = {k: 0 for k in gen.stats}
+    queue = DynamicQueue(len(codes), key="bench_subs_queue", deadline=time.time() + seconds)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    while True:
+        i = queue()
+        if i is None:
+            break
+        gen.generate(codes[i])
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    st = gen.stats
+    v = np.array([st["examples"], st["occurrences"], st["encoded_seqs"], st["encoded_tokens"],
+                  st["encoder_flop"], wall], dtype=np.float64)
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor(v, device=dev)
+        g = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(g, t)
+        allv = torch.stack(g).cpu().numpy()
+    else:
+        allv = v[None]
+    tot = allv[:, :5].sum(0)
+    wall = allv[:, 5].max()
+    eng.close()
+    return {"workload": "CodeBERT masked-LM substitute generation (get_substitutes.py: top-60, "
+                        "60 re-encodes per identifier occurrence, cosine top-30, BPE perplexity), "
+                        "test_subs_0_400 functions in order, block 512",
+            "precision": precision, "items": int(tot[0]), "occurrences": int(tot[1]),
+            "reencoded_sequences": int(tot[2]), "wall_s": round(wall, 2),
+            "items_per_min": round(60 * tot[0] / wall, 2),
+            "reencoded_sequences_per_s": round(tot[2] / wall, 1),
+            "encoder_tflops": round(tot[4] / wall / 1e12, 2)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -130,6 +184,8 @@ def main():
     ap.add_argument("--precision", default="f32x3", choices=["fp32", "f32x3", "bf16"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--subs-seconds", type=float, default=30.0,
+                    help="time budget of the substitute-generation leg (config 3; 0 disables)")
     ap.add_argument("--attack-seconds", type=float, default=90.0,
                     help="time budget of the end-to-end GA attack leg over test_subs_0_400 "
                          "(0 disables)")
@@ -246,6 +302,8 @@ def main():
     }
     if args.attack_seconds > 0:
         res["attack"] = attack_leg(dev, args.attack_seconds, rank, world, args.precision)
+    if args.subs_seconds > 0:
+        res["substitutes"] = subs_leg(dev, args.subs_seconds, rank, world, args.precision)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
         res["cpu_baseline"] = cpu_baseline(L, args.cpu_seconds, threads)

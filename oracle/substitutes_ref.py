@@ -136,7 +136,8 @@ def substitutes_for_example(sd, tokenizer, code_tokens, variable_names, is_valid
                 new_word_embed = new_emb[i][k0 + 1:k1 + 1]
                 sims.append((i, sum(cos(orig_word_embed, new_word_embed)) / subwords_leng))
             if trace is not None:
-                trace["sims"].append((tgt_word, one_pos, [float(v) for _, v in sims]))
+                trace["sims"].append((tgt_word, one_pos, [float(v) for _, v in sims],
+                                      [tuple(int(x) for x in c) for c in substitutes.t()]))
             sims = sorted(sims, key=lambda x: x[1], reverse=True)
             similar_substitutes, similar_word_pred_scores = [], []
             for i in range(int(nums_candis / 2)):

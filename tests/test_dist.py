@@ -89,3 +89,54 @@ def test_two_ranks_match_single_process(tmp_path):
     # both ranks pulled work from the shared queue
     per_rank = got["tot"]["per_rank"]
     assert len(per_rank) == 2 and all(r[0] >= 1 for r in per_rank)
+
+
+class FakeSubsGen:
+    """Stands in for SubstituteGenerator (the masked-LM arithmetic needs the GPU): the real host
+    identifier extraction, a deterministic substitute rule."""
+
+    def __init__(self):
+        self.stats = {"examples": 0, "occurrences": 0, "encoded_seqs": 0, "encoded_tokens": 0}
+
+    def generate(self, func):
+        from apmc_amd.attacker import get_identifiers
+        from apmc_amd.host import remove_comments
+        ids, _ = get_identifiers(remove_comments(func), "c")
+        self.stats["examples"] += 1
+        self.stats["occurrences"] += len(ids)
+        return {i[0]: [i[0] + "_x", "v" + str(len(i[0]))] for i in ids}
+
+
+def _subs_worker(rank, world, port, outdir):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), LOCAL_RANK=str(rank))
+    sys.path.insert(0, str(ROOT))
+    import _apmc  # noqa: F401
+    from apmc_amd.dist import init_from_env, run_sharded_substitutes
+    import torch.distributed as dist
+
+    init_from_env("gloo")
+    tot = run_sharded_substitutes(FakeSubsGen(), FIXTURE, str(pathlib.Path(outdir) / "subs.jsonl"),
+                                  0, N_EX)
+    if rank == 0:
+        import json
+        (pathlib.Path(outdir) / "tot.json").write_text(json.dumps(tot))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_substitutes_match_single_process(tmp_path):
+    """get_substitutes.py sharded over 2 ranks: merged jsonl == single-process output."""
+    sys.path.insert(0, str(ROOT))
+    import json
+    import random
+    import _apmc  # noqa: F401
+    from apmc_amd.substitutes import generate_file
+
+    port = 31500 + random.Random(os.getpid()).randint(0, 2000)
+    mp.spawn(_subs_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    generate_file(FakeSubsGen(), FIXTURE, tmp_path / "single.jsonl", 0, N_EX)
+    assert (tmp_path / "subs.jsonl").read_text() == (tmp_path / "single.jsonl").read_text()
+    tot = json.loads((tmp_path / "tot.json").read_text())
+    assert tot["items"] == N_EX and all(r[0] >= 1 for r in tot["per_rank"])
+    assert not list(tmp_path.glob("subs.jsonl.rank*"))

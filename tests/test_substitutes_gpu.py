@@ -76,7 +76,7 @@ def _near_tie_words(trace):
     logits = trace["logits"]  # [L, V]
     top61 = torch.topk(logits, 61, -1).values.numpy()[1:]
     tied_rows = set(np.nonzero(top61[:, 59] - top61[:, 60] < LOGIT_TIE)[0].tolist())
-    for word, pos, sims in trace["sims"]:
+    for word, pos, sims, _ in trace["sims"]:
         s = np.sort(np.asarray(sims, np.float64))[::-1]
         if s[29] - s[30] < SIM_TIE or len(set(np.round(sims, 7))) < len(sims):
             bad.add(word)
@@ -107,9 +107,15 @@ def test_substitutes_match_oracle_on_fixture_functions(setup):
         rows = [r for r in range(tr_o["topk_ids"].shape[0]) if r not in tied_rows]
         same = (tr_g["topk_ids"][rows] == tr_o["topk_ids"][rows])
         assert same.mean() > 0.995, same.mean()
-        for (wg, pg, sg), (wo, po, so) in zip(tr_g["sims"], tr_o["sims"]):
+        for (wg, pg, sg, cg), (wo, po, so, co) in zip(tr_g["sims"], tr_o["sims"]):
             assert (wg, pg) == (wo, po)
-            np.testing.assert_allclose(sg, so, atol=5e-5)
+            # cosine scores per candidate (adjacent near-equal logits may order the top-60
+            # columns differently; the candidate set is what must agree)
+            dg, do = dict(zip(cg, sg)), dict(zip(co, so))
+            common = set(dg) & set(do)
+            assert len(common) >= 58, len(common)
+            np.testing.assert_allclose([dg[c] for c in common], [do[c] for c in common],
+                                       atol=5e-5)
         for word in set(got) | set(exp):
             if word in bad:
                 excused += 1
