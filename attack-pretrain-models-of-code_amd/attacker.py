@@ -22,7 +22,7 @@ from .utils import (CodeDataset, InputFeatures, IdsDataset, _tokenize, crossover
 
 
 def _label_of(example):
-    lab = example[1]
+    lab = example[-1]  # (ids, label) / GCB (ids, mask, pos, label) / pairs: label is last
     return int(lab.item()) if hasattr(lab, "item") else int(lab)
 
 
@@ -59,8 +59,9 @@ class _Scorer:
                                         self.a.args.block_size)
 
     def texts(self, texts):
-        ids, lens = self.a.tokenizer_tgt.featurize(texts, self.a.args.block_size)
-        return self.a.model_tgt.get_results(IdsDataset(ids, lens), self.a.args.eval_batch_size)
+        m = self.a.model_tgt
+        return m.get_results(m.dataset_from_texts(texts, self.a.tokenizer_tgt, self.a.args),
+                             self.a.args.eval_batch_size)
 
 
 def get_importance_score(args, example, code, words_list, sub_words, variable_names, tgt_model,
@@ -72,8 +73,8 @@ def get_importance_score(args, example, code, words_list, sub_words, variable_na
         return None, None, None
     masked_token_list, replace_token_positions = get_masked_code_by_position(words_list, positions)
     texts = [" ".join(tokens) for tokens in [words_list] + masked_token_list]
-    ids, lens = tokenizer.featurize(texts, args.block_size)
-    logits, preds = tgt_model.get_results(IdsDataset(ids, lens), args.eval_batch_size)
+    logits, preds = tgt_model.get_results(tgt_model.dataset_from_texts(texts, tokenizer, args),
+                                          args.eval_batch_size)
     orig_probs = logits[0]
     orig_label = preds[0]
     orig_prob = max(orig_probs)

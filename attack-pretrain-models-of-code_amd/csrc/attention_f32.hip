@@ -18,6 +18,7 @@
 //   the next MFMA needs), so the row max / sum / rescale are lane-local plus one xor-32 shuffle.
 //   K/V tiles of 32 keys are double-buffered in LDS (K rows padded to 68 floats: conflict-free
 //   ds_read_b128), next tile's global loads issued before the current tile's MFMAs.
+#include <cfloat>
 #include "common.h"
 
 namespace {
@@ -128,8 +129,11 @@ __global__ __launch_bounds__(256, 2) void attn_f32_kernel(const float* __restric
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int kk = mfma32_row(r, lh);
-      const bool ok = (kt * KT + kk < len) && ((mbits >> kk) & 1u);
-      s[r] = ok ? s[r] : -INFINITY;
+      // absent keys (beyond the sequence) are -inf; keys the mask excludes score the most
+      // negative finite float, as HF's additive finfo(f32).min mask does: a query row that
+      // excludes every key then attends all of them uniformly (GraphCodeBERT truncated nodes)
+      const bool in = kt * KT + kk < len;
+      s[r] = !in ? -INFINITY : (((mbits >> kk) & 1u) ? s[r] : -FLT_MAX);
       mt = fmaxf(mt, s[r]);
     }
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));

@@ -13,6 +13,7 @@
 //                            straight from the S^T accumulator: accumulator registers 8t..8t+7 of
 //                            lane half h hold keys (j&3)+8(j>>2)+4h+16t — that permuted key order
 //                            is used for the V^T operand of the same k-slot.
+#include <cfloat>
 #include "common.h"
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -154,8 +155,11 @@ __global__ __launch_bounds__(256, 2) void attn_x3_kernel(const float* __restrict
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int kk = mfma32_row(r, lh);
-      const bool ok = (kt * KT + kk < len) && ((mbits >> kk) & 1u);
-      s[r] = ok ? s[r] : -INFINITY;
+      // absent keys (beyond the sequence) are -inf; keys the mask excludes score the most
+      // negative finite float, as HF's additive finfo(f32).min mask does: a query row that
+      // excludes every key then attends all of them uniformly (GraphCodeBERT truncated nodes)
+      const bool in = kt * KT + kk < len;
+      s[r] = !in ? -INFINITY : (((mbits >> kk) & 1u) ? s[r] : -FLT_MAX);
       mt = fmaxf(mt, s[r]);
     }
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));

@@ -39,7 +39,7 @@ hipError_t ae_launch_compact(const int*, const int*, const int*, int, int, int, 
                              int*, hipStream_t);
 hipError_t ae_launch_embed_ln(const int*, const int*, const float*, const float*, const float*,
                               const float*, const float*, float, int, int, float*, unsigned short*,
-                              int, hipStream_t);
+                              int, const uint32_t*, int, const int*, int, hipStream_t);
 hipError_t ae_launch_layernorm(const float*, const float*, const float*, float, int, float*,
                                unsigned short*, int, hipStream_t);
 hipError_t ae_launch_gather_cls(const float*, const float*, const int*, int, float*, float*,
@@ -322,7 +322,7 @@ int gemm_pk(ae_engine* e, const unsigned short* A, const unsigned short* Wp, con
 // (cls_only) or all rows in e->x.
 int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint32_t* mask_bits,
                 int n, int L, int64_t T, int max_len, bool cls_only, hipStream_t st,
-                int keep_all = 0) {
+                int keep_all = 0, bool node_avg = false) {
   const int H = e->cfg.hidden, F = e->cfg.ffn, NL = e->cfg.layers, heads = e->cfg.heads;
   const float eps = e->cfg.ln_eps;
   HIPC(ae_launch_compact(ids, pos, e->cu, n, L, e->cfg.pad_id, keep_all, e->tok_ids, e->tok_pos,
@@ -330,7 +330,8 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
                          st));
   const bool pl = e->planes;
   HIPC(ae_launch_embed_ln(e->tok_ids, e->tok_pos, e->wemb, e->pemb, e->temb, e->eg, e->eb, eps,
-                          (int)T, e->cfg.max_pos, e->x, pl ? e->xp : nullptr, e->np, st));
+                          (int)T, e->cfg.max_pos, e->x, pl ? e->xp : nullptr, e->np,
+                          node_avg ? mask_bits : nullptr, L, e->cu, n, st));
   for (int li = 0; li < NL; ++li) {
     const LayerW& w = e->layers[li];
     const bool last_cls = cls_only && li == NL - 1;
@@ -572,8 +573,25 @@ int ae_destroy(ae_engine* e) {
   return AE_OK;
 }
 
+static int score_impl(ae_engine* e, const int32_t* ids, const int32_t* lens, const int32_t* pos,
+                      const uint32_t* mask_bits, int32_t n, int32_t L, float* probs_out,
+                      void* stream, bool node_avg);
+
 int ae_score(ae_engine* e, const int32_t* ids, const int32_t* lens, const int32_t* pos,
              const uint32_t* mask_bits, int32_t n, int32_t L, float* probs_out, void* stream) {
+  return score_impl(e, ids, lens, pos, mask_bits, n, L, probs_out, stream, false);
+}
+
+int ae_score_graph(ae_engine* e, const int32_t* ids, const int32_t* lens, const int32_t* pos,
+                   const uint32_t* mask_bits, int32_t n, int32_t L, float* probs_out,
+                   void* stream) {
+  if (!pos || !mask_bits) return fail(AE_EINVAL, "ae_score_graph needs pos and mask_bits");
+  return score_impl(e, ids, lens, pos, mask_bits, n, L, probs_out, stream, true);
+}
+
+static int score_impl(ae_engine* e, const int32_t* ids, const int32_t* lens, const int32_t* pos,
+                      const uint32_t* mask_bits, int32_t n, int32_t L, float* probs_out,
+                      void* stream, bool node_avg) {
   int rc = check_common(e, ids, lens, n, L);
   if (rc) return rc;
   if (e->cfg.head_kind == AE_HEAD_NONE) return fail(AE_EINVAL, "engine has no task head");
@@ -588,7 +606,9 @@ int ae_score(ae_engine* e, const int32_t* ids, const int32_t* lens, const int32_
   if ((rc = upload_cu(e, lens, n, L, st, &T))) return rc;
   int max_len = 0;
   for (int i = 0; i < n; ++i) max_len = lens[i] > max_len ? lens[i] : max_len;
-  if ((rc = run_encoder(e, ids, pos, mask_bits, n, L, T, max_len, true, st))) return rc;
+  if ((rc = run_encoder(e, ids, pos, mask_bits, n, L, T, max_len, true, st, node_avg ? 1 : 0,
+                        node_avg)))
+    return rc;
   const int kind = e->cfg.head_kind == AE_HEAD_SIGMOID1 ? 0 : (e->cfg.head_kind == AE_HEAD_PAIR2 ? 2 : 1);
   const int n_out = kind == 2 ? n / 2 : n;
   // head: dense (+tanh) as a GEMM over the compact CLS rows (pair head: [n/2, 1536] view), then

@@ -114,24 +114,68 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(
     const float* __restrict__ wemb, const float* __restrict__ pemb,
     const float* __restrict__ temb, const float* __restrict__ g, const float* __restrict__ b,
     float eps, int T, int max_pos, float* __restrict__ x, unsigned short* __restrict__ xp,
-    int np) {
+    int np, const uint32_t* __restrict__ node_mask, int mask_L, const int* __restrict__ cu,
+    int n) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= T) return;
   const int id = tok_ids[row];
-  int p = tok_pos[row];
-  p = p < 0 ? 0 : (p >= max_pos ? max_pos - 1 : p);  // bound-check (GCB hazard)
-  const float* we = wemb + (size_t)id * AE_HIDDEN;
+  const int p_raw = tok_pos[row];
+  const int p = p_raw < 0 ? 0 : (p_raw >= max_pos ? max_pos - 1 : p_raw);  // GCB hazard, App. A
   const float* pe = pemb + (size_t)p * AE_HIDDEN;
+  float w[12];
+  if (node_mask && p_raw == 0) {
+    // GraphCodeBERT data-flow node (GraphCodeBERT/Defect-detection/code/model.py:27-33): its input
+    // embedding is the mean word embedding of the code tokens (position >= 2) its mask row
+    // attends; 0 when it attends none (0 / (0 + 1e-10)).  Rows are pad-compacted with trailing
+    // pads only, so the compacted index of a token equals its column in the mask row.
+    int lo = 0, hi = n;  // sequence s with cu[s] <= row < cu[s+1]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (cu[mid] <= row) lo = mid; else hi = mid;
+    }
+    const int base = cu[lo], len = cu[lo + 1] - base;
+    const uint32_t* mrow = node_mask + ((size_t)lo * mask_L + (row - base)) * (mask_L / 32);
+#pragma unroll
+    for (int e = 0; e < 12; ++e) w[e] = 0.f;
+    int cnt = 0;
+    for (int wd = 0; wd * 32 < len; ++wd) {
+      uint32_t bits = mrow[wd];
+      if (len - wd * 32 < 32) bits &= (1u << (len - wd * 32)) - 1u;
+      while (bits) {
+        const int j = wd * 32 + __builtin_ctz(bits);
+        bits &= bits - 1u;
+        if (tok_pos[base + j] < 2) continue;
+        ++cnt;
+        const float* te = wemb + (size_t)tok_ids[base + j] * AE_HIDDEN;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const floatx4 a = *reinterpret_cast<const floatx4*>(te + c * 256 + lane * 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[4 * c + e] += a[e];
+        }
+      }
+    }
+    const float inv = 1.0f / ((float)cnt + 1e-10f);
+#pragma unroll
+    for (int e = 0; e < 12; ++e) w[e] *= inv;
+  } else {
+    const float* we = wemb + (size_t)id * AE_HIDDEN;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const floatx4 a = *reinterpret_cast<const floatx4*>(we + c * 256 + lane * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w[4 * c + e] = a[e];
+    }
+  }
   float v[12];
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     const int col = c * 256 + lane * 4;
-    const floatx4 a = *reinterpret_cast<const floatx4*>(we + col);
     const floatx4 bb = *reinterpret_cast<const floatx4*>(pe + col);
     const floatx4 t = *reinterpret_cast<const floatx4*>(temb + col);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[4 * c + e] = (a[e] + t[e]) + bb[e];
+    for (int e = 0; e < 4; ++e) v[4 * c + e] = (w[4 * c + e] + t[e]) + bb[e];
   }
   const size_t o = (size_t)row * AE_HIDDEN;
   ln_row_store(v, g, b, eps, x + o, lane, xp ? xp + o * np : nullptr, np);
@@ -320,10 +364,11 @@ hipError_t ae_launch_nll_rows(const float* logits, const int* target, int T, int
 hipError_t ae_launch_embed_ln(const int* tok_ids, const int* tok_pos, const float* wemb,
                               const float* pemb, const float* temb, const float* g, const float* b,
                               float eps, int T, int max_pos, float* x, unsigned short* xp,
-                              int np, hipStream_t st) {
+                              int np, const uint32_t* node_mask, int mask_L, const int* cu, int n,
+                              hipStream_t st) {
   if (T <= 0) return hipSuccess;
   hipLaunchKernelGGL(embed_ln_kernel, dim3((T + 3) / 4), dim3(256), 0, st, tok_ids, tok_pos, wemb,
-                     pemb, temb, g, b, eps, T, max_pos, x, xp, np);
+                     pemb, temb, g, b, eps, T, max_pos, x, xp, np, node_mask, mask_L, cu, n);
   return hipGetLastError();
 }
 hipError_t ae_launch_layernorm(const float* in, const float* g, const float* b, float eps, int T,

@@ -33,7 +33,7 @@ class AeWeightView(ctypes.Structure):
 
 
 # every symbol include/alert_engine.h declares (checked by tests/test_abi.py)
-EXPORTS = ("ae_create", "ae_destroy", "ae_score", "ae_encode", "ae_encode_ex", "ae_mlm_topk",
+EXPORTS = ("ae_create", "ae_destroy", "ae_score", "ae_score_graph", "ae_encode", "ae_encode_ex", "ae_mlm_topk",
            "ae_mlm_nll", "ae_splice",
            "ae_topk", "ae_cosine_rank", "ae_set_profiling", "ae_kernel_time", "ae_last_error",
            "ae_version")
@@ -59,6 +59,7 @@ def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
                               ctypes.POINTER(vp)]
     lib.ae_destroy.argtypes = [vp]
     lib.ae_score.argtypes = [vp, vp, vp, vp, vp, i32, i32, vp, vp]
+    lib.ae_score_graph.argtypes = [vp, vp, vp, vp, vp, i32, i32, vp, vp]
     lib.ae_encode.argtypes = [vp, vp, vp, i32, i32, vp, vp]
     lib.ae_encode_ex.argtypes = [vp, vp, vp, i32, i32, i32, i32, i32, vp, vp]
     lib.ae_mlm_topk.argtypes = [vp, vp, i32, i32, vp, vp, vp]
@@ -155,6 +156,27 @@ class Engine:
         _check(self.lib.ae_score(self.handle, _ptr(ids), ctypes.c_void_p(lens.ctypes.data),
                                  _ptr(pos), _ptr(mask_bits), n, L, _ptr(out), _stream(stream)),
                "ae_score")
+        return out
+
+    def score_graph(self, ids, lens: np.ndarray, pos, mask_bits, out=None, stream=None):
+        """GraphCodeBERT forward (data-flow node averaging + explicit positions + data-flow mask).
+        ids/pos: device int32 [n, L]; mask_bits: device int32/uint32 [n, L, L/32]; lens: host
+        int32 [n] leading columns that take part, pads included (normally L)."""
+        import torch
+
+        n, L = ids.shape
+        assert ids.dtype == torch.int32 and ids.is_cuda and ids.is_contiguous()
+        assert pos.shape == (n, L) and pos.dtype == torch.int32 and pos.is_contiguous()
+        assert L % 32 == 0 and mask_bits.shape == (n, L, L // 32) and mask_bits.is_contiguous()
+        assert mask_bits.element_size() == 4
+        lens = np.ascontiguousarray(lens, dtype=np.int32)
+        assert lens.shape == (n,)
+        n_out = n // 2 if self.head == "pair2" else n
+        if out is None:
+            out = torch.empty((n_out, self.out_cols), dtype=torch.float32, device=ids.device)
+        _check(self.lib.ae_score_graph(self.handle, _ptr(ids), ctypes.c_void_p(lens.ctypes.data),
+                                       _ptr(pos), _ptr(mask_bits), n, L, _ptr(out),
+                                       _stream(stream)), "ae_score_graph")
         return out
 
     def encode(self, ids, lens: np.ndarray, attend_pad: bool = False, row0: int = 0,

@@ -1,0 +1,280 @@
+"""GraphCodeBERT victims: data-flow featurisation, the graph-guided attention mask, and the drop-in
+`Model` whose forward averages data-flow node embeddings (ae_score_graph).
+
+Mirrors:
+  convert_code_to_features (GCB)   GraphCodeBERT/Defect-detection/code/attacker.py:30-63
+  pair features (clone)            GraphCodeBERT/clonedetection/code/attacker.py:33-72
+  GraphCodeDataset / CodePairDataset  utils.py:540-639
+  Model.forward / get_results      GraphCodeBERT/Defect-detection/code/model.py:24-60,
+                                   GraphCodeBERT/clonedetection/code/model.py:41-85
+  extract_dataflow                 python_parser/run_parser.py:190-216 (DFG from csrc/host/dfg.cpp)
+
+The reference builds a bool [L, L] mask per query in Python loops and ships it to the GPU as
+L*L bytes; here the mask is built with numpy slices and shipped bit-packed (uint32 [L, L/32],
+bit j of word w = key 32*w + j), 8x less host->device traffic, which is what the attention kernel
+reads directly.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .host import Example
+from .model import Model
+
+DFG_REL = ("comesFrom", "computedFrom")
+
+
+class GraphInputFeatures:
+    """GraphCodeBERT/Defect-detection/code/run.py InputFeatures (input_tokens, input_ids,
+    position_idx, dfg_to_code, dfg_to_dfg, idx, label)."""
+
+    def __init__(self, input_tokens, input_ids, position_idx, dfg_to_code, dfg_to_dfg, idx, label):
+        self.input_tokens = input_tokens
+        self.input_ids = input_ids
+        self.position_idx = position_idx
+        self.dfg_to_code = dfg_to_code
+        self.dfg_to_dfg = dfg_to_dfg
+        self.idx = str(idx)
+        self.label = label
+
+
+def extract_dataflow(code: str, lang: str = "c"):
+    """run_parser.py:190-216 -> (DFG sorted by leaf index, index_table, code_tokens).  DFG entries
+    are (code, idx, relation, [from names], [from idx]) as DFG_c builds them; index_table is not
+    reproduced (no caller on the query path reads it) and is returned as None."""
+    ex = Example(code, lang)
+    toks = ex.leaves(identifiers=True)
+    dfg = [(toks[i], i, DFG_REL[int(comp)], [toks[j] for j in fr], fr) for i, comp, fr in ex.dfg()]
+    return dfg, None, toks
+
+
+class _LeafIds:
+    """Per-tokenizer cache of `tokenize('@ ' + leaf)[1:]` ids (attacker.py:35): leaf strings repeat
+    heavily across a mutant population, so each distinct leaf is tokenised once."""
+
+    def __init__(self, tok):
+        self.tok = tok
+        self.first: dict[str, list[int]] = {}
+        self.rest: dict[str, list[int]] = {}
+
+    def __call__(self, leaf: str, first: bool) -> list[int]:
+        d = self.first if first else self.rest
+        r = d.get(leaf)
+        if r is None:
+            r = self.tok.encode_ids(leaf) if first else self.tok.encode_ids("@ " + leaf)[1:]
+            d[leaf] = r
+        return r
+
+
+def _leaf_ids(tokenizer):
+    c = getattr(tokenizer, "_apmc_leaf_ids", None)
+    if c is None:
+        c = _LeafIds(tokenizer)
+        tokenizer._apmc_leaf_ids = c
+    return c
+
+
+def convert_code_to_features(code, tokenizer, label, args, lang: str = "c"):
+    """GraphCodeBERT/Defect-detection/code/attacker.py:30-63 (code_length + data_flow_length
+    row; DFG nodes appended as <unk> ids at position 0; pads at position pad_id)."""
+    code = " ".join(code.split())
+    dfg, _, code_tokens = extract_dataflow(code, lang)
+    leaf = _leaf_ids(tokenizer)
+    runs = [leaf(x, idx == 0) for idx, x in enumerate(code_tokens)]
+    ends = np.cumsum([0] + [len(r) for r in runs])  # ori2cur_pos[i] = (ends[i], ends[i+1])
+    flat = [y for r in runs for y in r]
+    total = args.code_length + args.data_flow_length
+    flat = flat[:total - 2 - min(len(dfg), args.data_flow_length)]
+    pad, cls, sep, unk = (tokenizer.pad_token_id, tokenizer.cls_token_id, tokenizer.sep_token_id,
+                          tokenizer.unk_token_id)
+    source_ids = [cls] + flat + [sep]
+    position_idx = list(range(pad + 1, pad + 1 + len(source_ids)))
+    dfg = dfg[:total - len(source_ids)]
+    source_ids += [unk] * len(dfg)
+    position_idx += [0] * len(dfg)
+    padding = total - len(source_ids)
+    position_idx += [pad] * padding
+    source_ids += [pad] * padding
+    reverse_index = {x[1]: i for i, x in enumerate(dfg)}
+    dfg_to_dfg = [[reverse_index[i] for i in x[-1] if i in reverse_index] for x in dfg]
+    dfg_to_code = [(int(ends[x[1]]) + 1, int(ends[x[1] + 1]) + 1) for x in dfg]
+    # input_tokens (strings) are not read by any query-path consumer
+    return GraphInputFeatures(None, source_ids, position_idx, dfg_to_code, dfg_to_dfg, 0, label)
+
+
+def graph_mask(input_ids, position_idx, dfg_to_code, dfg_to_dfg, L: int | None = None) -> np.ndarray:
+    """GraphCodeDataset.__getitem__'s graph-guided mask (utils.py:547-570) as bool [L, L]."""
+    pos = np.asarray(position_idx)
+    ids = np.asarray(input_ids)
+    L = L or len(pos)
+    m = np.zeros((L, L), dtype=bool)
+    node_index = int((pos > 1).sum())
+    max_length = int((pos != 1).sum())
+    m[:node_index, :node_index] = True  # sequence attends to sequence
+    m[np.nonzero((ids == 0) | (ids == 2))[0], :max_length] = True  # special tokens attend to all
+    for idx, (a, b) in enumerate(dfg_to_code):  # nodes <-> the code tokens they come from
+        if a < node_index and b < node_index:
+            m[idx + node_index, a:b] = True
+            m[a:b, idx + node_index] = True
+    n_pos = len(pos)
+    for idx, nodes in enumerate(dfg_to_dfg):  # nodes attend to adjacent nodes
+        cols = [a + node_index for a in nodes if a + node_index < n_pos]
+        if cols:
+            m[idx + node_index, cols] = True
+    return m
+
+
+def pack_mask(m: np.ndarray) -> np.ndarray:
+    """bool [..., L, L] -> int32 [..., L, L/32] (bit j of word w = key 32*w + j)."""
+    L = m.shape[-1]
+    if L % 32:
+        raise ValueError(f"mask width {L} is not a multiple of 32")
+    return np.packbits(m, axis=-1, bitorder="little").view("<i4")
+
+
+class GraphCodeDataset:
+    """utils.py:540-576.  Items are the reference's (ids, attn_mask bool [L,L], pos, label)
+    tensors; `packed()` is the engine's fast path (no bool mask materialised per query)."""
+
+    def __init__(self, examples, args=None):
+        self.examples = examples
+        self.args = args
+
+    def __len__(self):
+        return len(self.examples)
+
+    def __getitem__(self, item):
+        import torch
+
+        f = self.examples[item]
+        m = graph_mask(f.input_ids, f.position_idx, f.dfg_to_code, f.dfg_to_dfg)
+        return (torch.tensor(f.input_ids), torch.tensor(m), torch.tensor(f.position_idx),
+                torch.tensor(f.label))
+
+    def packed(self):
+        """-> ids int32 [n, L], pos int32 [n, L], mask bits int32 [n, L, L/32]."""
+        ids = np.asarray([f.input_ids for f in self.examples], dtype=np.int32)
+        pos = np.asarray([f.position_idx for f in self.examples], dtype=np.int32)
+        bits = np.stack([pack_mask(graph_mask(f.input_ids, f.position_idx, f.dfg_to_code,
+                                              f.dfg_to_dfg)) for f in self.examples])
+        return ids, pos, bits
+
+
+class GraphPairFeatures:
+    """GraphCodeBERT/clonedetection/code/run.py InputFeatures of a pair (field suffixes _1/_2)."""
+
+    def __init__(self, f1: GraphInputFeatures, f2: GraphInputFeatures, label, url1="", url2=""):
+        for k in ("input_tokens", "input_ids", "position_idx", "dfg_to_code", "dfg_to_dfg"):
+            setattr(self, k + "_1", getattr(f1, k))
+            setattr(self, k + "_2", getattr(f2, k))
+        self.label = label
+        self.url1, self.url2 = url1, url2
+
+
+class CodePairDataset:
+    """utils.py:578-639 — items (ids1, pos1, mask1, ids2, pos2, mask2, label)."""
+
+    def __init__(self, examples, args=None):
+        self.examples = examples
+        self.args = args
+
+    def __len__(self):
+        return len(self.examples)
+
+    def __getitem__(self, item):
+        import torch
+
+        f = self.examples[item]
+        out = []
+        for s in ("_1", "_2"):
+            ids, pos = getattr(f, "input_ids" + s), getattr(f, "position_idx" + s)
+            m = graph_mask(ids, pos, getattr(f, "dfg_to_code" + s), getattr(f, "dfg_to_dfg" + s))
+            out += [torch.tensor(ids), torch.tensor(pos), torch.tensor(m)]
+        return tuple(out) + (torch.tensor(f.label),)
+
+    def packed(self):
+        """Rows interleaved code1, code2 per pair (clonedetection/code/model.py:42-45)."""
+        ids, pos, bits = [], [], []
+        for f in self.examples:
+            for s in ("_1", "_2"):
+                i, p = getattr(f, "input_ids" + s), getattr(f, "position_idx" + s)
+                ids.append(i)
+                pos.append(p)
+                bits.append(pack_mask(graph_mask(i, p, getattr(f, "dfg_to_code" + s),
+                                                 getattr(f, "dfg_to_dfg" + s))))
+        return (np.asarray(ids, dtype=np.int32), np.asarray(pos, dtype=np.int32),
+                np.stack(bits))
+
+
+def _np(x):
+    if hasattr(x, "detach"):
+        x = x.detach().cpu().numpy()
+    return np.asarray(x)
+
+
+def _pack_items(dataset, pair: bool):
+    """Generic dataset of the reference's tuples -> packed arrays (rows interleaved for pairs)."""
+    ids, pos, bits = [], [], []
+    for i in range(len(dataset)):
+        it = dataset[i]
+        groups = [(it[0], it[1], it[2]), (it[3], it[4], it[5])] if pair else \
+            [(it[0], it[2], it[1])]  # (ids, mask, pos, label) -> (ids, pos, mask)
+        for a, p, m in groups:
+            ids.append(_np(a).reshape(-1))
+            pos.append(_np(p).reshape(-1))
+            bits.append(pack_mask(_np(m).astype(bool)))
+    return (np.asarray(ids, dtype=np.int32), np.asarray(pos, dtype=np.int32), np.stack(bits))
+
+
+class GraphModel(Model):
+    """GraphCodeBERT victim: task "devign" (sigmoid head, GraphCodeBERT/Defect-detection) or
+    "clone" (pair head over interleaved code1/code2 rows, GraphCodeBERT/clonedetection)."""
+
+    def __init__(self, encoder, config=None, tokenizer=None, args=None, task: str = "devign",
+                 precision: str = "fp32", device: int = 0):
+        super().__init__(encoder, config, tokenizer, args, task=task, precision=precision,
+                         device=device)
+
+    def score_packed(self, ids: np.ndarray, pos: np.ndarray, bits: np.ndarray) -> np.ndarray:
+        import torch
+
+        n, L = ids.shape
+        if bits.shape != (n, L, L // 32) or pos.shape != (n, L):
+            raise ValueError(f"graph inputs disagree: ids {ids.shape} pos {pos.shape} "
+                             f"mask bits {bits.shape}")
+        outs = []
+        dev = f"cuda:{self.engine.device}"
+        step = self.max_rows_per_launch
+        for s in range(0, n, step):
+            e = min(n, s + step)
+            # every column takes part (pads too): a fully masked query row attends all L keys
+            # uniformly under HF's finfo.min additive mask (alert_engine.h ae_score_graph)
+            lens = np.full((e - s,), L, dtype=np.int32)
+            t = lambda a: torch.from_numpy(np.ascontiguousarray(a[s:e])).to(dev)  # noqa: E731
+            outs.append(self.engine.score_graph(t(ids), lens, t(pos), t(bits)))
+        return torch.cat(outs, 0).cpu().numpy() if len(outs) > 1 else outs[0].cpu().numpy()
+
+    def get_results(self, dataset, batch_size=None, threshold: float = 0.5):
+        """(probs, pred_labels) of GraphCodeBERT/*/code/model.py get_results."""
+        self.query += len(dataset)
+        if len(dataset) == 0:
+            return [], []
+        if hasattr(dataset, "packed"):
+            ids, pos, bits = dataset.packed()
+        else:
+            ids, pos, bits = _pack_items(dataset, self.task == "clone")
+        return self._format(self.score_packed(ids, pos, bits), threshold)
+
+    def dataset_from_texts(self, texts, tokenizer, args, label=0):
+        """Mutant texts -> GraphCodeDataset (the GCB attacker featurises every mutant text with
+        convert_code_to_features, GraphCodeBERT/Defect-detection/code/attacker.py:30-63)."""
+        return GraphCodeDataset([convert_code_to_features(t, tokenizer, label, args)
+                                 for t in texts], args)
+
+    def get_results_population(self, example, tokenizer, population, mode: int, block_size: int,
+                               threshold: float = 0.5):
+        """A population of chromosomes of one program: mutant texts (host get_example(_batch))
+        -> data-flow features -> ae_score_graph.  len(population) queries."""
+        texts = [example.mutant_text(pairs, mode) for pairs in population]
+        return self.get_results(self.dataset_from_texts(texts, tokenizer, self.args), None,
+                                threshold)

@@ -100,6 +100,14 @@ class Model:
             logits = self._score_ids(stack_ids(dataset))
         return self._format(logits, threshold)
 
+    def dataset_from_texts(self, texts, tokenizer, args, label=0):
+        """Mutant texts -> the dataset get_results consumes (convert_code_to_features of every
+        text, CodeXGLUE/Defect-detection/code/attacker.py:38-45, batched in the host library)."""
+        from .utils import IdsDataset
+
+        ids, lens = tokenizer.featurize(list(texts), args.block_size)
+        return IdsDataset(ids, lens)
+
     def get_results_population(self, example, tokenizer, population, mode: int, block_size: int,
                                threshold: float = 0.5):
         """Score a population of chromosomes of one program (len(population) queries).

@@ -17,7 +17,10 @@
  *                    (CodeXGLUE/Defect-detection/code/model.py:24-59; clone head
  *                    CodeXGLUE/Clone-detection-BigCloneBench/code/model.py:13-85;
  *                    authorship head CodeXGLUE/Authorship-Attribution/code/model.py:13-91;
- *                    GraphCodeBERT GraphCodeBERT/Defect-detection/code/model.py:24-45)
+ *                    GraphCodeBERT mask/positions without node averaging)
+ *   ae_score_graph<- GraphCodeBERT Model.forward incl. data-flow node averaging
+ *                    (GraphCodeBERT/Defect-detection/code/model.py:24-45,
+ *                    GraphCodeBERT/clonedetection/code/model.py:41-64)
  *   ae_splice     <- the text-level mutant construction + re-tokenisation
  *                    (python_parser/run_parser.py:218-266 get_example/get_example_batch,
  *                    CodeXGLUE/Defect-detection/code/attacker.py:38-45 convert_code_to_features)
@@ -111,6 +114,17 @@ int ae_destroy(ae_engine *eng);
  */
 int ae_score(ae_engine *eng, const int32_t *ids, const int32_t *lens, const int32_t *pos,
              const uint32_t *mask_bits, int32_t n, int32_t L, float *probs_out, void *stream);
+
+/* GraphCodeBERT Model.forward (GraphCodeBERT/Defect-detection/code/model.py:24-45, clone pair
+ * GraphCodeBERT/clonedetection/code/model.py:41-64): ae_score with explicit positions and the
+ * data-flow mask, where each data-flow node row (pos == 0) first takes as its input embedding the
+ * mean word embedding of the code tokens (pos >= 2) its mask row attends (model.py:27-33).
+ * pos and mask_bits are required.  Here lens[i] is the number of leading columns of row i that
+ * take part, pad ids included (normally L): as in HF's additive finfo(f32).min mask, a query row
+ * whose mask excludes every key (a data-flow node whose code span was truncated away, a pad row)
+ * attends all lens[i] keys uniformly, so pads are not dropped on this path. */
+int ae_score_graph(ae_engine *eng, const int32_t *ids, const int32_t *lens, const int32_t *pos,
+                   const uint32_t *mask_bits, int32_t n, int32_t L, float *probs_out, void *stream);
 
 /* Encoder hidden states of n sequences: hidden_out device float [n, L, hidden]
  * (rows of pad positions are left untouched). */

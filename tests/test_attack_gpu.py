@@ -89,3 +89,76 @@ def test_driver_runs_and_counts(victim):
     assert out["examples"] == 6
     assert out["queries"] == sum(r["queries"] for r in out["records"])
     assert all(r["queries"] >= 1 for r in out["records"])
+
+
+class _GraphVictim(attack_ref.Victim):
+    """Text oracle victim for GraphCodeBERT: every mutant text featurised by oracle/graph_ref.py
+    (reference-loop features and mask), scored by the same engine's graph forward."""
+
+    def __init__(self, model, code0, args):
+        super().__init__(None, 0)
+        self.model, self.code0, self.args = model, code0, args
+
+    def _feats(self, code):
+        from apmc_amd.graph import extract_dataflow
+        from oracle import graph_ref
+        dfg, _, toks = extract_dataflow(" ".join(code.split()), "c")
+        ids, pos, d2c, d2d = graph_ref.convert_code_to_features(
+            dfg, toks, self.args.code_length, self.args.data_flow_length)
+        L = len(ids)
+        m = graph_ref.graph_mask(ids, pos, d2c, d2d, L)
+        return ids, pos, np.packbits(m, axis=-1, bitorder="little").view("<i4")
+
+    def texts(self, codes):
+        fs = [self._feats(c) for c in codes]
+        self.query += len(fs)
+        p = self.model.score_packed(np.array([f[0] for f in fs], np.int32),
+                                    np.array([f[1] for f in fs], np.int32),
+                                    np.stack([f[2] for f in fs]))[:, 0]
+        return [[1 - x, x] for x in p], [1 if x > 0.5 else 0 for x in p]
+
+    def ids(self, _ids0):
+        return self.texts([self.code0])
+
+
+def test_graphcodebert_greedy_then_ga_matches_text_oracle():
+    """GraphCodeBERT Devign victim (GraphCodeBERT/Defect-detection/code/attacker.py): mutants are
+    re-featurised with the data-flow graph; product Attacker + GraphModel vs the text oracle."""
+    import types
+    from apmc_amd.attacker import Attacker
+    from apmc_amd.drivers import load_fixture
+    from apmc_amd.graph import GraphCodeDataset, GraphModel, convert_code_to_features
+    from apmc_amd.host import Tokenizer
+    from apmc_amd.weights import synthetic_state_dict
+
+    args = types.SimpleNamespace(code_length=256, data_flow_length=64, block_size=320,
+                                 eval_batch_size=16, lang="c")
+    model = GraphModel(synthetic_state_dict(seed=5, head="sigmoid1", out_std=8.0), args=args)
+    codes, subs, labels = load_fixture(FIXTURE, 0, 120)
+    tok = Tokenizer()
+    att = Attacker(args, model, tok, None, tok, 1, 0)
+    kinds = []
+    for i in _pick(codes, subs, 5):
+        code, sb, lab = codes[i], subs[i], labels[i]
+        ex = GraphCodeDataset([convert_code_to_features(code, tok, lab, args)], args)[0]
+        random.seed(2000 + i)
+        q0 = model.query
+        res = att.greedy_attack(ex, code, sb)
+        kind = "greedy"
+        if res[6] == -1:
+            res = att.ga_attack(ex, code, sb, initial_replace=res[11])
+            kind = "ga"
+        q_prod = model.query - q0
+        random.seed(2000 + i)
+        v = _GraphVictim(model, code, args)
+        ref = attack_ref.greedy(v, np.zeros(1), lab, code, sb)
+        if ref["is_success"] == -1:
+            ref = attack_ref.ga(v, np.zeros(1), lab, code, sb, initial_replace=ref["replaced"],
+                                eval_batch_size=16)
+        assert res[6] == ref["is_success"], (i, kind)
+        assert q_prod == v.query, (i, kind, q_prod, v.query)
+        if res[6] == 1:
+            assert res[2] == ref["adv_code"], i
+            assert dict(res[11]) == ref["replaced"]
+        kinds.append((kind, res[6]))
+    assert kinds

@@ -1,0 +1,146 @@
+"""GraphCodeBERT path: data-flow featurisation + graph-guided mask (CPU, bit-exact against
+oracle/graph_ref.py on the reference's Devign fixture functions) and the node-averaged forward
+through ae_score_graph (GPU, probabilities within 1e-4 of the oracle in fp32 / f32x3)."""
+import types
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, synthetic_sd
+from oracle import graph_ref
+
+DEVIGN = ROOT / "data" / "devign" / "test_subs_0_400.jsonl"
+PROB_TOL = 1e-4
+# GraphCodeBERT Devign attack defaults (GraphCodeBERT/Defect-detection/code/attack.py:460-467)
+ARGS = types.SimpleNamespace(code_length=256, data_flow_length=64, block_size=512,
+                             eval_batch_size=64)
+
+
+def _funcs(limit):
+    import json
+    out = []
+    with open(DEVIGN) as f:
+        for i, line in enumerate(f):
+            if i >= limit:
+                break
+            js = json.loads(line)
+            out.append((js["func"], int(js["target"])))
+    return out
+
+
+@pytest.fixture(scope="module")
+def tok():
+    from apmc_amd.host import Tokenizer
+    return Tokenizer()
+
+
+def _oracle_features(code, args):
+    from apmc_amd.graph import extract_dataflow
+    code = " ".join(code.split())
+    dfg, _, toks = extract_dataflow(code, "c")
+    return graph_ref.convert_code_to_features(dfg, toks, args.code_length, args.data_flow_length)
+
+
+@pytest.mark.parametrize("code_length,dfl", [(256, 64), (512, 128), (64, 32)])
+def test_features_and_mask_match_oracle(tok, code_length, dfl):
+    from apmc_amd.graph import convert_code_to_features, graph_mask, pack_mask
+    args = types.SimpleNamespace(code_length=code_length, data_flow_length=dfl)
+    L = code_length + dfl
+    n_nodes = 0
+    for code, label in _funcs(60):
+        f = convert_code_to_features(code, tok, label, args)
+        ids, pos, d2c, d2d = _oracle_features(code, args)
+        assert f.input_ids == ids
+        assert f.position_idx == pos
+        assert [tuple(x) for x in f.dfg_to_code] == [tuple(x) for x in d2c]
+        assert f.dfg_to_dfg == d2d
+        m = graph_mask(f.input_ids, f.position_idx, f.dfg_to_code, f.dfg_to_dfg)
+        np.testing.assert_array_equal(m, graph_ref.graph_mask(ids, pos, d2c, d2d, L))
+        bits = pack_mask(m).view(np.uint32)
+        for r in (0, 5, L - 1):  # bit layout: bit j of word w = key 32 w + j
+            np.testing.assert_array_equal(
+                np.array([(bits[r, k // 32] >> (k % 32)) & 1 for k in range(L)], bool), m[r])
+        n_nodes += sum(p == 0 for p in pos)
+    assert n_nodes > 0
+
+
+def test_dataset_items_have_reference_shapes(tok):
+    from apmc_amd.graph import (CodePairDataset, GraphCodeDataset, GraphPairFeatures,
+                                convert_code_to_features)
+    fs = [convert_code_to_features(c, tok, y, ARGS) for c, y in _funcs(3)]
+    L = ARGS.code_length + ARGS.data_flow_length
+    ids, m, pos, lab = GraphCodeDataset(fs)[1]
+    assert ids.shape == (L,) and m.shape == (L, L) and pos.shape == (L,) and int(lab) == fs[1].label
+    ids, pos, bits = GraphCodeDataset(fs).packed()
+    assert ids.shape == (3, L) and bits.shape == (3, L, L // 32)
+    item = CodePairDataset([GraphPairFeatures(fs[0], fs[1], 1)])[0]
+    assert len(item) == 7 and item[2].shape == (L, L) and item[5].shape == (L, L)
+
+
+# ---------------------------------------------------------------------------------------- GPU
+def _gmodel(task, precision="fp32"):
+    from apmc_amd.graph import GraphModel
+    cache = _gmodel.__dict__.setdefault("cache", {})
+    key = (task, precision)
+    if key not in cache:
+        head, nl, seed = ("sigmoid1", 1, 0) if task == "devign" else ("pair2", 2, 2)
+        cache[key] = GraphModel(synthetic_sd(seed, head, nl), config=nl, args=ARGS, task=task,
+                                precision=precision)
+    return cache[key]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["fp32", "f32x3"])
+def test_graph_devign_matches_oracle(gpu, tok, precision):
+    from apmc_amd.graph import GraphCodeDataset, convert_code_to_features
+    funcs = _funcs(6)
+    fs = [convert_code_to_features(c, tok, y, ARGS) for c, y in funcs]
+    L = ARGS.code_length + ARGS.data_flow_length
+    ids = np.array([f.input_ids for f in fs])
+    pos = np.array([f.position_idx for f in fs])
+    m = np.stack([graph_ref.graph_mask(f.input_ids, f.position_idx, f.dfg_to_code, f.dfg_to_dfg,
+                                       L) for f in fs])
+    ref = graph_ref.graph_score(synthetic_sd(0, "sigmoid1"), ids, m, pos, "sigmoid1")
+    model = _gmodel("devign", precision)
+    q0 = model.query
+    probs, preds = model.get_results(GraphCodeDataset(fs, ARGS), 64)
+    assert model.query - q0 == len(fs)
+    got = np.array([p[1] for p in probs])
+    np.testing.assert_allclose(got, ref[:, 0], atol=PROB_TOL, rtol=0)
+    assert preds == [1 if p > 0.5 else 0 for p in got]
+    # the reference's tuple items (bool masks) take the same path
+    ds = GraphCodeDataset(fs, ARGS)
+    probs2, _ = model.get_results([ds[i] for i in range(len(ds))], 64)
+    np.testing.assert_array_equal(np.array(probs2), np.array(probs))
+
+
+@pytest.mark.gpu
+def test_graph_node_average_matters(gpu, tok):
+    """Without node averaging (plain ae_score) the probabilities differ: the averaging runs."""
+    import torch
+    from apmc_amd.graph import GraphCodeDataset, convert_code_to_features
+    fs = [convert_code_to_features(c, tok, y, ARGS) for c, y in _funcs(4)]
+    ids, pos, bits = GraphCodeDataset(fs).packed()
+    model = _gmodel("devign")
+    a = model.score_packed(ids, pos, bits)
+    lens = (ids != 1).sum(1).astype(np.int32)
+    b = model.engine.score(torch.from_numpy(ids).cuda(), lens, pos=torch.from_numpy(pos).cuda(),
+                           mask_bits=torch.from_numpy(bits).cuda()).cpu().numpy()
+    assert np.abs(a - b).max() > 1e-6
+
+
+@pytest.mark.gpu
+def test_graph_clone_pairs_match_oracle(gpu, tok):
+    from apmc_amd.graph import CodePairDataset, GraphPairFeatures, convert_code_to_features
+    fs = [convert_code_to_features(c, tok, y, ARGS) for c, y in _funcs(6)]
+    pairs = [GraphPairFeatures(fs[i], fs[i + 1], i % 2) for i in range(0, 6, 2)]
+    ds = CodePairDataset(pairs, ARGS)
+    ids, pos, bits = ds.packed()
+    L = ids.shape[1]
+    m = np.stack([graph_ref.graph_mask(f.input_ids, f.position_idx, f.dfg_to_code, f.dfg_to_dfg,
+                                       L) for f in fs])
+    ref = graph_ref.graph_score(synthetic_sd(2, "pair2", 2), ids, m, pos, "pair2")
+    model = _gmodel("clone")
+    probs, preds = model.get_results(ds, 64)
+    np.testing.assert_allclose(np.asarray(probs), ref, atol=PROB_TOL, rtol=0)
+    assert preds == [0 if p[0] > 0.5 else 1 for p in ref]
