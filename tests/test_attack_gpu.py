@@ -162,3 +162,42 @@ def test_graphcodebert_greedy_then_ga_matches_text_oracle():
             assert dict(res[11]) == ref["replaced"]
         kinds.append((kind, res[6]))
     assert kinds
+
+
+@pytest.mark.parametrize("kind", ["mcmc", "mcmc_random"])
+def test_mhm_matches_text_oracle(victim, kind):
+    """MHM-NS baseline (attacker.py:466-738): product MHM_Attacker (host mutants, engine scoring)
+    vs oracle/mhm_ref.py over text, same Python `random` seed: identical outcome, adversarial
+    code, replacement chain and query count."""
+    from apmc_amd.attacker import MHM_Attacker
+    from apmc_amd.drivers import AttackArgs, load_fixture
+    from apmc_amd.host import Tokenizer
+    from apmc_amd.utils import isUID
+    from oracle import mhm_ref
+
+    codes, subs, labels = load_fixture(FIXTURE, 0, 120)
+    tok = Tokenizer()
+    args = AttackArgs(block_size=BLOCK, eval_batch_size=32)
+    vocab = sorted({w for s in subs[:60] for v in s.values() for w in v})
+    idx2token = vocab if kind == "mcmc_random" else None
+    att = MHM_Attacker(args, victim, None, tok, {w: i for i, w in enumerate(vocab)}, vocab)
+    seen = []
+    for i in _pick(codes, subs, 5):
+        code, sb, lab = codes[i], subs[i], labels[i]
+        random.seed(3000 + i)
+        q0 = victim.query
+        res = getattr(att, kind)(tok, sb, code, lab, _n_candi=30, _max_iter=12)
+        q_prod = victim.query - q0
+        random.seed(3000 + i)
+        v = attack_ref.Victim(_score_fn(victim), BLOCK)
+        ref = mhm_ref.mcmc(v, isUID, sb, code, lab, n_candi=30, max_iter=12, idx2token=idx2token)
+        assert res["succ"] == ref["succ"], i
+        assert q_prod == v.query, (i, q_prod, v.query)
+        if res["succ"] is not None:
+            assert res["tokens"] == ref["tokens"], i
+            assert res["replace_info"] == ref["replace_info"], i
+            assert res["nb_changed_var"] == ref["nb_changed_var"]
+            assert res["nb_changed_pos"] == ref["nb_changed_pos"]
+            assert res["prog_length"] == ref["prog_length"]
+        seen.append(res["succ"])
+    assert any(s is not None for s in seen)
