@@ -40,6 +40,12 @@ class FakeVictim:
             ids = np.stack([np.asarray(d[0]) for d in dataset])
         return self._fmt(self._p(ids))
 
+    def dataset_from_texts(self, texts, tokenizer, args, label=0):
+        from apmc_amd.utils import IdsDataset
+
+        ids, lens = tokenizer.featurize(list(texts), args.block_size)
+        return IdsDataset(ids, lens)
+
     def get_results_population(self, example, tokenizer, population, mode, block_size):
         self.query += len(population)
         ids, _ = example.mutant_ids(tokenizer, population, block_size, mode)
