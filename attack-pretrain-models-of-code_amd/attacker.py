@@ -324,8 +324,27 @@ class MHM_Attacker:
         self.tokenizer_mlm = tokenizer_mlm
         self.lang = getattr(args, "lang", "c")
 
+    # The MCMC loop is written once, as a generator: every victim query is a `yield (ids, lens)`
+    # that receives `(probs, preds)` back.  `_run` answers each request with its own get_results
+    # call (the reference's one-example-at-a-time behaviour); `mcmc_batched` answers the pending
+    # requests of many examples with ONE device batch.  Rows are scored batch-invariantly, so the
+    # two give identical results; `rng` is the Python `random` module (sequential, as the
+    # reference) or a per-example `random.Random(seed)` (batched: interleaved examples cannot
+    # share one global stream).
     def _run(self, tokenizer, substituions, code, _label, _n_candi, _max_iter, _prob_threshold,
              replace, attack_type):
+        gen = self._run_gen(tokenizer, substituions, code, _label, _n_candi, _max_iter,
+                            _prob_threshold, replace, attack_type, random)
+        try:
+            req = next(gen)
+            while True:
+                req = gen.send(self.classifier.get_results(IdsDataset(*req),
+                                                           self.args.eval_batch_size))
+        except StopIteration as stop:
+            return stop.value
+
+    def _run_gen(self, tokenizer, substituions, code, _label, _n_candi, _max_iter, _prob_threshold,
+                 replace, attack_type, rng):
         identifiers, code_tokens = get_identifiers(code, self.lang)
         prog_length = len(code_tokens)
         processed_code = " ".join(code_tokens)
@@ -342,9 +361,9 @@ class MHM_Attacker:
         old_uid = ""
         res = None
         for iteration in range(1, 1 + _max_iter):
-            res = replace(_tokens=code, _label=_label, _uid=uid,
-                          substitute_dict=variable_substitue_dict, _n_candi=_n_candi,
-                          _prob_threshold=_prob_threshold)
+            res = yield from replace(rng, _tokens=code, _label=_label, _uid=uid,
+                                     substitute_dict=variable_substitue_dict, _n_candi=_n_candi,
+                                     _prob_threshold=_prob_threshold)
             self._print_res(iteration, res)
             if res["status"].lower() in ["s", "a"]:
                 if iteration == 1:
@@ -397,7 +416,58 @@ class MHM_Attacker:
         return self._run(tokenizer, substituions, code, _label, _n_candi, _max_iter,
                          _prob_threshold, self._replace_uid_random, "MHM-Origin")
 
-    def _candidates_result(self, _tokens, _label, selected_uid, candi_token, candi_pairs,
+    def mcmc_batched(self, tokenizer, jobs, _n_candi=30, _max_iter=100, _prob_threshold=0.95,
+                     original=False, max_inflight=64, on_done=None):
+        """Many examples' MCMC chains in flight at once.
+
+        `jobs` = [(substituions, code, label, seed)]; example j runs on `random.Random(seed)`, so
+        its chain is exactly `random.seed(seed); mcmc(...)` (or `mcmc_random` if `original`).  Each
+        round gathers the pending ≤(1+_n_candi)-candidate requests of up to `max_inflight` chains
+        into ONE `get_results` call, so the device sees batches of hundreds of sequences instead of
+        ≤31.  The victim's query counter advances by the same total as the sequential runs.
+        Returns `[(result_dict, queries)]` in job order; `on_done(j, result, queries)` is called as
+        each chain finishes."""
+        replace = self._replace_uid_random if original else self._replace_uid
+        kind = "MHM-Origin" if original else "MHM"
+        out = [None] * len(jobs)
+        live = []  # [job index, generator, pending (ids, lens), queries so far]
+        nxt = 0
+
+        def finish(j, value, q):
+            out[j] = (value, q)
+            if on_done is not None:
+                on_done(j, value, q)
+
+        while nxt < len(jobs) or live:
+            while nxt < len(jobs) and len(live) < max_inflight:
+                subs, code, label, seed = jobs[nxt]
+                gen = self._run_gen(tokenizer, subs, code, label, _n_candi, _max_iter,
+                                    _prob_threshold, replace, kind, random.Random(seed))
+                try:
+                    live.append([nxt, gen, next(gen), 0])
+                except StopIteration as stop:
+                    finish(nxt, stop.value, 0)
+                nxt += 1
+            if not live:
+                break
+            ids = np.concatenate([c[2][0] for c in live], 0)
+            lens = np.concatenate([c[2][1] for c in live], 0)
+            prob, pred = self.classifier.get_results(IdsDataset(ids, lens),
+                                                     self.args.eval_batch_size)
+            still, off = [], 0
+            for c in live:
+                n = c[2][0].shape[0]
+                c[3] += n
+                try:
+                    c[2] = c[1].send((prob[off:off + n], pred[off:off + n]))
+                    still.append(c)
+                except StopIteration as stop:
+                    finish(c[0], stop.value, c[3])
+                off += n
+            live = still
+        return out
+
+    def _candidates_result(self, rng, _tokens, _label, selected_uid, candi_token, candi_pairs,
                            _prob_threshold):
         """Shared tail of __replaceUID / __replaceUID_random (attacker.py:634-670)."""
         # candidate 0 is the unmodified code; the others are get_example(code, uid, c)
@@ -412,7 +482,7 @@ class MHM_Attacker:
             lens = np.concatenate([lens0, lensm], 0)
         else:
             ids, lens = ids0, lens0
-        prob, pred = self.classifier.get_results(IdsDataset(ids, lens), self.args.eval_batch_size)
+        prob, pred = yield (ids, lens)
         candi_tokens = [_tokens] + [None] * len(pops)
 
         def text(i):
@@ -435,42 +505,42 @@ class MHM_Attacker:
         alpha = (1 - prob[candi_idx][_label] + 1e-10) / (1 - prob[0][_label] + 1e-10)
         # the reference reports candi_tokens[i] with i the LAST loop index (attacker.py:662-670)
         i = len(candi_token) - 1
-        status = "r" if (random.uniform(0, 1) > alpha or alpha < _prob_threshold) else "a"
+        status = "r" if (rng.uniform(0, 1) > alpha or alpha < _prob_threshold) else "a"
         return {"status": status, "alpha": alpha, "tokens": text(i), "old_uid": selected_uid,
                 "new_uid": candi_token[i], "old_prob": prob[0], "new_prob": prob[i],
                 "old_pred": pred[0], "new_pred": pred[i],
                 "nb_changed_pos": _tokens.count(selected_uid)}
 
-    def _replace_uid(self, _tokens, _label=None, _uid={}, substitute_dict={}, _n_candi=30,
+    def _replace_uid(self, rng, _tokens, _label=None, _uid={}, substitute_dict={}, _n_candi=30,
                      _prob_threshold=0.95, _candi_mode="random"):
         assert _candi_mode.lower() in ["random", "nearby"]
-        selected_uid = random.sample(list(substitute_dict.keys()), 1)[0]
+        selected_uid = rng.sample(list(substitute_dict.keys()), 1)[0]
         candi_token = [selected_uid]
         pairs = []
         pool = substitute_dict[selected_uid]
-        for c in random.sample(pool, min(_n_candi, len(pool))):
+        for c in rng.sample(pool, min(_n_candi, len(pool))):
             if c in _uid.keys():
                 continue
             if isUID(c):
                 candi_token.append(c)
                 pairs.append(c)
-        return self._candidates_result(_tokens, _label, selected_uid, candi_token, pairs,
-                                       _prob_threshold)
+        return (yield from self._candidates_result(rng, _tokens, _label, selected_uid, candi_token,
+                                                   pairs, _prob_threshold))
 
-    def _replace_uid_random(self, _tokens, _label=None, _uid={}, substitute_dict={},
+    def _replace_uid_random(self, rng, _tokens, _label=None, _uid={}, substitute_dict={},
                             _n_candi=30, _prob_threshold=0.95, _candi_mode="random"):
         assert _candi_mode.lower() in ["random", "nearby"]
-        selected_uid = random.sample(list(substitute_dict.keys()), 1)[0]
+        selected_uid = rng.sample(list(substitute_dict.keys()), 1)[0]
         candi_token = [selected_uid]
         pairs = []
-        for c in random.sample(self.idx2token, _n_candi):
+        for c in rng.sample(self.idx2token, _n_candi):
             if c in _uid.keys():
                 continue
             if isUID(c):
                 candi_token.append(c)
                 pairs.append(c)
-        return self._candidates_result(_tokens, _label, selected_uid, candi_token, pairs,
-                                       _prob_threshold)
+        return (yield from self._candidates_result(rng, _tokens, _label, selected_uid, candi_token,
+                                                   pairs, _prob_threshold))
 
     def _print_res(self, _iter=None, _res=None, _prefix="  => "):
         if not getattr(self.args, "verbose", False):

@@ -127,8 +127,15 @@ def run_gi_attack(model, codes, subs, labels, args: AttackArgs, indices=None, to
 
 
 def run_mhm_attack(model, codes, subs, labels, args: AttackArgs, indices=None, tok=None,
-                   n_candi=30, max_iter=100, prob_threshold=1, original=False):
-    """mhm_attack.py:160-236 (MHM-NS; `original` = MHM with the random-token candidates)."""
+                   n_candi=30, max_iter=100, prob_threshold=1, original=False, max_inflight=1):
+    """mhm_attack.py:160-236 (MHM-NS; `original` = MHM with the random-token candidates).
+
+    max_inflight = 1 is the reference loop (one global `random` stream seeded once).  With
+    max_inflight > 1 the examples' chains run interleaved through `MHM_Attacker.mcmc_batched`:
+    the original-prediction queries of all examples go out as one batch, then up to
+    `max_inflight` chains share every device batch; example `index` then draws from
+    `random.Random(args.seed + index)` — the same per-example seeding `rng="per_example"` gives
+    the GA driver — and records stay in index order."""
     tok = tok or Tokenizer()
     from .attacker import get_identifiers
 
@@ -138,6 +145,24 @@ def run_mhm_attack(model, codes, subs, labels, args: AttackArgs, indices=None, t
     attacker = MHM_Attacker(args, model, None, tok, token2id, id2token)
     order = list(range(len(codes))) if indices is None else list(indices)
     records, t0 = [], time.time()
+    if max_inflight > 1:
+        exs = [_example(tok, codes[i], labels[i], args.block_size) for i in order]
+        _, preds = model.get_results(exs, args.eval_batch_size) if exs else ([], [])
+        by_index, jobs, job_index = {}, [], []
+        for index, p in zip(order, preds):
+            if p != labels[index]:
+                by_index[index] = dict(index=index, is_success=-4, queries=1)
+            else:
+                jobs.append((subs[index], codes[index], labels[index], args.seed + index))
+                job_index.append(index)
+        done = attacker.mcmc_batched(tok, jobs, _n_candi=n_candi, _max_iter=max_iter,
+                                     _prob_threshold=prob_threshold, original=original,
+                                     max_inflight=max_inflight)
+        for index, (res, q) in zip(job_index, done):
+            ok = 1 if res["succ"] else (-1 if res["succ"] is not None else -3)
+            by_index[index] = dict(index=index, is_success=ok, queries=1 + q)
+        records = [by_index[i] for i in order]
+        order = []
     for index in order:
         example = _example(tok, codes[index], labels[index], args.block_size)
         q0 = model.query

@@ -120,6 +120,62 @@ def attack_leg(dev, seconds, rank, world, precision):
             "sharding": "dynamic queue (torch.distributed store counter)"}
 
 
+def mhm_leg(dev, n_examples, seq_seconds, rank, world, precision):
+    """Config-5 baseline workload: MHM-NS (mhm_attack.py, n_candi 30, max_iter 100, threshold 1)
+    over test_subs_0_400 with the CodeBERT Devign victim.  Batched: the first `n_examples` fixture
+    examples (strided over ranks) with every chain in flight at once (`mcmc_batched`); sequential:
+    the reference loop (one ≤31-candidate batch per query round) over the same examples in order
+    until `seq_seconds` are spent, for the comparison."""
+    from apmc_amd.drivers import AttackArgs, load_fixture, run_mhm_attack
+    from apmc_amd.model import Model
+    from apmc_amd.weights import synthetic_state_dict
+
+    codes, subs, labels = load_fixture(ROOT / "data" / "devign" / "test_subs_0_400.jsonl")
+    model = Model(synthetic_state_dict(seed=0, head="sigmoid1"), task="devign",
+                  precision=precision, device=dev.index)
+    args = AttackArgs(block_size=512, eval_batch_size=64, seed=123456)
+    mine = list(range(rank, n_examples, world))
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    out = run_mhm_attack(model, codes, subs, labels, args, indices=mine, max_iter=100,
+                         prob_threshold=1, max_inflight=len(mine))
+    st = np.array([out["examples"], out["total_cnt"], out["success"], out["queries"],
+                   out["wall_s"]], dtype=np.float64)
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor(st, device=dev)
+        g = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(g, t)
+        allst = torch.stack(g).cpu().numpy()
+    else:
+        allst = st[None]
+    ex, cnt, suc, q = allst[:, :4].sum(0)
+    wall = allst[:, 4].max()
+    res = {"workload": "MHM-NS (mhm_attack.py: n_candi 30, max_iter 100) CodeBERT Devign victim, "
+                       f"test_subs_0_400 examples [0, {n_examples}), block 512",
+           "precision": precision, "examples": int(ex), "correctly_classified": int(cnt),
+           "successes": int(suc), "victim_queries": int(q), "wall_s": round(wall, 2),
+           "victim_queries_per_s": round(q / wall, 2),
+           "attacked_examples_per_min": round(60 * ex / wall, 3),
+           "mode": "cross-example batched chains (mcmc_batched), random.Random(123456 + index)"}
+    if rank == 0 and world == 1 and seq_seconds > 0:
+        q0, t0, n = model.query, time.time(), 0
+        for i in mine:
+            run_mhm_attack(model, codes, subs, labels, args, indices=[i], max_iter=100,
+                           prob_threshold=1)
+            n += 1
+            if time.time() - t0 > seq_seconds:
+                break
+        w = time.time() - t0
+        res["sequential"] = {"examples": n, "victim_queries": model.query - q0,
+                             "wall_s": round(w, 2),
+                             "victim_queries_per_s": round((model.query - q0) / w, 2)}
+        res["batched_speedup"] = round(res["victim_queries_per_s"]
+                                       / res["sequential"]["victim_queries_per_s"], 2)
+    return res
+
+
 def subs_leg(dev, seconds, rank, world, precision):
     """Config-3 workload: masked-LM substitute generation (get_substitutes.py) over the Devign
     fixture functions in order (12-layer codebert-shaped MLM, synthetic weights), items pulled
@@ -189,6 +245,10 @@ def main():
     ap.add_argument("--attack-seconds", type=float, default=90.0,
                     help="time budget of the end-to-end GA attack leg over test_subs_0_400 "
                          "(0 disables)")
+    ap.add_argument("--mhm-examples", type=int, default=32,
+                    help="examples of the batched MHM-NS leg (config 5 baseline; 0 disables)")
+    ap.add_argument("--mhm-seq-seconds", type=float, default=15.0,
+                    help="time budget of the sequential MHM-NS comparison run")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -304,6 +364,9 @@ def main():
         res["attack"] = attack_leg(dev, args.attack_seconds, rank, world, args.precision)
     if args.subs_seconds > 0:
         res["substitutes"] = subs_leg(dev, args.subs_seconds, rank, world, args.precision)
+    if args.mhm_examples > 0:
+        res["mhm"] = mhm_leg(dev, args.mhm_examples, args.mhm_seq_seconds, rank, world,
+                             args.precision)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
         res["cpu_baseline"] = cpu_baseline(L, args.cpu_seconds, threads)
