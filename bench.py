@@ -120,12 +120,12 @@ def attack_leg(dev, seconds, rank, world, precision):
             "sharding": "dynamic queue (torch.distributed store counter)"}
 
 
-def mhm_leg(dev, n_examples, seq_seconds, rank, world, precision):
+def mhm_leg(dev, n_examples, seq_examples, rank, world, precision):
     """Config-5 baseline workload: MHM-NS (mhm_attack.py, n_candi 30, max_iter 100, threshold 1)
     over test_subs_0_400 with the CodeBERT Devign victim.  Batched: the first `n_examples` fixture
     examples (strided over ranks) with every chain in flight at once (`mcmc_batched`); sequential:
-    the reference loop (one ≤31-candidate batch per query round) over the same examples in order
-    until `seq_seconds` are spent, for the comparison."""
+    the reference loop (one ≤31-candidate batch per query round) over the first `seq_examples`
+    of them, for the comparison (rank 0, N=1 only)."""
     from apmc_amd.drivers import AttackArgs, load_fixture, run_mhm_attack
     from apmc_amd.model import Model
     from apmc_amd.weights import synthetic_state_dict
@@ -159,18 +159,12 @@ def mhm_leg(dev, n_examples, seq_seconds, rank, world, precision):
            "victim_queries_per_s": round(q / wall, 2),
            "attacked_examples_per_min": round(60 * ex / wall, 3),
            "mode": "cross-example batched chains (mcmc_batched), random.Random(123456 + index)"}
-    if rank == 0 and world == 1 and seq_seconds > 0:
-        q0, t0, n = model.query, time.time(), 0
-        for i in mine:
-            run_mhm_attack(model, codes, subs, labels, args, indices=[i], max_iter=100,
-                           prob_threshold=1)
-            n += 1
-            if time.time() - t0 > seq_seconds:
-                break
-        w = time.time() - t0
-        res["sequential"] = {"examples": n, "victim_queries": model.query - q0,
-                             "wall_s": round(w, 2),
-                             "victim_queries_per_s": round((model.query - q0) / w, 2)}
+    if rank == 0 and world == 1 and seq_examples > 0:
+        seq = run_mhm_attack(model, codes, subs, labels, args, indices=mine[:seq_examples],
+                             max_iter=100, prob_threshold=1, max_inflight=1)
+        res["sequential"] = {"examples": seq["examples"], "victim_queries": seq["queries"],
+                             "wall_s": round(seq["wall_s"], 2),
+                             "victim_queries_per_s": round(seq["queries"] / seq["wall_s"], 2)}
         res["batched_speedup"] = round(res["victim_queries_per_s"]
                                        / res["sequential"]["victim_queries_per_s"], 2)
     return res
@@ -247,8 +241,8 @@ def main():
                          "(0 disables)")
     ap.add_argument("--mhm-examples", type=int, default=32,
                     help="examples of the batched MHM-NS leg (config 5 baseline; 0 disables)")
-    ap.add_argument("--mhm-seq-seconds", type=float, default=15.0,
-                    help="time budget of the sequential MHM-NS comparison run")
+    ap.add_argument("--mhm-seq-examples", type=int, default=4,
+                    help="examples of the sequential MHM-NS comparison run")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -365,7 +359,7 @@ def main():
     if args.subs_seconds > 0:
         res["substitutes"] = subs_leg(dev, args.subs_seconds, rank, world, args.precision)
     if args.mhm_examples > 0:
-        res["mhm"] = mhm_leg(dev, args.mhm_examples, args.mhm_seq_seconds, rank, world,
+        res["mhm"] = mhm_leg(dev, args.mhm_examples, args.mhm_seq_examples, rank, world,
                              args.precision)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)

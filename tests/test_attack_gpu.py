@@ -201,3 +201,32 @@ def test_mhm_matches_text_oracle(victim, kind):
             assert res["prog_length"] == ref["prog_length"]
         seen.append(res["succ"])
     assert any(s is not None for s in seen)
+
+
+def test_mhm_batched_equals_sequential_on_engine(victim):
+    """Cross-example batched MHM-NS (mcmc_batched) on the HIP engine: many
+    chains share each device batch, and every chain still equals `random.seed(s); mcmc(...)` run
+    alone (the engine scores rows batch-invariantly), with the same per-example query counts."""
+    from apmc_amd.attacker import MHM_Attacker
+    from apmc_amd.drivers import AttackArgs, load_fixture
+    from apmc_amd.host import Tokenizer
+
+    codes, subs, labels = load_fixture(FIXTURE, 0, 120)
+    tok = Tokenizer()
+    args = AttackArgs(block_size=BLOCK, eval_batch_size=32)
+    vocab = sorted({w for s in subs[:60] for v in s.values() for w in v})
+    att = MHM_Attacker(args, victim, None, tok, {w: i for i, w in enumerate(vocab)}, vocab)
+    jobs = [(subs[i], codes[i], labels[i], 5000 + i) for i in _pick(codes, subs, 8)]
+    seq = []
+    for sb, code, lab, seed in jobs:
+        random.seed(seed)
+        q0 = victim.query
+        res = att.mcmc(tok, sb, code, lab, _n_candi=30, _max_iter=10)
+        seq.append((res, victim.query - q0))
+    got = att.mcmc_batched(tok, jobs, _n_candi=30, _max_iter=10, max_inflight=8)
+    for j, ((rs, qs), (rb, qb)) in enumerate(zip(seq, got)):
+        assert qs == qb, j
+        assert rs["succ"] == rb["succ"], j
+        if rs["succ"] is not None:
+            assert rs["tokens"] == rb["tokens"], j
+            assert rs["replace_info"] == rb["replace_info"], j
