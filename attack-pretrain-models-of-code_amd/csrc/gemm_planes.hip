@@ -293,7 +293,7 @@ hipError_t pk_launch(const __bf16* A, const __bf16* W, const float* bias, const 
   }
   const int tiles = ((M + PK_BM - 1) / PK_BM) * ((N + BN - 1) / BN);
   const char* gv = std::getenv("AE_PK_GROUP");
-  const int group_m = gv && std::atoi(gv) > 0 ? std::atoi(gv) : 8;
+  const int group_m = gv && std::atoi(gv) > 0 ? std::atoi(gv) : 4;  // 4 > 8 > 16 > 32 by A/B (r1)
   // AE_PK_DIAG (timing experiments only, results WRONG): 1 = no refill DMA after the first two
   // K-tiles, 2 = no post-read barrier, 3 = no barriers at all, 4 = no fragment reads after the
   // first K-tile, 5 = no MFMAs, 6 = epilogue only

@@ -8,7 +8,7 @@ mkdir -p gpurun_out/envab
 P=${P:-f32x3}
 for E in ${ENVS:--}; do
   TAG=${E//[,=]/_}
-  ( [ "$E" != "-" ] && export ${E//,/ }; timeout -k 10 300 python bench.py --steps ${STEPS:-8} --warmup 2 --no-cpu-baseline --attack-seconds 0 --precision $P > gpurun_out/envab/$TAG.log 2>&1 )
+  ( [ "$E" != "-" ] && export ${E//,/ }; timeout -k 10 300 python bench.py --steps ${STEPS:-8} --warmup 2 --no-cpu-baseline --attack-seconds 0 --subs-seconds 0 --mhm-examples 0 --precision $P > gpurun_out/envab/$TAG.log 2>&1 )
   rc=$?; echo "$E rc=$rc $(grep -o '"value": [0-9.]*' gpurun_out/envab/$TAG.log)"; [ $rc -ne 0 ] && tail -5 gpurun_out/envab/$TAG.log && exit $rc
 done
 exit 0
