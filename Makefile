@@ -1,11 +1,14 @@
 # Build of the gfx950 engine (C-ABI shared library) and the CPU oracle pieces.
+# Every .hip is compiled to its own object (in parallel under make -j), then linked.
 HIPCC ?= /opt/rocm/bin/hipcc
 PKG := attack-pretrain-models-of-code_amd
 CSRC := $(PKG)/csrc
+OBJDIR := $(PKG)/build
 LIB := $(PKG)/lib/libalert_engine.so
 SRCS := $(CSRC)/engine.hip $(CSRC)/gemm_f32.hip $(CSRC)/gemm_x3.hip $(CSRC)/gemm_planes.hip $(CSRC)/attention_f32.hip $(CSRC)/attention_x3.hip $(CSRC)/rowops.hip $(CSRC)/splice_topk.hip
+OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS))
 HDRS := $(CSRC)/common.h include/alert_engine.h
-HIPFLAGS := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Iinclude -Wall -Wno-unused-result
+HIPFLAGS := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -Wall -Wno-unused-result
 
 HOSTLIB := $(PKG)/lib/libalert_host.so
 HOSTSRCS := $(CSRC)/host/bpe.cpp $(CSRC)/host/lexer.cpp $(CSRC)/host/mutate.cpp $(CSRC)/host/dfg.cpp $(CSRC)/host/capi.cpp
@@ -19,11 +22,15 @@ $(HOSTLIB): $(HOSTSRCS) $(HOSTHDRS)
 	@mkdir -p $(dir $@)
 	$(CXX) $(HOSTFLAGS) -o $@ $(HOSTSRCS)
 
-$(LIB): $(SRCS) $(HDRS)
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(dir $@)
-	$(HIPCC) $(HIPFLAGS) -o $@ $(SRCS)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB): $(OBJS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $(OBJS)
 
 clean:
-	rm -f $(LIB) $(HOSTLIB)
+	rm -f $(LIB) $(HOSTLIB) $(OBJS)
 
 .PHONY: all clean

@@ -46,35 +46,42 @@ def get_identifiers(code, lang):
 
 
 class _Scorer:
-    """Victim queries for one attacked example: ids built from chromosomes (host) and scored."""
+    """Victim requests for one attacked example: ids built from chromosomes (host + device
+    splice) or from texts."""
 
     def __init__(self, attacker, code, lang="c"):
         self.a = attacker
         self.ex = Example(code, lang)
 
     def population(self, pops, mode):
-        """pops: list of [(tgt, sub), ...] -> (probs, preds) via the device splice path."""
-        m = self.a.model_tgt
-        return m.get_results_population(self.ex, self.a.tokenizer_tgt, pops, mode,
-                                        self.a.args.block_size)
+        """pops: list of [(tgt, sub), ...] -> a request (Payload) of len(pops) queries."""
+        return self.a.model_tgt.prepare_population(self.ex, self.a.tokenizer_tgt, pops, mode,
+                                                   self.a.args.block_size)
 
     def texts(self, texts):
         m = self.a.model_tgt
-        return m.get_results(m.dataset_from_texts(texts, self.a.tokenizer_tgt, self.a.args),
-                             self.a.args.eval_batch_size)
+        return m.prepare(m.dataset_from_texts(texts, self.a.tokenizer_tgt, self.a.args))
 
 
-def get_importance_score(args, example, code, words_list, sub_words, variable_names, tgt_model,
-                         tokenizer, label_list, batch_size=16, max_length=512,
-                         model_type="classification"):
-    """attacker.py:48-83: 1 + #occurrences queries (original + one '<unk>' copy per occurrence)."""
+def answer(model, gen):
+    """Run an attack generator to completion, answering each request with its own
+    get_results-equivalent call (the reference's one-example-at-a-time loop)."""
+    try:
+        req = next(gen)
+        while True:
+            req = gen.send(model.score_prepared([req])[0])
+    except StopIteration as stop:
+        return stop.value
+
+
+def _importance_gen(args, words_list, variable_names, tgt_model, tokenizer):
+    """get_importance_score as a request generator (attacker.py:48-83)."""
     positions = get_identifier_posistions_from_code(words_list, variable_names)
     if len(positions) == 0:
         return None, None, None
     masked_token_list, replace_token_positions = get_masked_code_by_position(words_list, positions)
     texts = [" ".join(tokens) for tokens in [words_list] + masked_token_list]
-    logits, preds = tgt_model.get_results(tgt_model.dataset_from_texts(texts, tokenizer, args),
-                                          args.eval_batch_size)
+    logits, preds = yield tgt_model.prepare(tgt_model.dataset_from_texts(texts, tokenizer, args))
     orig_probs = logits[0]
     orig_label = preds[0]
     orig_prob = max(orig_probs)
@@ -82,11 +89,20 @@ def get_importance_score(args, example, code, words_list, sub_words, variable_na
     return importance_score, replace_token_positions, positions
 
 
+def get_importance_score(args, example, code, words_list, sub_words, variable_names, tgt_model,
+                         tokenizer, label_list, batch_size=16, max_length=512,
+                         model_type="classification"):
+    """attacker.py:48-83: 1 + #occurrences queries (original + one '<unk>' copy per occurrence)."""
+    return answer(tgt_model, _importance_gen(args, words_list, variable_names, tgt_model,
+                                             tokenizer))
+
+
 def compute_fitness(chromesome, codebert_tgt, tokenizer_tgt, orig_prob, orig_label, true_label,
                     code, names_positions_dict, args, scorer=None):
     """attacker.py:25-35: one query for one chromosome."""
     if scorer is not None:
-        new_logits, preds = scorer.population([list(chromesome.items())], MODE_BATCH)
+        new_logits, preds = codebert_tgt.score_prepared(
+            [scorer.population([list(chromesome.items())], MODE_BATCH)])[0]
     else:
         temp_code = map_chromesome(chromesome, code, "c")
         new_feature = convert_code_to_features(temp_code, tokenizer_tgt, true_label, args)
@@ -96,6 +112,14 @@ def compute_fitness(chromesome, codebert_tgt, tokenizer_tgt, orig_prob, orig_lab
 
 
 class Attacker:
+    """greedy_attack / ga_attack with the reference's signatures and 12-tuple results.
+
+    Each attack is written once, as a generator that yields its victim requests (Payloads) and
+    receives (probs, preds) back: greedy_attack / ga_attack answer every request with its own
+    call (the reference loop, Python's global `random`), while drivers.run_gi_attack_batched
+    keeps many examples' generators in flight and answers all their pending requests with ONE
+    device batch (each example on its own `random.Random(seed + index)`)."""
+
     def __init__(self, args, model_tgt, tokenizer_tgt, model_mlm, tokenizer_mlm, use_bpe,
                  threshold_pred_score) -> None:
         self.args = args
@@ -106,11 +130,25 @@ class Attacker:
         self.use_bpe = use_bpe
         self.threshold_pred_score = threshold_pred_score
         self.lang = getattr(args, "lang", "c")
+        # GA mutants per iteration: args.eval_batch_size (CodeBERT Devign, attacker.py:226);
+        # the GraphCodeBERT Devign and CodeBERT clone attackers hard-code 64
+        # (GraphCodeBERT/Defect-detection/code/attacker.py:246)
+        self.ga_batch = None
 
     # ------------------------------------------------------------------------------------------
     def ga_attack(self, example, code, substituions, initial_replace=None):
         """Genetic attack (attacker.py:96-272); returns the reference's 12-tuple."""
-        logits, preds = self.model_tgt.get_results([example], self.args.eval_batch_size)
+        return answer(self.model_tgt, self.ga_gen(example, code, substituions, initial_replace,
+                                                  random))
+
+    def greedy_attack(self, example, code, substituions):
+        """Importance-ordered greedy attack (attacker.py:277-453); returns the 12-tuple."""
+        return answer(self.model_tgt, self.greedy_gen(example, code, substituions))
+
+    # ------------------------------------------------------------------------------------------
+    def ga_gen(self, example, code, substituions, initial_replace=None, rng=random):
+        m = self.model_tgt
+        logits, preds = yield m.prepare([example])
         orig_prob = logits[0]
         orig_label = preds[0]
         current_prob = max(orig_prob)
@@ -152,8 +190,8 @@ class Attacker:
                 substitute_list = list(variable_substitue_dict[tgt_word])
                 if len(substitute_list) == 0:
                     continue
-                logits, preds = scorer.population([[(tgt_word, s)] for s in substitute_list],
-                                                  MODE_SINGLE)
+                logits, preds = yield scorer.population([[(tgt_word, s)] for s in substitute_list],
+                                                        MODE_SINGLE)
                 best = -1
                 for index, temp_prob in enumerate(logits):
                     temp_label = preds[index]
@@ -167,34 +205,35 @@ class Attacker:
             temp_chromesome = copy.deepcopy(base_chromesome)
             temp_chromesome[tgt_word] = initial_candidate
             population.append(temp_chromesome)
-            temp_fitness, temp_label = compute_fitness(temp_chromesome, self.model_tgt,
-                                                       self.tokenizer_tgt, max(orig_prob),
-                                                       orig_label, true_label, code,
-                                                       names_positions_dict, self.args, scorer)
+            # compute_fitness (attacker.py:25-35): one query
+            new_logits, fpreds = yield scorer.population([list(temp_chromesome.items())],
+                                                         MODE_BATCH)
+            temp_fitness, temp_label = max(orig_prob) - new_logits[0][orig_label], fpreds[0]
             fitness_values.append(temp_fitness)
 
         cross_probability = 0.7
         max_iter = max(5 * len(population), 10)
+        batch = self.ga_batch or self.args.eval_batch_size
         for i in range(max_iter):
             _temp_mutants = []
-            for j in range(self.args.eval_batch_size):
-                p = random.random()
-                chromesome_1, index_1, chromesome_2, index_2 = select_parents(population)
+            for j in range(batch):
+                p = rng.random()
+                chromesome_1, index_1, chromesome_2, index_2 = select_parents(population, rng)
                 if p < cross_probability:
                     if chromesome_1 == chromesome_2:
-                        child_1 = mutate(chromesome_1, variable_substitue_dict)
+                        child_1 = mutate(chromesome_1, variable_substitue_dict, rng)
                         continue
-                    child_1, child_2 = crossover(chromesome_1, chromesome_2)
+                    child_1, child_2 = crossover(chromesome_1, chromesome_2, rng=rng)
                     if child_1 == chromesome_1 or child_1 == chromesome_2:
-                        child_1 = mutate(chromesome_1, variable_substitue_dict)
+                        child_1 = mutate(chromesome_1, variable_substitue_dict, rng)
                 else:
-                    child_1 = mutate(chromesome_1, variable_substitue_dict)
+                    child_1 = mutate(chromesome_1, variable_substitue_dict, rng)
                 _temp_mutants.append(child_1)
             if len(_temp_mutants) == 0:
                 continue
             # the dicts are read only now, after every in-place mutate of this iteration
-            mutate_logits, mutate_preds = scorer.population(
-                [list(m.items()) for m in _temp_mutants], MODE_BATCH)
+            mutate_logits, mutate_preds = yield scorer.population(
+                [list(mt.items()) for mt in _temp_mutants], MODE_BATCH)
             mutate_fitness_values = []
             for index, logits in enumerate(mutate_logits):
                 if mutate_preds[index] != orig_label:
@@ -218,9 +257,9 @@ class Attacker:
             variable_names, None, nb_changed_var, nb_changed_pos, None
 
     # ------------------------------------------------------------------------------------------
-    def greedy_attack(self, example, code, substituions):
-        """Importance-ordered greedy attack (attacker.py:277-453); returns the 12-tuple."""
-        logits, preds = self.model_tgt.get_results([example], self.args.eval_batch_size)
+    def greedy_gen(self, example, code, substituions):
+        m = self.model_tgt
+        logits, preds = yield m.prepare([example])
         orig_prob = logits[0]
         orig_label = preds[0]
         current_prob = max(orig_prob)
@@ -241,10 +280,8 @@ class Attacker:
             return code, prog_length, adv_code, true_label, orig_label, temp_label, -3, \
                 variable_names, None, None, None, None
 
-        importance_score, replace_token_positions, names_positions_dict = get_importance_score(
-            self.args, example, processed_code, words, sub_words, variable_names, self.model_tgt,
-            self.tokenizer_tgt, [0, 1], batch_size=self.args.eval_batch_size,
-            max_length=self.args.block_size, model_type="classification")
+        importance_score, replace_token_positions, names_positions_dict = yield from \
+            _importance_gen(self.args, words, variable_names, m, self.tokenizer_tgt)
         if importance_score is None:
             return code, prog_length, adv_code, true_label, orig_label, temp_label, -3, \
                 variable_names, None, None, None, None
@@ -274,8 +311,8 @@ class Attacker:
                 continue
             # get_example(final_code, tgt, sub) per substitute, one batch
             scorer = _Scorer(self, final_code, self.lang)
-            logits, preds = scorer.population([[(tgt_word, s)] for s in substitute_list],
-                                              MODE_SINGLE)
+            logits, preds = yield scorer.population([[(tgt_word, s)] for s in substitute_list],
+                                                    MODE_SINGLE)
             assert len(logits) == len(substitute_list)
             for index, temp_prob in enumerate(logits):
                 temp_label = preds[index]

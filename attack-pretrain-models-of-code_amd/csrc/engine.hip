@@ -25,9 +25,6 @@ hipError_t ae_launch_gemm_f32(const float*, const float*, const float*, const fl
 hipError_t ae_launch_gemm_x3(const float*, const unsigned short*, const unsigned short*,
                              const float*, const float*, float*, int, int, int, int, int, int,
                              int, int, hipStream_t);
-hipError_t ae_launch_gemm_x3g(const float*, const unsigned short*, const unsigned short*,
-                              const float*, const float*, float*, int, int, int, int, int, int,
-                              int, int, hipStream_t);
 hipError_t ae_launch_attention_f32(const float*, float*, const int*, const int*, int, int, int,
                                    const uint32_t*, int, hipStream_t);
 hipError_t ae_launch_attention_x3(const float*, float*, unsigned short*, const int*, const int*,
@@ -36,7 +33,7 @@ hipError_t ae_launch_gemm_packed(const unsigned short*, const unsigned short*, c
                                  const float*, float*, unsigned short*, int, int, int, int, int,
                                  hipStream_t);
 hipError_t ae_launch_compact(const int*, const int*, const int*, int, int, int, int, int*, int*,
-                             int*, hipStream_t);
+                             int*, int*, hipStream_t);
 hipError_t ae_launch_embed_ln(const int*, const int*, const float*, const float*, const float*,
                               const float*, const float*, float, int, int, float*, unsigned short*,
                               int, const uint32_t*, int, const int*, int, hipStream_t);
@@ -45,14 +42,14 @@ hipError_t ae_launch_layernorm(const float*, const float*, const float*, float, 
 hipError_t ae_launch_gather_cls(const float*, const float*, const int*, int, float*, float*,
                                 hipStream_t);
 hipError_t ae_launch_head_out(const float*, const float*, const float*, int, int, int, float*,
-                              hipStream_t);
+                              const int*, hipStream_t);
 hipError_t ae_launch_splice(const int*, const int*, const int*, const int*, int, int, int, int,
                             int, int*, int*, hipStream_t);
 hipError_t ae_launch_topk(const float*, int, int, int, float*, int*, hipStream_t);
 hipError_t ae_launch_cosine_rank(const float*, const float*, int, int, int, float, float*,
                                  hipStream_t);
 hipError_t ae_launch_scatter_rows(const float*, const int*, const int*, int, int, int, int,
-                                  float*, hipStream_t);
+                                  float*, const int*, hipStream_t);
 hipError_t ae_launch_nll_rows(const float*, const int*, int, int, float*, hipStream_t);
 }
 
@@ -106,16 +103,17 @@ struct ae_engine {
   bool planes = false;
   int np = 1;
   int *tok_ids = nullptr, *tok_pos = nullptr, *src_col = nullptr, *cu = nullptr, *one = nullptr;
+  int* err = nullptr;  // device flag: some row's lens disagreed with its ids (compact_kernel)
   float* logits = nullptr;
   size_t cap_logits = 0;
   int* pinned_cu = nullptr;
   size_t cap_pinned = 0;
   hipEvent_t pinned_ready = nullptr;
-  // GEMM variant for the split-bf16 modes: 0 = register-staged (default, faster today), 1 = LDS-DMA ring
-  int gemm_variant = 0;
-  // profiling
+  // profiling: event pairs are created when profiling is switched on (never inside the timed
+  // launches) and recycled by ae_kernel_time
   int prof_kind = -1;
   std::vector<ProfRec> prof;
+  std::vector<ProfRec> prof_pool;
 };
 
 namespace {
@@ -276,9 +274,14 @@ struct Prof {
   ProfRec rec;
   Prof(ae_engine* e_, hipStream_t s, bool enabled, double flop) : e(e_), st(s), on(enabled) {
     if (on) {
+      if (!e->prof_pool.empty()) {
+        rec = e->prof_pool.back();
+        e->prof_pool.pop_back();
+      } else {  // pool exhausted (more launches than ae_set_profiling reserved)
+        (void)hipEventCreate(&rec.a);
+        (void)hipEventCreate(&rec.b);
+      }
       rec.flop = flop;
-      (void)hipEventCreate(&rec.a);
-      (void)hipEventCreate(&rec.b);
       (void)hipEventRecord(rec.a, st);
     }
   }
@@ -297,10 +300,7 @@ int gemm(ae_engine* e, const float* A, const float* W, const unsigned short* Wh,
   Prof p(e, st, prof, 2.0 * M * N * K);
   if (e->cfg.precision != AE_PREC_FP32 && Wh) {
     const int terms = e->cfg.precision == AE_PREC_F32X3 ? 3 : 1;
-    if (e->gemm_variant == 1 && M >= 256 && K % 16 == 0)
-      HIPC(ae_launch_gemm_x3g(A, Wh, Wl, bias, R, C, M, N, K, K, K, N, epi, terms, st));
-    else
-      HIPC(ae_launch_gemm_x3(A, Wh, Wl, bias, R, C, M, N, K, K, K, N, epi, terms, st));
+    HIPC(ae_launch_gemm_x3(A, Wh, Wl, bias, R, C, M, N, K, K, K, N, epi, terms, st));
   } else {
     HIPC(ae_launch_gemm_f32(A, W, bias, R, C, M, N, K, K, K, N, epi, nullptr, st));
   }
@@ -325,9 +325,9 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
                 int keep_all = 0, bool node_avg = false) {
   const int H = e->cfg.hidden, F = e->cfg.ffn, NL = e->cfg.layers, heads = e->cfg.heads;
   const float eps = e->cfg.ln_eps;
+  HIPC(hipMemsetAsync(e->err, 0, sizeof(int), st));
   HIPC(ae_launch_compact(ids, pos, e->cu, n, L, e->cfg.pad_id, keep_all, e->tok_ids, e->tok_pos,
-                         e->src_col,
-                         st));
+                         e->src_col, e->err, st));
   const bool pl = e->planes;
   HIPC(ae_launch_embed_ln(e->tok_ids, e->tok_pos, e->wemb, e->pemb, e->temb, e->eg, e->eb, eps,
                           (int)T, e->cfg.max_pos, e->x, pl ? e->xp : nullptr, e->np,
@@ -428,11 +428,8 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
   ae_engine* e = new ae_engine();
   e->cfg = *cfg;
   e->device = device;
-  if (const char* v = std::getenv("AE_GEMM_VARIANT")) e->gemm_variant = std::atoi(v);
-  // split-precision modes run the full-length GEMMs on bf16 activation planes (gemm_planes.hip);
-  // AE_PLANES=0 keeps the f32-activation kernels (A/B runs)
+  // split-precision modes run the full-length GEMMs on bf16 activation planes (gemm_planes.hip)
   e->planes = cfg->precision != AE_PREC_FP32;
-  if (const char* v = std::getenv("AE_PLANES")) e->planes = e->planes && std::atoi(v) != 0;
   e->np = cfg->precision == AE_PREC_F32X3 ? 2 : 1;
   WeightTable wt;
   for (int i = 0; i < n_weights; ++i) wt.by_name[weights[i].name] = &weights[i];
@@ -544,7 +541,7 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
     UP("lm_head.bias", V, &e->lm_bias);  // decoder weight is tied to word_embeddings
   }
 #undef UP
-  if ((rc = dev_alloc(e, (void**)&e->one, 16))) {
+  if ((rc = dev_alloc(e, (void**)&e->one, 16)) || (rc = dev_alloc(e, (void**)&e->err, 16))) {
     ae_destroy(e);
     return fail(rc, "alloc");
   }
@@ -565,10 +562,11 @@ int ae_destroy(ae_engine* e) {
     if (p) (void)hipFree(p);
   if (e->pinned_cu) (void)hipHostFree(e->pinned_cu);
   if (e->pinned_ready) (void)hipEventDestroy(e->pinned_ready);
-  for (auto& r : e->prof) {
-    (void)hipEventDestroy(r.a);
-    (void)hipEventDestroy(r.b);
-  }
+  for (auto* v : {&e->prof, &e->prof_pool})
+    for (auto& r : *v) {
+      (void)hipEventDestroy(r.a);
+      (void)hipEventDestroy(r.b);
+    }
   delete e;
   return AE_OK;
 }
@@ -616,7 +614,8 @@ static int score_impl(ae_engine* e, const int32_t* ids, const int32_t* lens, con
   const int in_dim = kind == 2 ? 2 * e->cfg.hidden : e->cfg.hidden;
   HIPC(ae_launch_gemm_f32(e->xc, e->hd_w, e->hd_b, nullptr, e->tc, n_out, e->cfg.hidden, in_dim,
                           in_dim, in_dim, e->cfg.hidden, EPI_BIAS_TANH, nullptr, st));
-  HIPC(ae_launch_head_out(e->tc, e->ho_w, e->ho_b, kind, e->cfg.num_labels, n_out, probs_out, st));
+  HIPC(ae_launch_head_out(e->tc, e->ho_w, e->ho_b, kind, e->cfg.num_labels, n_out, probs_out,
+                          e->err, st));
   return AE_OK;
 }
 
@@ -638,7 +637,8 @@ int ae_encode_ex(ae_engine* e, const int32_t* ids, const int32_t* lens, int32_t 
   if ((rc = run_encoder(e, ids, nullptr, nullptr, n, L, T, max_len, false, st,
                         (flags & AE_ENC_ATTEND_PAD) ? 1 : 0)))
     return rc;
-  HIPC(ae_launch_scatter_rows(e->x, e->cu, e->src_col, n, row0, nrows, (int)T, hidden_out, st));
+  HIPC(ae_launch_scatter_rows(e->x, e->cu, e->src_col, n, row0, nrows, (int)T, hidden_out, e->err,
+                              st));
   return AE_OK;
 }
 
@@ -742,6 +742,15 @@ int ae_cosine_rank(const float* ref, const float* cand, int32_t n, int32_t span_
 
 int ae_set_profiling(ae_engine* e, int32_t kind, int32_t enabled) {
   if (!e) return fail(AE_EINVAL, "null engine");
+  if (enabled) {  // reserve the events now, outside whatever region the caller times
+    HIPC(hipSetDevice(e->device));
+    while (e->prof_pool.size() < 1024) {
+      ProfRec r{};
+      HIPC(hipEventCreate(&r.a));
+      HIPC(hipEventCreate(&r.b));
+      e->prof_pool.push_back(r);
+    }
+  }
   e->prof_kind = enabled ? kind : -1;
   return AE_OK;
 }
@@ -758,8 +767,7 @@ int ae_kernel_time(ae_engine* e, double* ms_total, int64_t* launches, double* fl
     ms += t;
     fl += r.flop;
     ++cnt;
-    (void)hipEventDestroy(r.a);
-    (void)hipEventDestroy(r.b);
+    e->prof_pool.push_back(r);
   }
   e->prof.clear();
   *ms_total = ms;

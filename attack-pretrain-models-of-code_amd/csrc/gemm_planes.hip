@@ -28,7 +28,6 @@
 //     bf16 planes (the FFN2 operand)
 #include "common.h"
 
-#include <cstdlib>
 
 // m0 is written only by dma16 below; nothing else in these kernels reads it
 #pragma clang diagnostic ignored "-Winline-asm"
@@ -61,16 +60,24 @@ __device__ __forceinline__ void wait_vm() {
 }
 }  // namespace
 
+// keeps a value live in a diagnostic build whose consumer was cut out (rule 17)
+__device__ __forceinline__ void keep_f32(float x) { asm volatile("" ::"v"(x)); }
+
 // element offset of (row, col) in a packed [rows][NP*ld] matrix, plane p
 __device__ __forceinline__ size_t pk_index(int row, int col, int ld, int np, int p) {
   return (size_t)row * np * ld + (size_t)(col >> 5) * 32 * np + 32 * p + (col & 31);
 }
 
-template <int BN, int NP, int EPI>
+// DIAG (timing experiments only, reachable only through ae_bench_gemm_packed; results WRONG):
+// 1 = no refill DMA after the first two K-tiles, 2 = no post-read barrier, 3 = no barriers at
+// all, 4 = no fragment reads after the first K-tile, 5 = no MFMAs, 6 = epilogue only,
+// 7 = no epilogue stores.  The production instantiations have DIAG = 0.
+template <int BN, int NP, int EPI, int DIAG>
 __global__ __launch_bounds__(512, 1) void gemm_pk_kernel(
     const __bf16* __restrict__ A, const __bf16* __restrict__ W, const float* __restrict__ bias,
     const float* __restrict__ R, float* __restrict__ C, __bf16* __restrict__ Cp, int M, int N,
-    int K, int group_m, int diag) {
+    int K, int group_m) {
+  constexpr int diag = DIAG;
   extern __shared__ __attribute__((aligned(16))) unsigned char pk_smem[];
   constexpr int WM = BN == 256 ? 2 : 4, WN = 8 / WM;
   constexpr int TM = PK_BM / WM / 32, TN = BN / WN / 32;
@@ -154,6 +161,16 @@ __global__ __launch_bounds__(512, 1) void gemm_pk_kernel(
       }
   };
 
+  auto keep_live = [&](const bf16x8 (&fa)[NP][TM], const bf16x8 (&fw)[NP][TN]) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+#pragma unroll
+      for (int a = 0; a < TM; ++a) asm volatile("" ::"v"(fa[p][a]));
+#pragma unroll
+      for (int b = 0; b < TN; ++b) asm volatile("" ::"v"(fw[p][b]));
+    }
+  };
+
   bf16x8 fa[NS][NP][TM], fw[NS][NP][TN];
   if (nk > 0) issue(0);
   if (nk > 1) issue(1);
@@ -186,8 +203,10 @@ __global__ __launch_bounds__(512, 1) void gemm_pk_kernel(
     for (int s = NS0; s < NS; ++s)
       if (diag != 4 || kt == 0) read_step(s);
 #pragma unroll
-    for (int s = 0; s < NS0; ++s)
+    for (int s = 0; s < NS0; ++s) {
       if (diag != 5) mfma_step(fa[s], fw[s]);
+      else keep_live(fa[s], fw[s]);
+    }
     {
       constexpr int RD1 = (NS - NS0) * NP * (TM + TN);
       constexpr int MF0 = NS0 * (NP == 2 ? 3 : 1) * TM * TN;
@@ -209,9 +228,20 @@ __global__ __launch_bounds__(512, 1) void gemm_pk_kernel(
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int s = NS0; s < NS; ++s)
+    for (int s = NS0; s < NS; ++s) {
       if (diag != 5) mfma_step(fa[s], fw[s]);
+      else keep_live(fa[s], fw[s]);
+    }
     __builtin_amdgcn_s_setprio(0);
+  }
+  if constexpr (DIAG == 7) {
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) keep_f32(acc[a][b][r]);
+    return;
   }
 
   // ---- epilogue through LDS: each 32x32 accumulator tile is transposed through a private
@@ -280,51 +310,67 @@ __global__ __launch_bounds__(512, 1) void gemm_pk_kernel(
 }
 
 namespace {
-template <int BN, int NP, int EPI>
+constexpr int PK_GROUP_M = 4;  // grouped tile order: 4 > 8 > 16 > 32 M-tiles by A/B (round 1)
+
+template <int BN, int NP, int EPI, int DIAG>
 hipError_t pk_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R, float* C,
                      __bf16* Cp, int M, int N, int K, hipStream_t st) {
   constexpr int lds = 2 * (PK_BM + BN) * PK_ROWB;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_pk_kernel<BN, NP, EPI>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_pk_kernel<BN, NP, EPI, DIAG>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
   const int tiles = ((M + PK_BM - 1) / PK_BM) * ((N + BN - 1) / BN);
-  const char* gv = std::getenv("AE_PK_GROUP");
-  const int group_m = gv && std::atoi(gv) > 0 ? std::atoi(gv) : 4;  // 4 > 8 > 16 > 32 by A/B (r1)
-  // AE_PK_DIAG (timing experiments only, results WRONG): 1 = no refill DMA after the first two
-  // K-tiles, 2 = no post-read barrier, 3 = no barriers at all, 4 = no fragment reads after the
-  // first K-tile, 5 = no MFMAs, 6 = epilogue only
-  const char* dv = std::getenv("AE_PK_DIAG");
-  const int diag = dv ? std::atoi(dv) : 0;
-  hipLaunchKernelGGL((gemm_pk_kernel<BN, NP, EPI>), dim3(tiles), dim3(512), lds, st, A, W, bias,
-                     R, C, Cp, M, N, K, group_m, diag);
+  hipLaunchKernelGGL((gemm_pk_kernel<BN, NP, EPI, DIAG>), dim3(tiles), dim3(512), lds, st, A, W,
+                     bias, R, C, Cp, M, N, K, PK_GROUP_M);
   return hipGetLastError();
 }
 
-template <int BN, int NP>
+template <int BN, int NP, int DIAG>
 hipError_t pk_epi(int epi, const __bf16* A, const __bf16* W, const float* bias, const float* R,
                   float* C, __bf16* Cp, int M, int N, int K, hipStream_t st) {
+  if constexpr (DIAG != 0) {  // diagnostic builds: split-bf16, bias / GELU epilogues only
+    if (NP != 2 || (epi != PK_EPI_BIAS && epi != PK_EPI_GELU_PACKED)) return hipErrorInvalidValue;
+    if (epi == PK_EPI_BIAS)
+      return pk_launch<BN, 2, PK_EPI_BIAS, DIAG>(A, W, bias, R, C, Cp, M, N, K, st);
+    return pk_launch<BN, 2, PK_EPI_GELU_PACKED, DIAG>(A, W, bias, R, C, Cp, M, N, K, st);
+  }
   switch (epi) {
-    case PK_EPI_BIAS: return pk_launch<BN, NP, PK_EPI_BIAS>(A, W, bias, R, C, Cp, M, N, K, st);
+    case PK_EPI_BIAS: return pk_launch<BN, NP, PK_EPI_BIAS, DIAG>(A, W, bias, R, C, Cp, M, N, K, st);
     case PK_EPI_GELU_PACKED:
-      return pk_launch<BN, NP, PK_EPI_GELU_PACKED>(A, W, bias, R, C, Cp, M, N, K, st);
-    case PK_EPI_RES: return pk_launch<BN, NP, PK_EPI_RES>(A, W, bias, R, C, Cp, M, N, K, st);
-    default: return pk_launch<BN, NP, PK_EPI_TANH>(A, W, bias, R, C, Cp, M, N, K, st);
+      return pk_launch<BN, NP, PK_EPI_GELU_PACKED, DIAG>(A, W, bias, R, C, Cp, M, N, K, st);
+    case PK_EPI_RES: return pk_launch<BN, NP, PK_EPI_RES, DIAG>(A, W, bias, R, C, Cp, M, N, K, st);
+    default: return pk_launch<BN, NP, PK_EPI_TANH, DIAG>(A, W, bias, R, C, Cp, M, N, K, st);
   }
 }
 
 // Tile width per problem: wall time ~ rounds of 256 CUs x per-tile time (256x128 ~0.55 of 256^2)
 int pick_bn(int M, int N) {
-  const char* fv = std::getenv("AE_PL_BN");  // A/B override, read per call (tests flip it)
-  const int force = fv ? std::atoi(fv) : 0;
-  if (force == 128 || force == 256) return force;
   const long tm = (M + PK_BM - 1) / PK_BM;
   const long t256 = tm * ((N + 255) / 256), t128 = tm * ((N + 127) / 128);
   const double c256 = (double)((t256 + 255) / 256), c128 = 0.55 * (double)((t128 + 255) / 256);
   return c128 < c256 ? 128 : 256;
+}
+
+template <int DIAG>
+hipError_t pk_dispatch(const unsigned short* A, const unsigned short* W, const float* bias,
+                       const float* R, float* C, unsigned short* Cp, int M, int N, int K, int epi,
+                       int np, int bn, hipStream_t st) {
+  auto bf = [](const unsigned short* p) { return reinterpret_cast<const __bf16*>(p); };
+  auto bfm = [](unsigned short* p) { return reinterpret_cast<__bf16*>(p); };
+  if (np == 2) {
+    if (bn == 256) return pk_epi<256, 2, DIAG>(epi, bf(A), bf(W), bias, R, C, bfm(Cp), M, N, K, st);
+    return pk_epi<128, 2, DIAG>(epi, bf(A), bf(W), bias, R, C, bfm(Cp), M, N, K, st);
+  }
+  if (bn == 256) return pk_epi<256, 1, DIAG>(epi, bf(A), bf(W), bias, R, C, bfm(Cp), M, N, K, st);
+  return pk_epi<128, 1, DIAG>(epi, bf(A), bf(W), bias, R, C, bfm(Cp), M, N, K, st);
+}
+
+bool pk_shape_ok(int M, int N, int K, int np) {
+  return K % 64 == 0 && N % 32 == 0 && (np == 1 || np == 2) && N > 0 && M >= 0;
 }
 }  // namespace
 
@@ -336,14 +382,29 @@ extern "C" hipError_t ae_launch_gemm_packed(const unsigned short* A, const unsig
                                             unsigned short* Cp, int M, int N, int K, int epi,
                                             int np, hipStream_t st) {
   if (M <= 0) return hipSuccess;
-  if (K % 64 != 0 || N % 32 != 0 || (np != 1 && np != 2) || N <= 0) return hipErrorInvalidValue;
-  auto bf = [](const unsigned short* p) { return reinterpret_cast<const __bf16*>(p); };
-  auto bfm = [](unsigned short* p) { return reinterpret_cast<__bf16*>(p); };
-  const int bn = pick_bn(M, N);
-  if (np == 2) {
-    if (bn == 256) return pk_epi<256, 2>(epi, bf(A), bf(W), bias, R, C, bfm(Cp), M, N, K, st);
-    return pk_epi<128, 2>(epi, bf(A), bf(W), bias, R, C, bfm(Cp), M, N, K, st);
+  if (!pk_shape_ok(M, N, K, np)) return hipErrorInvalidValue;
+  return pk_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, pick_bn(M, N), st);
+}
+
+// Kernel experiments (tools/gemm_bench.py, tests): explicit tile width (0 = the production choice)
+// and a diagnostic variant (0 = the production kernel; see DIAG above — other values give WRONG
+// results and exist only to time parts of the pipeline).  Not part of include/alert_engine.h.
+extern "C" hipError_t ae_bench_gemm_packed(const unsigned short* A, const unsigned short* W,
+                                           const float* bias, const float* R, float* C,
+                                           unsigned short* Cp, int M, int N, int K, int epi,
+                                           int np, int bn, int diag, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  if (!pk_shape_ok(M, N, K, np) || (bn != 0 && bn != 128 && bn != 256)) return hipErrorInvalidValue;
+  if (bn == 0) bn = pick_bn(M, N);
+  switch (diag) {
+    case 0: return pk_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, bn, st);
+    case 1: return pk_dispatch<1>(A, W, bias, R, C, Cp, M, N, K, epi, np, bn, st);
+    case 2: return pk_dispatch<2>(A, W, bias, R, C, Cp, M, N, K, epi, np, bn, st);
+    case 3: return pk_dispatch<3>(A, W, bias, R, C, Cp, M, N, K, epi, np, bn, st);
+    case 4: return pk_dispatch<4>(A, W, bias, R, C, Cp, M, N, K, epi, np, bn, st);
+    case 5: return pk_dispatch<5>(A, W, bias, R, C, Cp, M, N, K, epi, np, bn, st);
+    case 6: return pk_dispatch<6>(A, W, bias, R, C, Cp, M, N, K, epi, np, bn, st);
+    case 7: return pk_dispatch<7>(A, W, bias, R, C, Cp, M, N, K, epi, np, bn, st);
+    default: return hipErrorInvalidValue;
   }
-  if (bn == 256) return pk_epi<256, 1>(epi, bf(A), bf(W), bias, R, C, bfm(Cp), M, N, K, st);
-  return pk_epi<128, 1>(epi, bf(A), bf(W), bias, R, C, bfm(Cp), M, N, K, st);
 }

@@ -41,7 +41,11 @@ void featurize_words(ah::Tokenizer& t, const std::vector<std::string>& words, in
   }
   ids[1 + n] = t.sep_id;
   for (int32_t k = n + 2; k < L; ++k) ids[k] = t.pad_id;
-  *len = n + 2;
+  // ae_score's lens = the non-pad count: a literal "<pad>" in the text tokenises to the pad id,
+  // which the reference masks (attention_mask = ids.ne(1)) and the engine drops
+  int32_t pads = 0;
+  for (int32_t k = 1; k <= n; ++k) pads += ids[k] == t.pad_id;
+  *len = n + 2 - pads;
 }
 
 bool build_mutant(ah_example* e, int32_t mode, int32_t b, int32_t end, const char* const* tgts,
@@ -187,7 +191,7 @@ int32_t ah_example_mutant_words(ah_example* e, ah_tokenizer* t, int32_t mode, in
     if (!build_mutant(e, mode, pair_off[m], pair_off[m + 1], tgts, subs, code))
       return fail("single mode needs 1 pair per mutant");
     const std::vector<std::string> words = ah::py_split(code);
-    int32_t ntok = 0;
+    int32_t ntok = 0, pads = 0;
     for (size_t w = 0; w < words.size(); ++w) {
       const int first = w == 0 ? 1 : 0;
       auto it = e->word_id[first].find(words[w]);
@@ -202,10 +206,11 @@ int32_t ah_example_mutant_words(ah_example* e, ah_tokenizer* t, int32_t mode, in
         id = it->second;
       }
       seq.push_back(id);
-      ntok += e->word_off[id + 1] - e->word_off[id];
+      for (int32_t k = e->word_off[id]; k < e->word_off[id + 1]; ++k, ++ntok)
+        if (ntok < L - 2 && e->word_tok[k] == t->t.pad_id) ++pads;  // literal "<pad>" text
     }
     mut_off[m + 1] = (int32_t)seq.size();
-    lens_out[m] = std::min(ntok, L - 2) + 2;
+    lens_out[m] = std::min(ntok, L - 2) + 2 - pads;  // non-pad count (ae_score's lens)
   }
   if ((int32_t)seq.size() > cap_words) return -(int32_t)seq.size();
   if (mut_words) std::memcpy(mut_words, seq.data(), seq.size() * 4);

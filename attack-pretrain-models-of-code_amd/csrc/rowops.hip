@@ -18,13 +18,18 @@
 // position is `pad`, and only non-pad tokens advance the position counter (HF
 // create_position_ids_from_input_ids).
 // Also records where each compacted token came from (src_col) for ae_encode scatter-back.
+// The segment of row s is exactly cu[s+1]-cu[s] tokens: a row whose non-pad count disagrees with
+// that length (e.g. caller lens that count a literal "<pad>" token of the source text) never writes
+// outside its segment; its unfilled slots get the pad id and `err` is set, which turns every
+// output of the call into NaN (head_out / scatter_rows) instead of a silently wrong score.
 __global__ __launch_bounds__(256) void compact_kernel(const int* __restrict__ ids,
                                                       const int* __restrict__ pos,
                                                       const int* __restrict__ cu, int L, int pad,
                                                       int keep_all,
                                                       int* __restrict__ tok_ids,
                                                       int* __restrict__ tok_pos,
-                                                      int* __restrict__ src_col) {
+                                                      int* __restrict__ src_col,
+                                                      int* __restrict__ err) {
   __shared__ int wave_tot[4], wave_np[4];
   __shared__ int carry, carry_np;
   const int s = blockIdx.x;
@@ -52,7 +57,7 @@ __global__ __launch_bounds__(256) void compact_kernel(const int* __restrict__ id
       off += wave_tot[w];
       off_np += wave_np[w];
     }
-    if (keep) {
+    if (keep && off + before < len) {
       const int j = off + before;
       tok_ids[base + j] = id;
       tok_pos[base + j] = pos ? pos[(size_t)s * L + c] : (nonpad ? pad + 1 + off_np + np_before : pad);
@@ -64,6 +69,14 @@ __global__ __launch_bounds__(256) void compact_kernel(const int* __restrict__ id
       carry_np += wave_np[0] + wave_np[1] + wave_np[2] + wave_np[3];
     }
     __syncthreads();
+  }
+  if (carry != len) {  // lens disagree with the row's ids: fill the rest in-bounds, flag the call
+    for (int j = carry + tid; j < len; j += 256) {
+      tok_ids[base + j] = pad;
+      tok_pos[base + j] = pad;
+      if (src_col) src_col[base + j] = L;  // outside every scatter window
+    }
+    if (tid == 0) atomicOr(err, 1);
   }
 }
 
@@ -231,11 +244,16 @@ __global__ __launch_bounds__(256) void gather_cls_kernel(const float* __restrict
 __global__ __launch_bounds__(256) void head_out_kernel(const float* __restrict__ hid,
                                                        const float* __restrict__ wo,
                                                        const float* __restrict__ bo, int kind,
-                                                       int C, int n_out, float* __restrict__ out) {
+                                                       int C, int n_out, float* __restrict__ out,
+                                                       const int* __restrict__ err) {
   __shared__ float logit[4][128];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + wave;
   if (row >= n_out) return;
+  if (err && *err) {  // compact_kernel found lens that disagree with the ids
+    for (int c = lane; c < (kind == 0 ? 1 : C); c += 64) out[(size_t)row * (kind == 0 ? 1 : C) + c] = NAN;
+    return;
+  }
   const float* h = hid + (size_t)row * AE_HIDDEN;
   float hv[12];
 #pragma unroll
@@ -277,12 +295,14 @@ __global__ __launch_bounds__(256) void scatter_rows_kernel(const float* __restri
                                                            const int* __restrict__ cu,
                                                            const int* __restrict__ src_col, int n,
                                                            int row0, int nrows, int T,
-                                                           float* __restrict__ out) {
+                                                           float* __restrict__ out,
+                                                           const int* __restrict__ err) {
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (t >= T) return;
   const int c = src_col[t] - row0;
   if (c < 0 || c >= nrows) return;
+  const bool bad = err && *err;  // lens disagreed with the ids (compact_kernel): poison the rows
   int lo = 0, hi = n;  // find s with cu[s] <= t < cu[s+1]
   while (hi - lo > 1) {
     const int mid = (lo + hi) >> 1;
@@ -292,8 +312,9 @@ __global__ __launch_bounds__(256) void scatter_rows_kernel(const float* __restri
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const int col = k * 256 + lane * 4;
-    *reinterpret_cast<floatx4*>(out + dst + col) =
-        *reinterpret_cast<const floatx4*>(x + (size_t)t * AE_HIDDEN + col);
+    floatx4 v = *reinterpret_cast<const floatx4*>(x + (size_t)t * AE_HIDDEN + col);
+    if (bad) v = floatx4{NAN, NAN, NAN, NAN};
+    *reinterpret_cast<floatx4*>(out + dst + col) = v;
   }
 }
 
@@ -341,18 +362,19 @@ __global__ __launch_bounds__(256) void nll_rows_kernel(const float* __restrict__
 // ---------------------------------------------------------------------------------------------
 extern "C" {
 hipError_t ae_launch_scatter_rows(const float* x, const int* cu, const int* src_col, int n,
-                                  int row0, int nrows, int T, float* out, hipStream_t st) {
+                                  int row0, int nrows, int T, float* out, const int* err,
+                                  hipStream_t st) {
   if (T <= 0) return hipSuccess;
   hipLaunchKernelGGL(scatter_rows_kernel, dim3((T + 3) / 4), dim3(256), 0, st, x, cu, src_col, n,
-                     row0, nrows, T, out);
+                     row0, nrows, T, out, err);
   return hipGetLastError();
 }
 hipError_t ae_launch_compact(const int* ids, const int* pos, const int* cu, int n, int L, int pad,
-                             int keep_all, int* tok_ids, int* tok_pos, int* src_col,
+                             int keep_all, int* tok_ids, int* tok_pos, int* src_col, int* err,
                              hipStream_t st) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(compact_kernel, dim3(n), dim3(256), 0, st, ids, pos, cu, L, pad, keep_all,
-                     tok_ids, tok_pos, src_col);
+                     tok_ids, tok_pos, src_col, err);
   return hipGetLastError();
 }
 hipError_t ae_launch_nll_rows(const float* logits, const int* target, int T, int V, float* nll,
@@ -385,11 +407,11 @@ hipError_t ae_launch_gather_cls(const float* a, const float* b, const int* cu, i
   return hipGetLastError();
 }
 hipError_t ae_launch_head_out(const float* hid, const float* wo, const float* bo, int kind, int C,
-                              int n_out, float* out, hipStream_t st) {
+                              int n_out, float* out, const int* err, hipStream_t st) {
   if (n_out <= 0) return hipSuccess;
   if (C < 1 || C > 128) return hipErrorInvalidValue;
   hipLaunchKernelGGL(head_out_kernel, dim3((n_out + 3) / 4), dim3(256), 0, st, hid, wo, bo, kind,
-                     C, n_out, out);
+                     C, n_out, out, err);
   return hipGetLastError();
 }
 }

@@ -29,14 +29,15 @@ __global__ __launch_bounds__(256) void splice_kernel(const int* __restrict__ wor
                                                      int* __restrict__ ids_out,
                                                      int* __restrict__ lens_out) {
   __shared__ int wave_tot[4];
-  __shared__ int carry_s;
+  __shared__ int carry_s, pads_s;
   const int m = blockIdx.x;
   const int w0 = mut_off[m], nw = mut_off[m + 1] - w0;
   int* out = ids_out + (size_t)m * L;
   const int cap = L - 2;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) carry_s = 0;
+  if (tid == 0) carry_s = pads_s = 0;
   __syncthreads();
+  int pads = 0;  // pad ids inside the kept tokens (a literal "<pad>" in the source text)
   for (int c0 = 0; c0 < nw; c0 += 256) {
     const int c = c0 + tid;
     int wlen = 0, wstart = 0;
@@ -58,12 +59,18 @@ __global__ __launch_bounds__(256) void splice_kernel(const int* __restrict__ wor
     for (int w = 0; w < wave; ++w) pos += wave_tot[w];
     for (int j = 0; j < wlen; ++j) {
       const int p = pos + j;
-      if (p < cap) out[1 + p] = word_tok[wstart + j];
+      if (p < cap) {
+        const int id = word_tok[wstart + j];
+        out[1 + p] = id;
+        pads += id == pad_id;
+      }
     }
     __syncthreads();
     if (tid == 0) carry_s += wave_tot[0] + wave_tot[1] + wave_tot[2] + wave_tot[3];
     __syncthreads();
   }
+  if (pads) atomicAdd(&pads_s, pads);
+  __syncthreads();
   const int total = carry_s;
   const int ntok = total < cap ? total : cap;
   for (int p = tid; p < L; p += 256) {
@@ -71,7 +78,7 @@ __global__ __launch_bounds__(256) void splice_kernel(const int* __restrict__ wor
     else if (p == ntok + 1) out[p] = sep_id;
     else if (p > ntok + 1) out[p] = pad_id;
   }
-  if (tid == 0) lens_out[m] = ntok + 2;
+  if (tid == 0) lens_out[m] = ntok + 2 - pads_s;  // non-pad count (ae_score's lens)
 }
 
 // --------------------------------------------------------------------------------------------

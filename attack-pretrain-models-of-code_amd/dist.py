@@ -65,14 +65,29 @@ class DynamicQueue:
         return self.order[i] if self.order is not None else i
 
 
+_CALLS = {}
+
+
+def call_key(prefix: str) -> str:
+    """A store key unique to this collective call: every rank makes the same sequence of sharded
+    calls, so a per-prefix call counter gives all ranks the same fresh key (a TCPStore counter
+    lives as long as the process group; reusing one would hand every rank None at once)."""
+    n = _CALLS.get(prefix, 0)
+    _CALLS[prefix] = n + 1
+    return f"{prefix}_{n}"
+
+
 def gather_stats(stats, device=None):
-    """All-gather one float64 vector per rank -> [world, len] numpy array."""
+    """All-gather one float64 vector per rank -> [world, len] numpy array.  With the nccl (RCCL)
+    backend the vector travels from this rank's current GPU."""
     import torch
     import torch.distributed as dist
 
     v = np.asarray(stats, dtype=np.float64)
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return v[None]
+    if device is None and dist.get_backend() == "nccl":
+        device = torch.device("cuda", torch.cuda.current_device())
     t = torch.tensor(v, dtype=torch.float64, device=device)
     out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(out, t)
@@ -92,10 +107,18 @@ def merge_records(records):
 
 
 def run_sharded_gi_attack(model, codes, subs, labels, args, device=None, tok=None):
-    """run_gi_attack over all ranks with a dynamic queue; returns (merged records, totals)."""
+    """run_gi_attack over all ranks with a dynamic queue; returns (merged records, totals).
+    Across ranks the examples are taken in scheduling order, so the per-example RNG
+    (args.rng == "per_example") is required for records identical to a 1-GPU run."""
+    import torch.distributed as dist
+
     from .drivers import run_gi_attack
 
-    q = DynamicQueue(len(codes))
+    world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    if world > 1 and args.rng != "per_example":
+        raise ValueError("run_sharded_gi_attack with world > 1 needs AttackArgs.rng='per_example' "
+                         "(one global random stream would depend on which rank took an example)")
+    q = DynamicQueue(len(codes), key=call_key("apmc_attack_queue"))
     t0 = time.time()
     out = run_gi_attack(model, codes, subs, labels, args, queue=q, tok=tok)
     wall = time.time() - t0
@@ -126,7 +149,7 @@ def run_sharded_substitutes(gen, in_path, out_path, start=0, end=None, device=No
         for i, _ in enumerate(f):
             if i >= start and (end is None or i < end):
                 n_items += 1
-    q = DynamicQueue(n_items, key="apmc_subs_queue", deadline=deadline)
+    q = DynamicQueue(n_items, key=call_key("apmc_subs_queue"), deadline=deadline)
     shard = f"{out_path}.rank{rank}"
     t0 = time.time()
     out = generate_file(gen, in_path, shard, start, end, queue=q)

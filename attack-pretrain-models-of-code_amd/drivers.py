@@ -66,6 +66,102 @@ def attack_one(attacker, tok, code, subs, label, args):
     return res, attack_type
 
 
+def attack_one_gen(attacker, tok, code, subs, label, args, rng):
+    """attack_one as a request generator (gi_attack.py:177-186): greedy, then GA on -1."""
+    example = _example(tok, code, label, args.block_size)
+    res = yield from attacker.greedy_gen(example, code, subs)
+    attack_type = "Greedy"
+    if res[6] == -1 and args.use_ga:
+        res = yield from attacker.ga_gen(example, code, subs, res[11], rng)
+        attack_type = "GA"
+    return res, attack_type
+
+
+def _record(index, res, attack_type, queries, dt_min, recorder):
+    (code, prog_length, adv_code, true_label, orig_label, temp_label, is_success,
+     variable_names, names_to_importance_score, nb_changed_var, nb_changed_pos,
+     replaced_words) = res
+    score_info = ""
+    if names_to_importance_score is not None:
+        for key in names_to_importance_score.keys():
+            score_info += key + ":" + str(names_to_importance_score[key]) + ","
+    replace_info = ""
+    if replaced_words is not None:
+        for key in replaced_words.keys():
+            replace_info += key + ":" + replaced_words[key] + ","
+    if recorder:
+        recorder.write(index, code, prog_length, adv_code, true_label, orig_label, temp_label,
+                       is_success, variable_names, score_info, nb_changed_var, nb_changed_pos,
+                       replace_info, attack_type, queries, dt_min)
+    return dict(index=index, is_success=is_success, attack_type=attack_type, queries=queries,
+                adv_code=adv_code, replace_info=replace_info, nb_changed_var=nb_changed_var,
+                nb_changed_pos=nb_changed_pos, prog_length=prog_length, time_s=dt_min * 60)
+
+
+def _totals(records, wall):
+    correct = sum(r["is_success"] >= -1 for r in records)
+    succ = sum(r["is_success"] == 1 for r in records)
+    return dict(records=records, examples=len(records), total_cnt=correct, success=succ,
+                success_rate=(succ / correct) if correct else 0.0,
+                queries=sum(r["queries"] for r in records), wall_s=wall)
+
+
+def run_gi_attack_batched(model, codes, subs, labels, args: AttackArgs, indices=None, tok=None,
+                          queue=None, log=None, max_inflight=64):
+    """greedy (+GA) over many examples at once: up to `max_inflight`
+    examples' attacks are in flight, and every round answers all their pending victim requests
+    with ONE device batch (Model.score_prepared), so the GPU sees thousands of rows instead of
+    one GA population of <= 64.  Example `index` draws from random.Random(args.seed + index),
+    so each record is exactly the sequential run with rng="per_example" (same outcome, mutants,
+    adversarial code and query count); records come back in example order."""
+    tok = tok or Tokenizer()
+    attacker = Attacker(args, model, tok, None, tok, use_bpe=1, threshold_pred_score=0)
+    attacker.ga_batch = getattr(args, "ga_batch", None)
+    recorder = Recorder(args.csv_store_path) if args.csv_store_path else None
+    order = list(range(len(codes))) if indices is None else list(indices)
+    pos = 0
+
+    def next_index():
+        nonlocal pos
+        if queue is not None:
+            return queue()
+        if pos >= len(order):
+            return None
+        pos += 1
+        return order[pos - 1]
+
+    done, live = {}, []  # live: [index, generator, pending payload, queries, t_start]
+    t0 = time.time()
+    drained = False
+    while True:
+        while not drained and len(live) < max_inflight:
+            index = next_index()
+            if index is None:
+                drained = True
+                break
+            gen = attack_one_gen(attacker, tok, codes[index], subs[index], labels[index], args,
+                                 random.Random(args.seed + index))
+            live.append([index, gen, next(gen), 0, time.time()])
+        if not live:
+            break
+        answers = model.score_prepared([c[2] for c in live])
+        still = []
+        for c, ans in zip(live, answers):
+            c[3] += c[2].n
+            try:
+                c[2] = c[1].send(ans)
+                still.append(c)
+            except StopIteration as stop:
+                res, attack_type = stop.value
+                done[c[0]] = (res, attack_type, c[3], (time.time() - c[4]) / 60)
+                if log:
+                    log(_record(c[0], *done[c[0]], None))
+        live = still
+    # CSV rows in example order, as the reference's loop writes them
+    records = [_record(i, *done[i], recorder) for i in sorted(done)]
+    return _totals(records, time.time() - t0)
+
+
 def run_gi_attack(model, codes, subs, labels, args: AttackArgs, indices=None, tok=None,
                   queue=None, log=None):
     """greedy (+GA) over the given examples; returns per-example records and totals.
@@ -94,36 +190,11 @@ def run_gi_attack(model, codes, subs, labels, args: AttackArgs, indices=None, to
         q0 = model.query
         ts = time.time()
         res, attack_type = attack_one(attacker, tok, codes[index], subs[index], labels[index], args)
-        (code, prog_length, adv_code, true_label, orig_label, temp_label, is_success,
-         variable_names, names_to_importance_score, nb_changed_var, nb_changed_pos,
-         replaced_words) = res
-        dt = (time.time() - ts) / 60
-        score_info = ""
-        if names_to_importance_score is not None:
-            for key in names_to_importance_score.keys():
-                score_info += key + ":" + str(names_to_importance_score[key]) + ","
-        replace_info = ""
-        if replaced_words is not None:
-            for key in replaced_words.keys():
-                replace_info += key + ":" + replaced_words[key] + ","
-        queries = model.query - q0
-        if recorder:
-            recorder.write(index, code, prog_length, adv_code, true_label, orig_label, temp_label,
-                           is_success, variable_names, score_info, nb_changed_var, nb_changed_pos,
-                           replace_info, attack_type, queries, dt)
-        records.append(dict(index=index, is_success=is_success, attack_type=attack_type,
-                            queries=queries, adv_code=adv_code, replace_info=replace_info,
-                            nb_changed_var=nb_changed_var, nb_changed_pos=nb_changed_pos,
-                            prog_length=prog_length, time_s=dt * 60))
+        records.append(_record(index, res, attack_type, model.query - q0, (time.time() - ts) / 60,
+                               recorder))
         if log:
             log(records[-1])
-    total = time.time() - t0
-    done = len(records)
-    correct = sum(r["is_success"] >= -1 for r in records)
-    succ = sum(r["is_success"] == 1 for r in records)
-    return dict(records=records, examples=done, total_cnt=correct, success=succ,
-                success_rate=(succ / correct) if correct else 0.0,
-                queries=sum(r["queries"] for r in records), wall_s=total)
+    return _totals(records, time.time() - t0)
 
 
 def run_mhm_attack(model, codes, subs, labels, args: AttackArgs, indices=None, tok=None,

@@ -19,7 +19,7 @@ from __future__ import annotations
 import numpy as np
 
 from .host import Example
-from .model import Model
+from .model import Model, Payload
 
 DFG_REL = ("comesFrom", "computedFrom")
 
@@ -254,27 +254,41 @@ class GraphModel(Model):
             outs.append(self.engine.score_graph(t(ids), lens, t(pos), t(bits)))
         return torch.cat(outs, 0).cpu().numpy() if len(outs) > 1 else outs[0].cpu().numpy()
 
-    def get_results(self, dataset, batch_size=None, threshold: float = 0.5):
-        """(probs, pred_labels) of GraphCodeBERT/*/code/model.py get_results."""
-        self.query += len(dataset)
-        if len(dataset) == 0:
-            return [], []
+    def prepare(self, dataset) -> Payload:
+        """(probs, pred_labels) request of GraphCodeBERT/*/code/model.py get_results: packed
+        ids / positions / mask bits (rows interleaved code1, code2 for clone pairs)."""
+        n = len(dataset)
+        if n == 0:
+            return Payload(None, None, 0)
         if hasattr(dataset, "packed"):
             ids, pos, bits = dataset.packed()
         else:
             ids, pos, bits = _pack_items(dataset, self.task == "clone")
-        return self._format(self.score_packed(ids, pos, bits), threshold)
+        return Payload(ids, None, n, (pos, bits))
+
+    def prepare_population(self, example, tokenizer, population, mode: int, block_size: int):
+        """A population of chromosomes of one program: mutant texts (host get_example(_batch))
+        -> data-flow features (len(population) queries)."""
+        texts = [example.mutant_text(pairs, mode) for pairs in population]
+        return self.prepare(self.dataset_from_texts(texts, tokenizer, self.args))
+
+    def score_prepared(self, payloads, threshold: float = 0.5):
+        self.query += sum(p.n for p in payloads)
+        live = [p for p in payloads if p.n]
+        if not live:
+            return [([], []) for _ in payloads]
+        ids = np.concatenate([p.ids for p in live])
+        pos = np.concatenate([p.extra[0] for p in live])
+        bits = np.concatenate([p.extra[1] for p in live])
+        logits = self.score_packed(ids, pos, bits)
+        out, off = [], 0
+        for p in payloads:
+            out.append(self._format(logits[off:off + p.n], threshold) if p.n else ([], []))
+            off += p.n
+        return out
 
     def dataset_from_texts(self, texts, tokenizer, args, label=0):
         """Mutant texts -> GraphCodeDataset (the GCB attacker featurises every mutant text with
         convert_code_to_features, GraphCodeBERT/Defect-detection/code/attacker.py:30-63)."""
         return GraphCodeDataset([convert_code_to_features(t, tokenizer, label, args)
                                  for t in texts], args)
-
-    def get_results_population(self, example, tokenizer, population, mode: int, block_size: int,
-                               threshold: float = 0.5):
-        """A population of chromosomes of one program: mutant texts (host get_example(_batch))
-        -> data-flow features -> ae_score_graph.  len(population) queries."""
-        texts = [example.mutant_text(pairs, mode) for pairs in population]
-        return self.get_results(self.dataset_from_texts(texts, tokenizer, self.args), None,
-                                threshold)

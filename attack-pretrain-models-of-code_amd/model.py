@@ -39,6 +39,26 @@ def stack_ids(dataset) -> np.ndarray:
     return np.stack(rows).astype(np.int32, copy=False)
 
 
+class Payload:
+    """A featurised victim request: `ids` (device rows; numpy arrays for graph models), host
+    `lens`, `n` = the queries it is charged (rows / 2 for clone pairs).  `extra` carries the graph
+    inputs (pos, mask bits) of GraphCodeBERT victims."""
+
+    __slots__ = ("ids", "lens", "n", "extra")
+
+    def __init__(self, ids, lens, n, extra=None):
+        self.ids, self.lens, self.n, self.extra = ids, lens, n, extra
+
+
+def _checked(logits: np.ndarray) -> np.ndarray:
+    """The engine turns every output of a call NaN when a row's lens disagreed with its ids
+    (ae_score contract); never let that reach an attack decision."""
+    if not np.isfinite(logits).all():
+        raise RuntimeError("ae_score returned non-finite probabilities: the lens passed for some "
+                           "row disagree with its count of non-pad ids")
+    return logits
+
+
 class Model:
     """Victim model.  `encoder` is an `Engine` (or a state dict, from which one is built)."""
 
@@ -70,35 +90,95 @@ class Model:
     def to(self, *a, **k):
         return self
 
-    def _score_ids(self, ids: np.ndarray, lens: np.ndarray | None = None) -> np.ndarray:
+    # ---- requests -------------------------------------------------------------------------
+    # Every victim query goes through prepare*/score_prepared: a request is featurised into a
+    # `Payload` (device ids + host lens), and score_prepared scores any number of payloads as
+    # ONE device batch and splits the results per payload.  get_results is the one-payload case;
+    # the cross-example attack drivers (drivers.run_gi_attack_batched) hand in the pending
+    # requests of many attacked examples at once.  Rows are scored batch-invariantly, so the
+    # split results equal separate calls bit for bit.
+    def prepare(self, dataset) -> "Payload":
+        """A get_results dataset (CodeDataset / IdsDataset / [example] list) -> Payload."""
         import torch
 
-        pad = self.engine.pad_id
-        if self.task == "clone":
+        n = len(dataset)
+        if hasattr(dataset, "ids") and hasattr(dataset, "lens") and dataset.lens is not None:
+            ids, lens = dataset.ids, np.asarray(dataset.lens, dtype=np.int32)
+        else:
+            ids = stack_ids(dataset) if n else np.zeros((0, self.block_size or 2), np.int32)
+            lens = None
+        if self.task == "clone" and n:
             # model.py:44 input_ids.view(-1, block_size): each row holds code1 | code2
             bs = self.block_size or ids.shape[1] // 2
             ids = ids.reshape(-1, bs)
+            lens = None
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        if lens is None:
+            lens = (ids != self.engine.pad_id).sum(axis=1).astype(np.int32)
+        dev = torch.from_numpy(ids).to(f"cuda:{self.engine.device}")
+        return Payload(dev, lens, n)
+
+    def prepare_population(self, example, tokenizer, population, mode: int, block_size: int):
+        """A population of chromosomes of one program (len(population) queries).
+
+        The host library reduces every mutant to its word-id sequence (the mutant text is built
+        exactly as get_example / get_example_batch would); ae_splice assembles the [n, block]
+        ids on the GPU from the example's word table.  Identical ids to featurising the mutant
+        texts (tests/test_host.py, tests/test_engine_gpu.py)."""
+        import torch
+
+        from .engine import splice
+
+        n = len(population)
+        dev = f"cuda:{self.engine.device}"
+        if n == 0:
+            return Payload(torch.zeros((0, block_size), dtype=torch.int32, device=dev),
+                           np.zeros((0,), np.int32), 0)
+        word_tok, word_off, mut_words, mut_off, lens = example.mutant_words(
+            tokenizer, population, block_size, mode)
+        ids, _ = splice(torch.from_numpy(word_tok).to(dev), torch.from_numpy(word_off).to(dev),
+                        torch.from_numpy(mut_words).to(dev), torch.from_numpy(mut_off).to(dev),
+                        n, block_size, tokenizer.cls_token_id, tokenizer.sep_token_id,
+                        tokenizer.pad_token_id)
+        return Payload(ids, lens, n)
+
+    def score_prepared(self, payloads, threshold: float = 0.5):
+        """Score payloads as one device batch; query += their total queries.  Returns one
+        (probs, pred_labels) per payload, each exactly what get_results gives for it alone."""
+        import torch
+
+        nq = [p.n for p in payloads]
+        self.query += sum(nq)
+        live = [p for p in payloads if p.n]
+        if not live:
+            return [([], []) for _ in payloads]
+        ids = torch.cat([p.ids for p in live], 0) if len(live) > 1 else live[0].ids
+        lens = np.concatenate([p.lens for p in live]) if len(live) > 1 else live[0].lens
+        logits = self._score_dev(ids, lens)
+        out, off = [], 0
+        per_row = 2 if self.task == "clone" else 1
+        for p in payloads:
+            k = p.n
+            out.append(self._format(logits[off:off + k], threshold) if k else ([], []))
+            off += k
+        assert off * per_row == ids.shape[0]
+        return out
+
+    def _score_dev(self, ids, lens: np.ndarray) -> np.ndarray:
+        import torch
+
         n = ids.shape[0]
-        outs = []
         step = self.max_rows_per_launch
-        for s in range(0, n, step):
-            chunk = np.ascontiguousarray(ids[s:s + step], dtype=np.int32)
-            cl = (chunk != pad).sum(axis=1).astype(np.int32) if lens is None or \
-                self.task == "clone" else np.ascontiguousarray(lens[s:s + step], dtype=np.int32)
-            dev = torch.from_numpy(chunk).to(f"cuda:{self.engine.device}", non_blocking=False)
-            outs.append(self.engine.score(dev, cl))
-        return torch.cat(outs, 0).cpu().numpy() if len(outs) > 1 else outs[0].cpu().numpy()
+        outs = [self.engine.score(ids[s:s + step].contiguous(), lens[s:s + step])
+                for s in range(0, n, step)]
+        return _checked(torch.cat(outs, 0).cpu().numpy() if len(outs) > 1 else
+                        outs[0].cpu().numpy())
 
     def get_results(self, dataset, batch_size=None, threshold: float = 0.5):
         """(probs, pred_labels) exactly as the reference's get_results of this task."""
-        self.query += len(dataset)
         if len(dataset) == 0:
             return [], []
-        if hasattr(dataset, "ids") and hasattr(dataset, "lens"):  # utils.IdsDataset fast path
-            logits = self._score_ids(dataset.ids, dataset.lens)
-        else:
-            logits = self._score_ids(stack_ids(dataset))
-        return self._format(logits, threshold)
+        return self.score_prepared([self.prepare(dataset)], threshold)[0]
 
     def dataset_from_texts(self, texts, tokenizer, args, label=0):
         """Mutant texts -> the dataset get_results consumes (convert_code_to_features of every
@@ -110,41 +190,87 @@ class Model:
 
     def get_results_population(self, example, tokenizer, population, mode: int, block_size: int,
                                threshold: float = 0.5):
-        """Score a population of chromosomes of one program (len(population) queries).
-
-        The host library reduces every mutant to its word-id sequence (the mutant text is built
-        exactly as get_example / get_example_batch would); ae_splice assembles the [n, block]
-        ids on the GPU from the example's word table; the engine scores them.  Identical ids to
-        featurising the mutant texts (tests/test_host.py, tests/test_engine_gpu.py)."""
-        import torch
-
-        from .engine import splice
-
-        n = len(population)
-        self.query += n
-        if n == 0:
+        """Score a population of chromosomes of one program (len(population) queries)."""
+        if len(population) == 0:
             return [], []
-        word_tok, word_off, mut_words, mut_off, lens = example.mutant_words(
-            tokenizer, population, block_size, mode)
-        dev = f"cuda:{self.engine.device}"
-        ids, _ = splice(torch.from_numpy(word_tok).to(dev), torch.from_numpy(word_off).to(dev),
-                        torch.from_numpy(mut_words).to(dev), torch.from_numpy(mut_off).to(dev),
-                        n, block_size, tokenizer.cls_token_id, tokenizer.sep_token_id,
-                        tokenizer.pad_token_id)
-        logits = self.engine.score(ids, lens).cpu().numpy()
-        return self._format(logits, threshold)
+        return self.score_prepared([self.prepare_population(example, tokenizer, population, mode,
+                                                            block_size)], threshold)[0]
 
     def _format(self, logits, threshold: float = 0.5):
-        if self.task == "devign":
-            # model.py:56-57
-            probs = [[1 - prob[0], prob[0]] for prob in logits]
-            pred_labels = [1 if label else 0 for label in logits[:, 0] > 0.5]
-        elif self.task == "clone":
-            # Clone-detection-BigCloneBench/code/model.py:81-82
-            probs = logits
-            pred_labels = [0 if first_softmax > threshold else 1 for first_softmax in logits[:, 0]]
+        return format_results(self.task, logits, threshold)
+
+
+def format_results(task, logits, threshold: float = 0.5):
+    """(probs, pred_labels) of one get_results call from the head outputs [n, C]."""
+    if task == "devign":
+        # model.py:56-57
+        probs = [[1 - prob[0], prob[0]] for prob in logits]
+        pred_labels = [1 if label else 0 for label in logits[:, 0] > 0.5]
+    elif task == "clone":
+        # Clone-detection-BigCloneBench/code/model.py:81-82
+        probs = logits
+        pred_labels = [0 if first_softmax > threshold else 1 for first_softmax in logits[:, 0]]
+    else:
+        # Authorship-Attribution/code/model.py:84-89
+        probs = logits
+        pred_labels = [np.argmax(logit) for logit in logits]
+    return probs, pred_labels
+
+
+class HostIdsVictim:
+    """The Model request API (prepare / prepare_population / score_prepared / get_results) over a
+    host scoring function `score_fn(ids int32 [n, L]) -> head outputs [n, C]` — for victims that
+    are not the engine (the CPU baseline of bench.py, multi-process CPU tests).  Mutant ids come
+    from the host featuriser (Example.mutant_ids), the same ids the device splice builds."""
+
+    def __init__(self, score_fn, task: str = "devign", block_size=None, pad_id: int = 1):
+        self.score_fn = score_fn
+        self.task = task
+        self.block_size = block_size
+        self.pad_id = pad_id
+        self.query = 0
+
+    def prepare(self, dataset) -> Payload:
+        n = len(dataset)
+        if hasattr(dataset, "ids"):
+            ids = dataset.ids
         else:
-            # Authorship-Attribution/code/model.py:84-89
-            probs = logits
-            pred_labels = [np.argmax(logit) for logit in logits]
-        return probs, pred_labels
+            ids = stack_ids(dataset)
+        if self.task == "clone" and n:
+            ids = ids.reshape(-1, self.block_size or ids.shape[1] // 2)
+        return Payload(np.ascontiguousarray(ids, dtype=np.int32), None, n)
+
+    def prepare_population(self, example, tokenizer, population, mode: int, block_size: int):
+        ids, lens = example.mutant_ids(tokenizer, population, block_size, mode)
+        return Payload(ids, lens, len(population))
+
+    def score_prepared(self, payloads, threshold: float = 0.5):
+        self.query += sum(p.n for p in payloads)
+        live = [p for p in payloads if p.n]
+        if not live:
+            return [([], []) for _ in payloads]
+        logits = np.asarray(self.score_fn(np.concatenate([p.ids for p in live])))
+        out, off = [], 0
+        for p in payloads:
+            out.append(format_results(self.task, logits[off:off + p.n], threshold)
+                       if p.n else ([], []))
+            off += p.n
+        return out
+
+    def get_results(self, dataset, batch_size=None, threshold: float = 0.5):
+        if len(dataset) == 0:
+            return [], []
+        return self.score_prepared([self.prepare(dataset)], threshold)[0]
+
+    def dataset_from_texts(self, texts, tokenizer, args, label=0):
+        from .utils import IdsDataset
+
+        ids, lens = tokenizer.featurize(list(texts), args.block_size)
+        return IdsDataset(ids, lens)
+
+    def get_results_population(self, example, tokenizer, population, mode: int, block_size: int,
+                               threshold: float = 0.5):
+        if len(population) == 0:
+            return [], []
+        return self.score_prepared([self.prepare_population(example, tokenizer, population, mode,
+                                                            block_size)], threshold)[0]

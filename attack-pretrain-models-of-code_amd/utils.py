@@ -66,27 +66,30 @@ MHM_OPS = frozenset(
 
 
 # --------------------------------------------------------------------------- GA operators
-def select_parents(population):
+# `rng` is the `random` module (the reference's global stream) or a `random.Random(seed)` of one
+# attacked example (cross-example batching runs many examples' streams interleaved); both give the
+# same draws for the same seed.
+def select_parents(population, rng=random):
     """Two independent uniform picks (utils.py:84-90)."""
     idx = range(len(population))
-    i1 = random.choice(idx)
-    i2 = random.choice(idx)
+    i1 = rng.choice(idx)
+    i2 = rng.choice(idx)
     return population[i1], i1, population[i2], i2
 
 
-def mutate(chromesome, variable_substitue_dict):
+def mutate(chromesome, variable_substitue_dict, rng=random):
     """In-place: one random gene gets a random substitute; returns the SAME dict (utils.py:92-97).
     Callers rely on the aliasing (attacker.py:228-238)."""
-    pos = random.choice(range(len(chromesome)))
+    pos = rng.choice(range(len(chromesome)))
     gene = list(chromesome.keys())[pos]
-    chromesome[gene] = random.choice(variable_substitue_dict[gene])
+    chromesome[gene] = rng.choice(variable_substitue_dict[gene])
     return chromesome
 
 
-def crossover(csome_1, csome_2, r=None):
+def crossover(csome_1, csome_2, r=None, rng=random):
     """Single-point crossover at r (utils.py:99-113): child_1 takes csome_2's genes before r."""
     if r is None:
-        r = random.choice(range(len(csome_1)))
+        r = rng.choice(range(len(csome_1)))
     child_1, child_2 = {}, {}
     for pos, name in enumerate(csome_1.keys()):
         first, second = (csome_2, csome_1) if pos < r else (csome_1, csome_2)

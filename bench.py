@@ -8,39 +8,101 @@ Inputs are resident in HBM before the timed region.  Per-GPU work is fixed (weak
 rank scores its own batches; there is no data-path collective.  The only collectives are the
 barrier around the timed region and the MAX-reduction of the elapsed time.
 
+`--gpus N` (N > 1) without torchrun's environment re-launches this script as N ranks through
+`python -m torch.distributed.run` (a child process started before anything touches the GPU);
+under torchrun (WORLD_SIZE set) every rank checks WORLD_SIZE == N and that RCCL sees N ranks.
+
 Prints ONE JSON line (rank 0).  `roofline` is the dominant kernel (the FFN1 GEMM,
-[T,768]x[768,3072] + bias + GELU) timed live with HIP events on the launch stream;
-`cpu_baseline` is oracle/roberta_cpu.py (PyTorch-CPU fp32 eager restatement) on host cores.
+[T,768]x[768,3072] + bias + GELU) timed live with HIP events on the launch stream (events created
+before the timed region); `cpu_baseline` is oracle/roberta_cpu.py (PyTorch-CPU fp32 eager
+restatement of the reference's scoring) on the host cores this job may use.  Sub-objects: the
+exact-fp32 mode of the same step (`fp32_mode`), the end-to-end config-2 GA attack over all of
+test_subs_0_400 (`attack`), config 1 (greedy, 16 functions) on GPU and CPU (`config1`), masked-LM
+substitute generation (`substitutes`) and the MHM-NS baseline (`mhm`).
 """
 import argparse
 import glob
 import json
 import os
 import pathlib
+import random
+import subprocess
 import sys
 import time
 
 ROOT = pathlib.Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
-import numpy as np  # noqa: E402
-import torch  # noqa: E402
-
-import _apmc  # noqa: E402,F401
-
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32-input MFMA dense peak (spec)
 BF16_MFMA_PEAK_TFLOPS = 2516.6  # dense bf16 (spec, no sparsity)
 METRIC = "victim queries/sec + attacked examples/min (node), CodeBERT Devign GA attack"
+FIXTURE = ROOT / "data" / "devign" / "test_subs_0_400.jsonl"
+# attack-sensitive synthetic victim (the attack parity tests' weights): a larger classifier
+# out_proj spreads probabilities so that substitutions can flip predictions
+VICTIM_SEED, VICTIM_OUT_STD = 5, 8.0
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--seq", type=int, default=512)
+    ap.add_argument("--precision", default="f32x3", choices=["fp32", "f32x3", "bf16"])
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="CPU scoring microbenchmark budget (cpu_baseline)")
+    ap.add_argument("--cpu-e2e-seconds", type=float, default=20.0,
+                    help="CPU config-1 greedy attack budget (config1.cpu)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--attack-examples", type=int, default=400,
+                    help="examples of test_subs_0_400 in the config-2 GA attack leg (0 disables)")
+    ap.add_argument("--attack-deadline", type=float, default=420.0,
+                    help="safety cap (s) of the attack leg; hitting it is reported")
+    ap.add_argument("--attack-inflight", type=int, default=64,
+                    help="examples whose attacks share each device batch")
+    ap.add_argument("--subs-seconds", type=float, default=20.0,
+                    help="time budget of the substitute-generation leg (config 3; 0 disables)")
+    ap.add_argument("--mhm-examples", type=int, default=32,
+                    help="examples of the batched MHM-NS leg (config 5 baseline; 0 disables)")
+    ap.add_argument("--mhm-seq-examples", type=int, default=4,
+                    help="examples of the sequential MHM-NS comparison run")
+    ap.add_argument("--no-fp32-mode", action="store_true")
+    return ap.parse_args()
+
+
+def relaunch_as_ranks(args):
+    """--gpus N outside torchrun: run N ranks via torch.distributed.run as a child process
+    (started before this process touches the GPU) and exit with its status."""
+    port = 29000 + (os.getpid() % 2000)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           f"--master-port={port}", str(pathlib.Path(__file__).resolve())] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def executed_flops_per_query(L, C=1):
+    """FLOP the engine executes per query of L tokens: 11 full layers, then the last layer's
+    QKV projection over every row but attention / O-proj / FFN for the CLS row only
+    (engine.hip run_encoder), then the head."""
+    H, F = 768, 3072
+    per_tok = 2 * (4 * H * H + 2 * H * F)
+    full = 11 * (L * per_tok + 4 * L * L * H)
+    last = 2 * L * H * 3 * H + 4 * L * H + 2 * H * H + 4 * H * F
+    return full + last + 2 * H * H + 2 * H * C
 
 
 def flops_per_query(L, C=1):
+    """SURVEY §8(d) algorithmic F(L) (12 full layers)."""
     per_tok = 2 * (4 * 768 * 768 + 2 * 768 * 3072)
     return 12 * (L * per_tok + 4 * L * L * 768) + 2 * 768 * 768 + 2 * 768 * C
 
 
 def pmc_traffic_per_launch(precision):
     """HBM bytes per FFN1 launch of this precision's kernel from the committed rocprofv3 PMC
-    summary (profiles/*pmc_ffn1.json, newest first), or None."""
+    summary (profiles/*pmc*ffn1*.json, newest round first), or None."""
     for f in sorted(glob.glob(str(ROOT / "profiles" / "*pmc*ffn1*.json")), reverse=True):
         try:
             d = json.load(open(f))
@@ -51,14 +113,65 @@ def pmc_traffic_per_launch(precision):
     return None
 
 
+def host_cores():
+    """(threads this job may use, physical cores of the host)."""
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    phys = set()
+    try:
+        cur = {}
+        for line in open("/proc/cpuinfo"):
+            if ":" in line:
+                k, v = [x.strip() for x in line.split(":", 1)]
+                cur[k] = v
+            elif cur:
+                phys.add((cur.get("physical id"), cur.get("core id")))
+                cur = {}
+        if cur:
+            phys.add((cur.get("physical id"), cur.get("core id")))
+    except OSError:
+        pass
+    return threads, (len(phys) or None)
+
+
+# ------------------------------------------------------------------------------------------ legs
+def time_steps(eng, ids_dev, lens, out, steps, warmup, dev, dist, profile):
+    import torch
+
+    stream = torch.cuda.current_stream(dev)
+    for _ in range(warmup):
+        eng.score(ids_dev, lens, out=out, stream=stream)
+    torch.cuda.synchronize(dev)
+    if profile:
+        eng.kernel_time()  # drop anything recorded so far
+        eng.set_profiling("gemm_ffn1", True)  # events are created here, before the timed region
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.score(ids_dev, lens, out=out, stream=stream)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kt = None
+    if profile:
+        eng.set_profiling("gemm_ffn1", False)
+        kt = eng.kernel_time()
+    return elapsed, kt
+
+
 def cpu_baseline(L, seconds, threads):
+    import numpy as np
+    import torch
+
     from apmc_amd.weights import synthetic_state_dict
     from oracle import roberta_cpu as ora
 
     torch.set_num_threads(threads)
     sd = synthetic_state_dict(seed=0, head="sigmoid1")
     rng = np.random.default_rng(0)
-    B = 4
+    B = 8
     ids = rng.integers(4, 50264, size=(B, L)).astype(np.int64)
     ids[:, 0], ids[:, -1] = 0, 2
     ora.score(sd, ids[:1, :64], "sigmoid1")  # warm up allocator / threads
@@ -69,35 +182,121 @@ def cpu_baseline(L, seconds, threads):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return {"value": done / el, "unit": "victim queries/s", "cores": threads, "kind": "port",
-            "sample": f"{done} queries of L={L} (batches of {B}) in {el:.1f} s, "
-                      f"oracle/roberta_cpu.py fp32 eager, torch threads={threads}"}
+    return done / el, f"{done} queries of L={L} (batches of {B}) in {el:.1f} s"
 
 
-def attack_leg(dev, seconds, rank, world, precision):
-    """End-to-end config-2 workload: greedy -> GA attack (gi_attack.py --use_ga) over the
-    test_subs_0_400 fixture, examples pulled in order from a shared queue until the time budget is
-    spent; victim queries/s and attacked examples/min over the whole job."""
-    from apmc_amd.drivers import AttackArgs, load_fixture, run_gi_attack
+def cpu_victim(threads):
+    """The CPU reference path of config 1: oracle/roberta_cpu.py (PyTorch-CPU fp32 eager, the
+    reference's padded [n, 512] batches with the key-padding mask) behind the request API."""
+    import numpy as np
+    import torch
+
+    from apmc_amd.model import HostIdsVictim
+    from apmc_amd.weights import synthetic_state_dict
+    from oracle import roberta_cpu as ora
+
+    torch.set_num_threads(threads)
+    sd = synthetic_state_dict(seed=VICTIM_SEED, head="sigmoid1", out_std=VICTIM_OUT_STD)
+
+    state = {"deadline": None, "scored": 0}
+
+    def score(ids):
+        out = []
+        for s in range(0, ids.shape[0], 64):  # model.py:40 DataLoader batch_size = eval_batch_size
+            if state["deadline"] is not None and time.time() > state["deadline"]:
+                raise TimeoutError  # bounded sample: stop at the next batch past the budget
+            out.append(ora.score(sd, ids[s:s + 64], "sigmoid1"))
+            state["scored"] += out[-1].shape[0]
+        return np.concatenate(out)
+
+    v = HostIdsVictim(score)
+    v.state = state
+    return v
+
+
+def greedy_run(model, codes, subs, labels, indices):
+    """Config 1: gi_attack.py without --use_ga (greedy only), sequential reference loop.  A
+    victim with a `state` dict (the CPU path) may stop the loop at its deadline; queries are then
+    the rows it actually scored."""
+    from apmc_amd.drivers import AttackArgs, run_gi_attack
+
+    args = AttackArgs(block_size=512, eval_batch_size=64, use_ga=False, seed=123456,
+                      rng="per_example")
+    q0 = model.query
+    done = []
+    t0 = time.time()
+    try:
+        run_gi_attack(model, codes, subs, labels, args, indices=indices, log=done.append)
+    except TimeoutError:
+        pass
+    wall = time.time() - t0
+    st = getattr(model, "state", None)
+    return dict(examples=len(done), queries=st["scored"] if st else model.query - q0, wall_s=wall,
+                successes=sum(r["is_success"] == 1 for r in done))
+
+
+def config1_leg(dev, precision, threads, cpu_seconds):
+    """Config 1 (BASELINE configs[0]): greedy attack on the first 16 test_subs_0_400 functions at
+    block 512 — on the GPU engine end to end, and on the CPU reference path (host featurisation +
+    oracle scoring) over a bounded prefix of the same loop."""
+    from apmc_amd.drivers import load_fixture
     from apmc_amd.model import Model
     from apmc_amd.weights import synthetic_state_dict
 
-    codes, subs, labels = load_fixture(ROOT / "data" / "devign" / "test_subs_0_400.jsonl")
-    model = Model(synthetic_state_dict(seed=0, head="sigmoid1"), task="devign",
-                  precision=precision, device=dev.index)
-    args = AttackArgs(block_size=512, eval_batch_size=64, seed=123456, rng="per_example")
-    from apmc_amd.dist import DynamicQueue
+    codes, subs, labels = load_fixture(FIXTURE, 0, 16)
+    model = Model(synthetic_state_dict(seed=VICTIM_SEED, head="sigmoid1", out_std=VICTIM_OUT_STD),
+                  task="devign", precision=precision, device=dev.index)
+    g = greedy_run(model, codes, subs, labels, list(range(16)))
+    model.engine.close()
+    res = {"workload": "CodeBERT Devign greedy attack (gi_attack.py without --use_ga), "
+                       "test_subs_0_400 functions [0, 16), block 512, eval_batch_size 64",
+           "gpu": {"precision": precision, "examples": g["examples"], "queries": g["queries"],
+                   "successes": g["successes"], "wall_s": round(g["wall_s"], 2),
+                   "victim_queries_per_s": round(g["queries"] / g["wall_s"], 1)}}
+    if cpu_seconds > 0:
+        cv = cpu_victim(threads)
+        cv.state["deadline"] = time.time() + cpu_seconds
+        c = greedy_run(cv, codes, subs, labels, list(range(16)))
+        res["cpu"] = {"kind": "port", "cores": threads, "examples_completed": c["examples"],
+                      "queries": c["queries"], "wall_s": round(c["wall_s"], 2),
+                      "victim_queries_per_s": round(c["queries"] / c["wall_s"], 3),
+                      "sample": f"the same greedy loop (host featurisation + oracle/roberta_cpu.py "
+                                f"fp32 eager scoring of padded 512-id rows in batches of 64, "
+                                f"torch threads={threads}) over the first {cpu_seconds:.0f} s "
+                                f"(stopped at the first batch past the budget)"}
+        res["gpu_vs_cpu_queries_per_s"] = round(res["gpu"]["victim_queries_per_s"]
+                                                / max(res["cpu"]["victim_queries_per_s"], 1e-9), 1)
+    return res
 
-    # all ranks pull the next example index from one atomic counter in the torch.distributed
-    # store (no tensor traffic), until the time budget is spent
-    queue = DynamicQueue(len(codes), key="bench_attack_queue",
-                         deadline=time.time() + seconds)
+
+def attack_leg(dev, n_examples, deadline_s, inflight, rank, world, precision):
+    """End-to-end config-2 workload: greedy -> GA attack (gi_attack.py --use_ga) over the first
+    `n_examples` of test_subs_0_400, block 512, eval_batch_size 64, with cross-example batching
+    (drivers.run_gi_attack_batched); ranks pull examples from one shared queue."""
+    import numpy as np
+    import torch
+
+    from apmc_amd.dist import DynamicQueue, call_key
+    from apmc_amd.drivers import AttackArgs, load_fixture, run_gi_attack_batched
+    from apmc_amd.model import Model
+    from apmc_amd.weights import synthetic_state_dict
+
+    codes, subs, labels = load_fixture(FIXTURE, 0, n_examples)
+    model = Model(synthetic_state_dict(seed=VICTIM_SEED, head="sigmoid1", out_std=VICTIM_OUT_STD),
+                  task="devign", precision=precision, device=dev.index)
+    args = AttackArgs(block_size=512, eval_batch_size=64, seed=123456, rng="per_example")
+    queue = DynamicQueue(len(codes), key=call_key("bench_attack_queue"),
+                         deadline=time.time() + deadline_s)
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
-    out = run_gi_attack(model, codes, subs, labels, args, queue=queue)
+    out = run_gi_attack_batched(model, codes, subs, labels, args, queue=queue,
+                                max_inflight=inflight)
+    recs = out["records"]
     stats = np.array([out["examples"], out["total_cnt"], out["success"], out["queries"],
-                      out["wall_s"]], dtype=np.float64)
+                      out["wall_s"], sum(r["attack_type"] == "GA" for r in recs),
+                      sum(r["attack_type"] == "GA" and r["is_success"] == 1 for r in recs)],
+                     dtype=np.float64)
     if world > 1:
         import torch.distributed as dist
         t = torch.tensor(stats, device=dev)
@@ -108,15 +307,21 @@ def attack_leg(dev, seconds, rank, world, precision):
         allst = stats[None]
     ex, cnt, suc, q = allst[:, 0].sum(), allst[:, 1].sum(), allst[:, 2].sum(), allst[:, 3].sum()
     wall = allst[:, 4].max()
-    ga = sum(r["attack_type"] == "GA" for r in out["records"])
+    model.engine.close()
     return {"workload": "CodeBERT Devign greedy->GA attack (gi_attack --use_ga), "
-                        "test_subs_0_400.jsonl in order, block 512, eval_batch_size 64",
+                        f"test_subs_0_400.jsonl examples [0, {n_examples}), block 512, "
+                        "eval_batch_size 64, attack-sensitive synthetic victim "
+                        f"(seed {VICTIM_SEED}, out_proj std {VICTIM_OUT_STD})",
             "precision": precision,
-            "examples": int(ex), "correctly_classified": int(cnt), "successes": int(suc),
-            "success_rate": round(suc / cnt, 4) if cnt else None, "victim_queries": int(q),
-            "wall_s": round(wall, 2), "victim_queries_per_s": round(q / wall, 2),
+            "examples": int(ex), "complete": bool(ex == n_examples),
+            "correctly_classified": int(cnt), "successes": int(suc),
+            "success_rate": round(suc / cnt, 4) if cnt else None,
+            "ga_runs": int(allst[:, 5].sum()), "ga_successes": int(allst[:, 6].sum()),
+            "victim_queries": int(q), "wall_s": round(wall, 2),
+            "victim_queries_per_s": round(q / wall, 2),
             "attacked_examples_per_min": round(60 * ex / wall, 3),
-            "rank0_ga_runs": int(ga), "rng": "random.seed(123456 + index) per example",
+            "rng": "random.Random(123456 + index) per example",
+            "batching": f"cross-example: up to {inflight} examples' requests per device batch",
             "sharding": "dynamic queue (torch.distributed store counter)"}
 
 
@@ -126,13 +331,16 @@ def mhm_leg(dev, n_examples, seq_examples, rank, world, precision):
     examples (strided over ranks) with every chain in flight at once (`mcmc_batched`); sequential:
     the reference loop (one ≤31-candidate batch per query round) over the first `seq_examples`
     of them, for the comparison (rank 0, N=1 only)."""
+    import numpy as np
+    import torch
+
     from apmc_amd.drivers import AttackArgs, load_fixture, run_mhm_attack
     from apmc_amd.model import Model
     from apmc_amd.weights import synthetic_state_dict
 
-    codes, subs, labels = load_fixture(ROOT / "data" / "devign" / "test_subs_0_400.jsonl")
-    model = Model(synthetic_state_dict(seed=0, head="sigmoid1"), task="devign",
-                  precision=precision, device=dev.index)
+    codes, subs, labels = load_fixture(FIXTURE)
+    model = Model(synthetic_state_dict(seed=VICTIM_SEED, head="sigmoid1", out_std=VICTIM_OUT_STD),
+                  task="devign", precision=precision, device=dev.index)
     args = AttackArgs(block_size=512, eval_batch_size=64, seed=123456)
     mine = list(range(rank, n_examples, world))
     if world > 1:
@@ -155,7 +363,8 @@ def mhm_leg(dev, n_examples, seq_examples, rank, world, precision):
     res = {"workload": "MHM-NS (mhm_attack.py: n_candi 30, max_iter 100) CodeBERT Devign victim, "
                        f"test_subs_0_400 examples [0, {n_examples}), block 512",
            "precision": precision, "examples": int(ex), "correctly_classified": int(cnt),
-           "successes": int(suc), "victim_queries": int(q), "wall_s": round(wall, 2),
+           "successes": int(suc), "success_rate": round(suc / cnt, 4) if cnt else None,
+           "victim_queries": int(q), "wall_s": round(wall, 2),
            "victim_queries_per_s": round(q / wall, 2),
            "attacked_examples_per_min": round(60 * ex / wall, 3),
            "mode": "cross-example batched chains (mcmc_batched), random.Random(123456 + index)"}
@@ -167,6 +376,7 @@ def mhm_leg(dev, n_examples, seq_examples, rank, world, precision):
                              "victim_queries_per_s": round(seq["queries"] / seq["wall_s"], 2)}
         res["batched_speedup"] = round(res["victim_queries_per_s"]
                                        / res["sequential"]["victim_queries_per_s"], 2)
+    model.engine.close()
     return res
 
 
@@ -174,7 +384,10 @@ def subs_leg(dev, seconds, rank, world, precision):
     """Config-3 workload: masked-LM substitute generation (get_substitutes.py) over the Devign
     fixture functions in order (12-layer codebert-shaped MLM, synthetic weights), items pulled
     from a shared queue until the time budget is spent."""
-    from apmc_amd.dist import DynamicQueue
+    import numpy as np
+    import torch
+
+    from apmc_amd.dist import DynamicQueue, call_key
     from apmc_amd.engine import Engine
     from apmc_amd.host import Tokenizer
     from apmc_amd.substitutes import SubstituteGenerator
@@ -183,11 +396,11 @@ def subs_leg(dev, seconds, rank, world, precision):
     eng = Engine(synthetic_state_dict(seed=0, head="none", with_mlm=True), head="none",
                  with_mlm=True, precision=precision, device=dev.index)
     gen = SubstituteGenerator(eng, Tokenizer(), block_size=512)
-    codes = [json.loads(line)["func"] for line in
-             open(ROOT / "data" / "devign" / "test_subs_0_400.jsonl")]
+    codes = [json.loads(line)["func"] for line in open(FIXTURE)]
     gen.generate(codes[0])  # warm-up (workspaces, logits buffer)
     gen.stats = {k: 0 for k in gen.stats}
-    queue = DynamicQueue(len(codes), key="bench_subs_queue", deadline=time.time() + seconds)
+    queue = DynamicQueue(len(codes), key=call_key("bench_subs_queue"),
+                         deadline=time.time() + seconds)
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
@@ -224,35 +437,31 @@ def subs_leg(dev, seconds, rank, world, precision):
             "encoder_tflops": round(tot[4] / wall / 1e12, 2)}
 
 
+# ------------------------------------------------------------------------------------------ main
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=64)
-    ap.add_argument("--seq", type=int, default=512)
-    ap.add_argument("--precision", default="f32x3", choices=["fp32", "f32x3", "bf16"])
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--subs-seconds", type=float, default=30.0,
-                    help="time budget of the substitute-generation leg (config 3; 0 disables)")
-    ap.add_argument("--attack-seconds", type=float, default=90.0,
-                    help="time budget of the end-to-end GA attack leg over test_subs_0_400 "
-                         "(0 disables)")
-    ap.add_argument("--mhm-examples", type=int, default=32,
-                    help="examples of the batched MHM-NS leg (config 5 baseline; 0 disables)")
-    ap.add_argument("--mhm-seq-examples", type=int, default=4,
-                    help="examples of the sequential MHM-NS comparison run")
-    args = ap.parse_args()
-
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_as_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+
+    import numpy as np
+    import torch
+
+    import _apmc  # noqa: F401
+
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        seen = torch.ones(1, device=f"cuda:{local}")
+        dist.all_reduce(seen)
+        if int(seen.item()) != args.gpus:
+            raise SystemExit(f"RCCL all-reduce saw {int(seen.item())} ranks, expected {args.gpus}")
     else:
         torch.cuda.set_device(0)
     dev = torch.device(f"cuda:{local if world > 1 else 0}")
@@ -260,8 +469,8 @@ def main():
     from apmc_amd.engine import Engine
     from apmc_amd.weights import synthetic_state_dict
 
-    eng = Engine(synthetic_state_dict(seed=0, head="sigmoid1"), head="sigmoid1", num_labels=1,
-                 precision=args.precision, device=dev.index)
+    sd = synthetic_state_dict(seed=0, head="sigmoid1")
+    eng = Engine(sd, head="sigmoid1", num_labels=1, precision=args.precision, device=dev.index)
     B, L = args.batch, args.seq
     rng = np.random.default_rng(0 + rank)
     ids = rng.integers(4, 50264, size=(B, L)).astype(np.int32)
@@ -269,27 +478,9 @@ def main():
     lens = np.full((B,), L, dtype=np.int32)
     ids_dev = torch.from_numpy(ids).to(dev)
     out = torch.empty((B, 1), dtype=torch.float32, device=dev)
-    stream = torch.cuda.current_stream(dev)
 
-    for _ in range(args.warmup):
-        eng.score(ids_dev, lens, out=out)
-    torch.cuda.synchronize(dev)
-    eng.kernel_time()  # drop anything recorded so far
-    eng.set_profiling("gemm_ffn1", True)
-
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.score(ids_dev, lens, out=out, stream=stream)
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    eng.set_profiling("gemm_ffn1", False)
-    k_ms, k_n, k_flop = eng.kernel_time()
-
+    elapsed, (k_ms, k_n, k_flop) = time_steps(eng, ids_dev, lens, out, args.steps, args.warmup,
+                                               dev, dist, profile=True)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -307,14 +498,24 @@ def main():
     # 3 bf16 MFMAs per product, so its ceiling in algorithmic FLOP/s is the bf16 peak / 3
     peak = {"fp32": FP32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS,
             "f32x3": BF16_MFMA_PEAK_TFLOPS / 3}[args.precision]
-    parity = None
-    if args.precision != "fp32" and rank == 0:
-        # the split / bf16 numbers are only meaningful with their parity on this very batch
-        ref_eng = Engine(synthetic_state_dict(seed=0, head="sigmoid1"), head="sigmoid1",
-                         num_labels=1, precision="fp32", device=dev.index)
-        ref = ref_eng.score(ids_dev, lens).cpu().numpy()[:, 0]
+    fp32_mode = None
+    if args.precision != "fp32" and not args.no_fp32_mode:
+        # the exact-fp32 mode of the same step, and the split / bf16 parity on this very batch
+        ref_eng = Engine(sd, head="sigmoid1", num_labels=1, precision="fp32", device=dev.index)
+        ref_out = torch.empty_like(out)
+        el32, _ = time_steps(ref_eng, ids_dev, lens, ref_out, max(3, args.steps // 2),
+                             args.warmup, dev, dist, profile=False)
+        if dist is not None:
+            t = torch.tensor([el32], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el32 = float(t.item())
+        n32 = max(3, args.steps // 2)
+        fp32_mode = {"value": round(world * n32 * B / el32, 3), "unit": "victim queries/s",
+                     "steps": n32, "ms_per_step": round(1e3 * el32 / n32, 4),
+                     "max_abs_dprob_vs_this_mode": float(np.abs(ref_out.cpu().numpy()[:, 0]
+                                                                - probs).max())}
         ref_eng.close()
-        parity = float(np.abs(out.cpu().numpy()[:, 0] - ref).max())
+    executed = executed_flops_per_query(L) * total_q / elapsed / 1e12
     res = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -330,11 +531,12 @@ def main():
                                            "per product, f32 accumulate; |dp| vs fp32 <= 1e-4)",
                   "bf16": "bf16 (f32 accumulate / residual)"}[args.precision],
         "precision_mode": args.precision,
-        "max_abs_dprob_vs_fp32_mode": parity,
+        "max_abs_dprob_vs_fp32_mode": fp32_mode["max_abs_dprob_vs_this_mode"] if fp32_mode else None,
         "data": "synthetic (seeded RoBERTa-base weights; uniform token ids; no checkpoint offline)",
         "config": {"workload": "CodeBERT Devign victim scoring of one GA mutant population per "
                                "step (config 2 shape: eval_batch_size 64 x block 512)",
-                   "global_batch": B * world, "seq_len": L, "parallelism": f"dp{world} (example shards)"},
+                   "global_batch": B * world, "seq_len": L,
+                   "parallelism": f"dp{world} (example shards)"},
         "roofline": {
             "bound": "mfma",
             "kernel": {"fp32": "gemm_f32_nt_kernel<EPI_BIAS_GELU>",
@@ -350,24 +552,35 @@ def main():
             "avg_launch_us": round(per_launch_s * 1e6, 2),
             "flop_per_launch": (k_flop / k_n) if k_n else None,
         },
-        "whole_step_tflops": round(flops_per_query(L) * total_q / elapsed / 1e12, 3),
-        "whole_step_frac_of_peak": round(flops_per_query(L) * total_q / elapsed / 1e12 / world / peak, 4),
+        "whole_step_executed_tflops": round(executed, 3),
+        "whole_step_frac_of_peak": round(executed / world / peak, 4),
         "probs_checksum": float(np.round(probs.astype(np.float64).sum(), 6)),
     }
-    if args.attack_seconds > 0:
-        res["attack"] = attack_leg(dev, args.attack_seconds, rank, world, args.precision)
+    if fp32_mode:
+        res["fp32_mode"] = fp32_mode
+    eng.close()
+    threads, phys = host_cores()
+    if args.attack_examples > 0:
+        res["attack"] = attack_leg(dev, args.attack_examples, args.attack_deadline,
+                                   args.attack_inflight, rank, world, args.precision)
+    if rank == 0 and world == 1:
+        res["config1"] = config1_leg(dev, args.precision, threads,
+                                     0 if args.no_cpu_baseline else args.cpu_e2e_seconds)
     if args.subs_seconds > 0:
         res["substitutes"] = subs_leg(dev, args.subs_seconds, rank, world, args.precision)
     if args.mhm_examples > 0:
         res["mhm"] = mhm_leg(dev, args.mhm_examples, args.mhm_seq_examples, rank, world,
                              args.precision)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-        res["cpu_baseline"] = cpu_baseline(L, args.cpu_seconds, threads)
-        res["speedup_vs_cpu"] = round(value / res["cpu_baseline"]["value"], 2)
+        v, sample = cpu_baseline(L, args.cpu_seconds, threads)
+        res["cpu_baseline"] = {"value": v, "unit": "victim queries/s", "cores": threads,
+                               "kind": "port",
+                               "sample": sample + f", oracle/roberta_cpu.py fp32 eager, torch "
+                                                  f"threads={threads} (this job's CPU share; "
+                                                  f"host has {phys} physical cores)"}
+        res["speedup_vs_cpu"] = round(value / v, 2)
     if rank == 0:
         print(json.dumps(res), flush=True)
-    eng.close()
     if dist is not None:
         dist.destroy_process_group()
 

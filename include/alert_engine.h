@@ -103,7 +103,9 @@ int ae_destroy(ae_engine *eng);
 /* Score n sequences of row length L.
  *   ids       device int32 [n, L]  token ids, pad = cfg.pad_id anywhere in the row
  *   lens      HOST  int32 [n]      count of non-pad ids of each row (the engine skips
- *                                  pad rows entirely: they never influence the CLS row)
+ *                                  pad rows entirely: they never influence the CLS row).  A row
+ *                                  whose ids disagree with its lens entry makes every output of
+ *                                  the call NaN (the engine never reads or writes out of bounds)
  *   pos       device int32 [n, L] or NULL  explicit position ids (GraphCodeBERT); NULL =
  *                                  RoBERTa rule cumsum(ids!=pad)*(ids!=pad)+pad
  *   mask_bits device uint32 [n, L, ceil(L/32)] or NULL  explicit attention mask (GraphCodeBERT
@@ -160,7 +162,7 @@ int ae_mlm_topk(ae_engine *eng, const int32_t *ids, int32_t L, int32_t k, float 
  *   mut_words  device int32 [sum n_words_m]  word-id sequence of each mutant
  *   mut_off    device int32 [n_mut+1]        offsets into mut_words
  *   ids_out    device int32 [n_mut, L]       [cls] + first L-2 tokens + [sep] + pad
- *   lens_out   device int32 [n_mut]          non-pad length of each row
+ *   lens_out   device int32 [n_mut]          non-pad count of each row (ae_score's lens)
  */
 int ae_splice(const int32_t *word_tok, const int32_t *word_off, const int32_t *mut_words,
               const int32_t *mut_off, int32_t n_mut, int32_t L, int32_t cls_id, int32_t sep_id,

@@ -16,9 +16,11 @@ def pytest_configure(config):
 
 
 @functools.lru_cache(maxsize=None)
-def synthetic_sd(seed: int, head: str, num_labels: int = 1, with_mlm: bool = False):
+def synthetic_sd(seed: int, head: str, num_labels: int = 1, with_mlm: bool = False,
+                 out_std: float = 0.5):
     from apmc_amd.weights import synthetic_state_dict
-    return synthetic_state_dict(seed=seed, head=head, num_labels=num_labels, with_mlm=with_mlm)
+    return synthetic_state_dict(seed=seed, head=head, num_labels=num_labels, with_mlm=with_mlm,
+                                out_std=out_std)
 
 
 @functools.lru_cache(maxsize=None)

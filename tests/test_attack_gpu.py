@@ -33,28 +33,39 @@ def _score_fn(model):
     return score
 
 
-def _pick(codes, subs, n, max_vars=6):
-    idx = [i for i in range(len(codes)) if 1 <= len(subs[i]) <= max_vars and len(codes[i]) < 1500]
+def _pick(codes, subs, n, max_vars=6, max_chars=1500):
+    idx = [i for i in range(len(codes))
+           if 1 <= len(subs[i]) <= max_vars and len(codes[i]) < max_chars]
     return idx[:n]
 
 
-def test_greedy_then_ga_matches_text_oracle(victim):
+# config-2 shape (gi_attack.py --block_size 512 --eval_batch_size 64): 16 fixture examples with
+# up to 8 variables, in 4 chunks so each test stays well inside the per-test time limit
+CONFIG2_BLOCK, CONFIG2_BATCH = 512, 64
+_OUTCOMES = []
+
+
+def _config2_examples(codes, subs):
+    return _pick(codes, subs, 16, max_vars=8, max_chars=4000)
+
+
+@pytest.mark.parametrize("chunk", [0, 1, 2, 3])
+def test_greedy_then_ga_matches_text_oracle(victim, chunk):
     from apmc_amd.drivers import AttackArgs, _example
     from apmc_amd.attacker import Attacker
     from apmc_amd.host import Tokenizer
     from apmc_amd.drivers import load_fixture
 
-    codes, subs, labels = load_fixture(FIXTURE, 0, 120)
+    codes, subs, labels = load_fixture(FIXTURE, 0, 200)
     tok = Tokenizer()
-    args = AttackArgs(block_size=BLOCK, eval_batch_size=16)
+    args = AttackArgs(block_size=CONFIG2_BLOCK, eval_batch_size=CONFIG2_BATCH)
     att = Attacker(args, victim, tok, None, tok, 1, 0)
-    outcomes = []
-    for i in _pick(codes, subs, 8):
+    for i in _config2_examples(codes, subs)[4 * chunk:4 * chunk + 4]:
         code, sb, lab = codes[i], subs[i], labels[i]
         # product
         random.seed(1000 + i)
         q0 = victim.query
-        ex = _example(tok, code, lab, BLOCK)
+        ex = _example(tok, code, lab, CONFIG2_BLOCK)
         res = att.greedy_attack(ex, code, sb)
         kind = "greedy"
         if res[6] == -1:
@@ -63,12 +74,12 @@ def test_greedy_then_ga_matches_text_oracle(victim):
         q_prod = victim.query - q0
         # oracle
         random.seed(1000 + i)
-        v = attack_ref.Victim(_score_fn(victim), BLOCK)
+        v = attack_ref.Victim(_score_fn(victim), CONFIG2_BLOCK)
         ids0 = ex[0].numpy().astype(np.int32)
         ref = attack_ref.greedy(v, ids0, lab, code, sb)
         if ref["is_success"] == -1:
             ref = attack_ref.ga(v, ids0, lab, code, sb, initial_replace=ref["replaced"],
-                                eval_batch_size=16)
+                                eval_batch_size=CONFIG2_BATCH)
         assert res[6] == ref["is_success"], (i, kind)
         assert q_prod == v.query, (i, kind, q_prod, v.query)
         assert res[1] == ref["prog_length"]
@@ -76,9 +87,53 @@ def test_greedy_then_ga_matches_text_oracle(victim):
             assert res[2] == ref["adv_code"], i
             assert res[9] == ref["nb_changed_var"] and res[10] == ref["nb_changed_pos"]
             assert dict(res[11]) == ref["replaced"]
-        outcomes.append((kind, res[6]))
-    # the sample must exercise both attacks
-    assert any(k == "ga" for k, _ in outcomes), outcomes
+        _OUTCOMES.append((kind, res[6]))
+
+
+def test_config2_sample_exercises_both_attacks():
+    """The 16 config-2 examples above include a greedy success and a GA success."""
+    if len(_OUTCOMES) < 16:
+        pytest.skip("needs the four chunks of test_greedy_then_ga_matches_text_oracle")
+    assert ("greedy", 1) in _OUTCOMES and ("ga", 1) in _OUTCOMES, _OUTCOMES
+
+
+def test_batched_gi_equals_sequential(victim):
+    """Cross-example batching on the HIP engine (drivers.run_gi_attack_batched): 16 examples'
+    greedy->GA attacks share every device batch; each record equals the sequential per-example
+    run (random.seed(seed + index)) — outcome, adversarial code, replacements, query count."""
+    from apmc_amd.drivers import AttackArgs, load_fixture, run_gi_attack, run_gi_attack_batched
+
+    codes, subs, labels = load_fixture(FIXTURE, 0, 200)
+    idx = _config2_examples(codes, subs)
+    args = AttackArgs(block_size=CONFIG2_BLOCK, eval_batch_size=CONFIG2_BATCH, rng="per_example")
+    seq = run_gi_attack(victim, codes, subs, labels, args, indices=idx)
+    bat = run_gi_attack_batched(victim, codes, subs, labels, args, indices=idx, max_inflight=16)
+    keys = ["index", "is_success", "attack_type", "queries", "adv_code", "replace_info",
+            "nb_changed_var", "nb_changed_pos"]
+    assert [{k: r[k] for k in keys} for r in seq["records"]] == \
+        [{k: r[k] for k in keys} for r in bat["records"]]
+    assert seq["queries"] == bat["queries"]
+
+
+def test_literal_pad_in_source(victim):
+    """A literal "<pad>" in the source tokenises to the pad id (the reference masks it with
+    attention_mask = ids.ne(1)); the featuriser's lens exclude it, the engine drops it, and the
+    score equals the oracle's on the same ids.  Lens that disagree with the ids give an error,
+    never a silently wrong score."""
+    from apmc_amd.host import Tokenizer
+    from apmc_amd.utils import IdsDataset
+    from conftest import synthetic_sd
+    from oracle import roberta_cpu as ora
+
+    tok = Tokenizer()
+    code = "int f(int a) { int <pad> = a; return a <pad> + 1; }"
+    ids, lens = tok.featurize([code, "int g(void) { return 0; }"], 64)
+    assert (ids[0, 1:lens[0]] == 1).any() and lens[0] == (ids[0] != 1).sum()
+    probs, _ = victim.get_results(IdsDataset(ids, lens))
+    ref = ora.score(synthetic_sd(seed=5, head="sigmoid1", out_std=8.0), ids, "sigmoid1")
+    assert abs(probs[0][1] - ref[0, 0]) < 1e-4 and abs(probs[1][1] - ref[1, 0]) < 1e-4
+    with pytest.raises(RuntimeError, match="non-finite"):
+        victim.get_results(IdsDataset(ids, lens + 1))
 
 
 def test_driver_runs_and_counts(victim):

@@ -16,40 +16,21 @@ FIXTURE = ROOT / "data" / "devign" / "test_subs_0_400.jsonl"
 N_EX = 10
 
 
-class FakeVictim:
-    """Devign-format victim over ids: p = sigmoid(<ids, w> / scale) (deterministic)."""
+def FakeVictim():
+    """Devign-format victim over ids: p = sigmoid(<ids, w> / scale) (deterministic numpy
+    stand-in for the engine behind the product's request API, apmc_amd.model.HostIdsVictim)."""
+    sys.path.insert(0, str(ROOT))
+    import _apmc  # noqa: F401
+    from apmc_amd.model import HostIdsVictim
 
-    def __init__(self):
-        rng = np.random.default_rng(0)
-        self.w = rng.standard_normal(50265).astype(np.float64)
-        self.query = 0
+    w = np.random.default_rng(0).standard_normal(50265).astype(np.float64)
 
-    def _p(self, ids):
+    def score(ids):
         ids = np.asarray(ids)
-        z = np.where(ids != 1, self.w[ids], 0.0).sum(1) / 8.0
-        return (1.0 / (1.0 + np.exp(-z))).astype(np.float32)
+        z = np.where(ids != 1, w[ids], 0.0).sum(1) / 8.0
+        return (1.0 / (1.0 + np.exp(-z))).astype(np.float32)[:, None]
 
-    def _fmt(self, p):
-        return [[1 - x, x] for x in p], [1 if x > 0.5 else 0 for x in p]
-
-    def get_results(self, dataset, batch_size=None):
-        self.query += len(dataset)
-        if hasattr(dataset, "ids"):
-            ids = dataset.ids
-        else:
-            ids = np.stack([np.asarray(d[0]) for d in dataset])
-        return self._fmt(self._p(ids))
-
-    def dataset_from_texts(self, texts, tokenizer, args, label=0):
-        from apmc_amd.utils import IdsDataset
-
-        ids, lens = tokenizer.featurize(list(texts), args.block_size)
-        return IdsDataset(ids, lens)
-
-    def get_results_population(self, example, tokenizer, population, mode, block_size):
-        self.query += len(population)
-        ids, _ = example.mutant_ids(tokenizer, population, block_size, mode)
-        return self._fmt(self._p(ids))
+    return HostIdsVictim(score)
 
 
 def _worker(rank, world, port, outdir):
@@ -65,9 +46,19 @@ def _worker(rank, world, port, outdir):
     codes, subs, labels = load_fixture(FIXTURE, 0, N_EX)
     args = AttackArgs(block_size=128, eval_batch_size=8, rng="per_example")
     recs, tot = run_sharded_gi_attack(FakeVictim(), codes, subs, labels, args)
+    # a second sharded call in the same process group (run.sh runs several chunks) must get a
+    # fresh queue, not the drained counter of the first call
+    recs2, tot2 = run_sharded_gi_attack(FakeVictim(), codes, subs, labels, args)
+    try:  # the global RNG stream would depend on which rank took an example: refused
+        run_sharded_gi_attack(FakeVictim(), codes, subs, labels,
+                              AttackArgs(block_size=128, eval_batch_size=8, rng="global"))
+        refused = False
+    except ValueError:
+        refused = True
     if rank == 0:
         import json
-        (pathlib.Path(outdir) / "dist.json").write_text(json.dumps({"recs": recs, "tot": tot}))
+        (pathlib.Path(outdir) / "dist.json").write_text(json.dumps(
+            {"recs": recs, "tot": tot, "recs2": recs2, "tot2": tot2, "refused": refused}))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -90,6 +81,8 @@ def test_two_ranks_match_single_process(tmp_path):
     a = [{k: r[k] for k in keys} for r in got["recs"]]
     b = [{k: r[k] for k in keys} for r in single["records"]]
     assert a == b
+    assert [{k: r[k] for k in keys} for r in got["recs2"]] == b
+    assert got["tot2"]["examples"] == N_EX and got["refused"]
     assert got["tot"]["examples"] == N_EX
     assert got["tot"]["queries"] == single["queries"]
     # both ranks pulled work from the shared queue

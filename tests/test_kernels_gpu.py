@@ -19,6 +19,8 @@ def _lib():
     vp, i32 = ctypes.c_void_p, ctypes.c_int32
     lib.ae_launch_gemm_packed.argtypes = [vp] * 6 + [i32] * 5 + [vp]
     lib.ae_launch_gemm_packed.restype = ctypes.c_int
+    lib.ae_bench_gemm_packed.argtypes = [vp] * 6 + [i32] * 7 + [vp]
+    lib.ae_bench_gemm_packed.restype = ctypes.c_int
     return lib
 
 
@@ -57,9 +59,7 @@ def _p(t):
     (700, 256, 256, 1, 1, "256"),
     (64, 2304, 768, 2, 0, ""),
 ])
-def test_gemm_packed_matches_split_products(gpu, monkeypatch, M, N, K, np_, epi, bn):
-    if bn:
-        monkeypatch.setenv("AE_PL_BN", bn)
+def test_gemm_packed_matches_split_products(gpu, M, N, K, np_, epi, bn):
     lib = _lib()
     g = torch.Generator().manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g) * 0.7
@@ -85,8 +85,12 @@ def test_gemm_packed_matches_split_products(gpu, monkeypatch, M, N, K, np_, epi,
     C = torch.full((M, N), float("nan"), device="cuda")
     Cp = torch.zeros((M, np_ * N), dtype=torch.bfloat16, device="cuda")
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    rc = lib.ae_launch_gemm_packed(_p(dA), _p(dW), _p(db), _p(dR), _p(C), _p(Cp), M, N, K, epi,
-                                   np_, st)
+    if bn:  # explicit tile width through the experiment entry point (production kernel, diag 0)
+        rc = lib.ae_bench_gemm_packed(_p(dA), _p(dW), _p(db), _p(dR), _p(C), _p(Cp), M, N, K, epi,
+                                      np_, int(bn), 0, st)
+    else:
+        rc = lib.ae_launch_gemm_packed(_p(dA), _p(dW), _p(db), _p(dR), _p(C), _p(Cp), M, N, K,
+                                       epi, np_, st)
     assert rc == 0
     torch.cuda.synchronize()
     if epi == 1:
