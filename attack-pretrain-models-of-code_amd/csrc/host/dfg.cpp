@@ -447,9 +447,18 @@ class CTree {
       } else {
         attach(decl, d);
       }
-      if (at(",")) add_leaf(decl, p_++);
-      else if (p_ == before) add_leaf(decl, p_++);
-      else if (!at(";")) break;
+      if (at(",")) {
+        add_leaf(decl, p_++);
+      } else if (p_ == before) {
+        // not a declarator (e.g. `volatile ("\t":::"memory")` once a raw newline broke the
+        // asm string): tree-sitter wraps the rest of the statement in an ERROR node, so no
+        // identifier in it sits directly under the declaration
+        const int err = make(N_GENERIC);
+        attach(decl, err);
+        while (p_ < limit && !at(";")) add_leaf(err, p_++);
+      } else if (!at(";")) {
+        break;
+      }
     }
   }
 

@@ -13,8 +13,10 @@
 //   * identifiers [A-Za-z_][A-Za-z0-9_]*; numbers (optional sign when an operand is expected,
 //     0x/0b, digits, '.', exponent sign after e/E/p/P, suffix letters);
 //   * string literal: opening quote (with L/u/U/u8 prefix) and closing quote are leaves, escape
-//     sequences are leaves, plain content is a hidden token (no leaf); an unescaped newline ends
-//     an unterminated literal;  char literal likewise;
+//     sequences are leaves, plain content is a hidden token (no leaf); at an unescaped newline a
+//     string literal closes if the next non-blank character is its quote (the closing quote may
+//     follow whitespace), else it ends unterminated at the line break;  char literal: ends at
+//     the line break;
 //   * operators: longest match over the C punctuators;
 //   * preprocessor line (# first on its line): directive leaf "#<ws>name"; #include <..> is one
 //     leaf; #define NAME [ (params) ] then the rest of the line (with \-continuations, up to a
@@ -248,7 +250,19 @@ class Lexer {
     }
     while (!c_.eof()) {
       const unsigned char d = c_.at();
-      if (d == '\n') return;  // unterminated: the literal ends at the line break
+      if (d == '\n') {
+        // a raw newline inside the literal: tree-sitter-c's content token is immediate and
+        // excludes '\n', but the closing quote is not immediate, so whitespace (the newline and
+        // the next line's indentation) may precede it — if the next non-blank character is the
+        // closing quote the literal closes there; otherwise it is unterminated and ends here
+        size_t k = c_.i;
+        while (k < c_.s.size() && (c_.s[k] == '\n' || c_.s[k] == ' ' || c_.s[k] == '\t' ||
+                                   c_.s[k] == '\r'))
+          ++k;
+        if (q != '"' || k >= c_.s.size() || (unsigned char)c_.s[k] != q) return;
+        while (c_.i < k) c_.adv();
+        continue;
+      }
       if (d == q) {
         const size_t b = c_.i;
         const int sl = c_.line, sc = c_.col();

@@ -236,7 +236,15 @@ class _Lex:
         while not self.eof():
             d = self.at()
             if d == "\n":
-                return
+                # the closing quote (not an immediate token) may follow blanks and newlines
+                k = self.i
+                while k < len(self.s) and self.s[k] in "\n \t\r":
+                    k += 1
+                if q != '"' or k >= len(self.s) or self.s[k] != q:
+                    return
+                while self.i < k:
+                    self.adv()
+                continue
             if d == q:
                 b, sl, sc = self.i, self.line, self.col()
                 self.adv()
@@ -478,12 +486,19 @@ def tokenizer():
     """transformers RobertaTokenizer (tokenizers-backed) on data/tokenizer — the oracle tokenizer."""
     global _TOK
     if _TOK is None:
+        import random
+
+        # importing / constructing the transformers tokenizer draws from Python's global random
+        # stream; the attack oracles share that stream with the product under one seed, so the
+        # first load must leave it untouched
+        state = random.getstate()
         from transformers import RobertaTokenizer
         v = json.load(open(ROOT / "data" / "tokenizer" / "vocab.json", encoding="utf-8"))
         merges = [tuple(l.rstrip("\n").split(" ")) for l in
                   open(ROOT / "data" / "tokenizer" / "merges.txt", encoding="utf-8")
                   if not l.startswith("#version")]
         _TOK = RobertaTokenizer(vocab=v, merges=merges)
+        random.setstate(state)
     return _TOK
 
 

@@ -221,22 +221,49 @@ def test_dfg_identifiers_known_answers():
     assert _idents(code) == ["u", "a", "b"]
 
 
-def test_dfg_identifiers_vs_reference_fixture_keys():
+def dfg_key_parity():
     """Known answer from the reference's own output: the substitute keys of every Devign fixture
-    function are get_identifiers(remove_comments(func)) (get_substitutes.py:56-83) minus names
-    without a surviving substitute, in the same order.  tree-sitter's error recovery on
-    macro-heavy code is not reproducible without the grammar, so the bar is a measured rate:
-    exact list match on >= 88% of the 2732 functions, keys a subsequence on >= 97%."""
-    from apmc_amd.host import remove_comments
-    tot = exact = subseq = 0
+    function are get_substitutes.py:47-137 applied to get_identifiers(remove_comments(func)): the
+    DFG names (run_parser.py:272-281) that occur as words (utils.get_identifier_posistions_from_code),
+    are valid C names, have an occurrence inside the MLM's 510 sub-words, and keep >= 1 substitute.
+    Returns (exact, consistent, total, residue): exact = our list after the same filters equals the
+    keys; consistent = exact, or (function longer than 380 of our sub-words) equal once cut at the
+    last key's first occurrence — the reference tokenizer's 510-sub-word boundary is unknowable
+    offline (codebert vocab absent), so for long functions only a prefix is pinned."""
+    from apmc_amd.host import Tokenizer, remove_comments
+    from apmc_amd.utils import _tokenize, get_identifier_posistions_from_code, is_valid_variable_name
+    tok = Tokenizer()
+    exact = consistent = tot = 0
+    residue = []
     for path in DEVIGN:
-        for js in load(path):
-            keys = list(js["substitutes"].keys())
-            ids = _idents(remove_comments(js["func"]))
-            it = iter(ids)
-            subseq += all(k in it for k in keys)
-            exact += ids == keys
+        for line, js in enumerate(load(path)):
             tot += 1
+            keys = list(js["substitutes"].keys())
+            from apmc_amd.attacker import get_identifiers
+            idents, code_tokens = get_identifiers(remove_comments(js["func"]), "c")
+            words, sub_words, kk = _tokenize(" ".join(code_tokens), tok)
+            names = [i[0] for i in idents if " " not in i[0].strip()]
+            pos = get_identifier_posistions_from_code(words, names)
+            ours = [n for n in pos if is_valid_variable_name(n, "c")]
+            if ours == keys:
+                exact += 1
+                consistent += 1
+                continue
+            if keys and len(sub_words) > 380 and all(k in pos for k in keys):
+                last = max(kk[pos[k][0]][0] for k in keys)
+                if [n for n in ours if kk[pos[n][0]][0] <= last] == keys:
+                    consistent += 1
+                    continue
+            residue.append((path.name, line, [n for n in ours if n not in keys],
+                            [k for k in keys if k not in ours]))
+    return exact, consistent, tot, residue
+
+
+def test_dfg_identifiers_vs_reference_fixture_keys():
+    """tree-sitter's error recovery on macro-heavy code is not reproducible without the grammar,
+    so the bar is a measured rate (DESIGN.md §5 lists the residue by cause): exact on >= 89% of the
+    2732 functions, truncation-consistent on >= 98%."""
+    exact, consistent, tot, residue = dfg_key_parity()
     assert tot == 2732
-    assert exact / tot >= 0.88, (exact, tot)
-    assert subseq / tot >= 0.97, (subseq, tot)
+    assert exact / tot >= 0.89, (exact, tot)
+    assert consistent / tot >= 0.98, (consistent, tot, residue[:5])
