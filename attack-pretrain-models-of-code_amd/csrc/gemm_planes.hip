@@ -12,14 +12,16 @@
 //
 // gfx950 mapping:
 //   * tile 256 x BN (BN = 256: 8 waves as 2 x 4, wave tile 128 x 64; BN = 128: 4 x 2, 64 x 64),
-//     one 512-thread workgroup per CU, LDS 2 x (256 + BN) x 128 B
+//     one 512-thread workgroup per CU, LDS NST x (256 + BN) x 128 B (NST = 3 stages for BN = 128,
+//     2 for BN = 256)
 //   * operands reach LDS by LDS-DMA (global_load_lds_dwordx4, one wave instruction = 8 rows x
 //     128 B, lane-linear image); the 16-B chunk of row r is XOR-swizzled by (r >> 1) & 7 on the
 //     SOURCE address, so fragment ds_read_b128s of 16 rows hit 16 different bank slots
 //   * a K-tile's fragments are pulled from LDS into registers as soon as the tile has landed;
-//     once every wave holds them (barrier) the stage is refilled with tile k+2, so TWO K-tiles of
-//     DMA (128 KiB per CU) are in flight behind the MFMAs instead of one — the kernel is bound by
-//     how many bytes a CU keeps in flight, not by LDS size
+//     2 stages (BN = 256): once every wave holds them (a second barrier) the stage is refilled
+//     with tile k+2; 3 stages (BN = 128): tile k+2 goes into tile k-1's stage right after the
+//     K-tile's one barrier, so two K-tiles of DMA are in flight behind the MFMAs — the kernel is
+//     bound by how many bytes a CU keeps in flight (tools/gemm_bench.py diag runs)
 //   * the MFMAs of the first half of the tile run between the fragment reads and that barrier,
 //     overlapping the LDS reads of the other waves
 //   * DMA issued from inline asm with hand-counted vmcnt (the compiler's wait-count pass would
@@ -56,8 +58,14 @@ __device__ __forceinline__ void wait_vm() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   else static_assert(N == 0, "unsupported vmcnt");
 }
+
+// LDS stages of the DMA ring: 3 when they fit in 160 KiB (256 x 128 tiles: 3 x 48 KiB), else 2
+template <int BN>
+constexpr int pk_stages() { return 3 * (256 + BN) * 128 <= 160 * 1024 ? 3 : 2; }
 }  // namespace
 
 // keeps a value live in a diagnostic build whose consumer was cut out (rule 17)
@@ -83,6 +91,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pk_kernel(
   constexpr int TM = PK_BM / WM / 32, TN = BN / WN / 32;
   constexpr int A_BYTES = PK_BM * PK_ROWB, W_BYTES = BN * PK_ROWB;
   constexpr int STAGE = A_BYTES + W_BYTES;
+  constexpr int NST = pk_stages<BN>();                 // ring depth: NST-1 K-tiles in flight
   constexpr int A_DMA = PK_BM / 64, W_DMA = BN / 64;  // DMA instructions per wave per K-tile
   constexpr int DMA = A_DMA + W_DMA;
   constexpr int KB = 64 / NP;                          // k per K-tile
@@ -128,7 +137,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pk_kernel(
 
   auto issue = [&](int kt) {
     const int kb = kt * PK_ROWB;  // byte offset of K-tile kt in a packed row
-    const uint32_t st = lds0 + (kt & 1) * STAGE;
+    const uint32_t st = lds0 + (kt % NST) * STAGE;
 #pragma unroll
     for (int u = 0; u < A_DMA; ++u) dma16(a_src[u] + kb, st + (A_DMA * wave + u) * 1024);
 #pragma unroll
@@ -172,6 +181,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pk_kernel(
   };
 
   bf16x8 fa[NS][NP][TM], fw[NS][NP][TN];
+  // prologue: tiles 0 and 1 (both ring depths refill with tile kt+2 during iteration kt)
   if (nk > 0) issue(0);
   if (nk > 1) issue(1);
   for (int kt = 0; kt < nk; ++kt) {
@@ -180,7 +190,13 @@ __global__ __launch_bounds__(512, 1) void gemm_pk_kernel(
     else wait_vm<0>();
     if (diag != 3) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    const unsigned char* st = pk_smem + (kt & 1) * STAGE;
+    if constexpr (NST == 3) {
+      // 3-stage ring: every wave is past this barrier, so every wave has finished reading tile
+      // kt-1 — its stage takes tile kt+2 right away, and one barrier per K-tile suffices
+      if (kt + 2 < nk && diag != 1) issue(kt + 2);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const unsigned char* st = pk_smem + (kt % NST) * STAGE;
     auto read_step = [&](int s) {
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
@@ -220,12 +236,14 @@ __global__ __launch_bounds__(512, 1) void gemm_pk_kernel(
     }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
-    // every wave holds tile kt in registers: refill its stage with tile kt+2
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (diag != 2 && diag != 3) __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (kt + 2 < nk && diag != 1) issue(kt + 2);
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (NST == 2) {
+      // every wave holds tile kt in registers: refill its stage with tile kt+2
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (diag != 2 && diag != 3) __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + 2 < nk && diag != 1) issue(kt + 2);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = NS0; s < NS; ++s) {
@@ -315,7 +333,7 @@ constexpr int PK_GROUP_M = 4;  // grouped tile order: 4 > 8 > 16 > 32 M-tiles by
 template <int BN, int NP, int EPI, int DIAG>
 hipError_t pk_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R, float* C,
                      __bf16* Cp, int M, int N, int K, hipStream_t st) {
-  constexpr int lds = 2 * (PK_BM + BN) * PK_ROWB;
+  constexpr int lds = pk_stages<BN>() * (PK_BM + BN) * PK_ROWB;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)gemm_pk_kernel<BN, NP, EPI, DIAG>,
