@@ -190,13 +190,68 @@ __global__ __launch_bounds__(512, 1) void gemm_pk_kernel(
     else wait_vm<0>();
     if (diag != 3) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    const unsigned char* st = pk_smem + (kt % NST) * STAGE;
     if constexpr (NST == 3) {
       // 3-stage ring: every wave is past this barrier, so every wave has finished reading tile
-      // kt-1 — its stage takes tile kt+2 right away, and one barrier per K-tile suffices
-      if (kt + 2 < nk && diag != 1) issue(kt + 2);
+      // kt-1 — its stage takes tile kt+2 during this K-tile, and one barrier per K-tile suffices.
+      // Issue order, pinned: step-0 fragment reads, then the step-0.. MFMAs with the later
+      // steps' fragment reads and the DMA pieces of tile kt+2 spread between them (a DMA piece
+      // issued in a burst holds the wave's issue for ~60-100 cycles each; between MFMAs it
+      // hides in their issue gaps), then the last step's MFMAs.
+      constexpr int T = NP == 2 ? 3 : 1;
+      constexpr int MPS = T * TM * TN;           // MFMAs per 16-deep step
+      constexpr int RPS = NP * (TM + TN);         // fragment reads per step
+      constexpr int MU = (NS - 1) * MPS, RU = (NS - 1) * RPS;
+      auto read_one = [&](int s, int i) {        // i-th fragment read of step s
+        const int p = i / (TM + TN), j = i % (TM + TN);
+        const int coff = 16 * ((4 * p + 2 * s + lh) ^ sw);
+        if (j < TN)
+          fw[s][p][j] = *reinterpret_cast<const bf16x8*>(st + w_row0 + j * 32 * PK_ROWB + coff);
+        else
+          fa[s][p][j - TN] =
+              *reinterpret_cast<const bf16x8*>(st + a_row0 + (j - TN) * 32 * PK_ROWB + coff);
+      };
+      auto mfma_one = [&](int s, int i) {        // i-th MFMA of step s
+        const int a = i / (T * TN), b = (i / T) % TN, term = i % T;
+        if (diag == 5) {
+          keep_f32(acc[a][b][0]);
+          return;
+        }
+        const bf16x8& x = (T == 3 && term == 0) ? fa[s][NP - 1][a] : fa[s][0][a];
+        const bf16x8& y = (T == 3 && term == 1) ? fw[s][NP - 1][b] : fw[s][0][b];
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, acc[a][b], 0, 0, 0);
+      };
+      const bool refill = kt + 2 < nk && diag != 1;
+      const int kb = (kt + 2) * PK_ROWB;
+      const uint32_t nst = lds0 + ((kt + 2) % NST) * STAGE;
+      auto dma_one = [&](int j) {
+        if (!refill) return;
+        if (j < A_DMA) dma16(a_src[j] + kb, nst + (A_DMA * wave + j) * 1024);
+        else dma16(w_src[j - A_DMA] + kb, nst + A_BYTES + (W_DMA * wave + j - A_DMA) * 1024);
+      };
+#pragma unroll
+      for (int i = 0; i < RPS; ++i)
+        if (diag != 4 || kt == 0) read_one(0, i);
       __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(0);
+      // MU MFMAs, RU reads and the DMA pieces in DMA groups, each group's share pinned in order
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int g = 0; g < DMA; ++g) {
+#pragma unroll
+        for (int i = g * MU / DMA; i < (g + 1) * MU / DMA; ++i) mfma_one(i / MPS, i % MPS);
+#pragma unroll
+        for (int i = g * RU / DMA; i < (g + 1) * RU / DMA; ++i)
+          if (diag != 4 || kt == 0) read_one(1 + i / RPS, i % RPS);
+        __builtin_amdgcn_sched_barrier(0);
+        dma_one(g);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int i = 0; i < MPS; ++i) mfma_one(NS - 1, i);
+      __builtin_amdgcn_s_setprio(0);
+      continue;
     }
-    const unsigned char* st = pk_smem + (kt % NST) * STAGE;
     auto read_step = [&](int s) {
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
@@ -289,7 +344,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pk_kernel(
             bf16x8 h, l;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-              const float v = gelu_erf(slab[rr * 33 + c8 + e] + (e < 4 ? b0[e] : b1[e - 4]));
+              const float v = gelu_erfc_fast(slab[rr * 33 + c8 + e] + (e < 4 ? b0[e] : b1[e - 4]));
               const __bf16 hv = (__bf16)v;
               h[e] = hv;
               l[e] = (__bf16)(v - (float)hv);

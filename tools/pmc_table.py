@@ -8,7 +8,7 @@ import sys
 root = pathlib.Path(sys.argv[1])
 pat = sys.argv[2]
 min_grid = int(sys.argv[3]) if len(sys.argv) > 3 else 0
-for run in sorted(p for p in root.iterdir() if p.is_dir()):
+for run in sorted(p for p in root.iterdir() if p.is_dir() and p.name.startswith("pmc")):
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in run.glob("p*/**/run_counter_collection.csv"):
         for r in csv.DictReader(open(f)):
