@@ -15,7 +15,7 @@ import random
 
 import numpy as np
 
-from .host import MODE_BATCH, MODE_SINGLE, Example
+from .host import MODE_BATCH, MODE_RAW, MODE_SINGLE, Example
 from .utils import (CodeDataset, InputFeatures, IdsDataset, _tokenize, crossover,
                     get_identifier_posistions_from_code, get_masked_code_by_position, isUID,
                     map_chromesome, mutate, select_parents)
@@ -26,19 +26,52 @@ def _label_of(example):
     return int(lab.item()) if hasattr(lab, "item") else int(lab)
 
 
-def convert_code_to_features(code, tokenizer, label, args):
-    """attacker.py:38-45 (host tokenizer; ' '.join(code.split()) -> [:block-2] -> CLS/SEP/pad)."""
-    ids, _ = tokenizer.featurize([code], args.block_size)
-    row = ids[0].tolist()
-    n = int((ids[0] != tokenizer.pad_token_id).sum())
-    return InputFeatures(None, row, 0, label)
+def convert_code_to_features(code, tokenizer, label, args, raw: bool = False):
+    """attacker.py:38-45 (host tokenizer; ' '.join(code.split()) -> [:block-2] -> CLS/SEP/pad).
+    raw: the Authorship-Attribution form, which tokenizes the text as is
+    (CodeXGLUE/Authorship-Attribution/code/attacker.py:31-37)."""
+    ids, _ = tokenizer.featurize([code], args.block_size, raw=raw)
+    return InputFeatures(None, ids[0].tolist(), 0, label)
+
+
+def remove_python_docstrings(source: str) -> str:
+    """remove_comments_and_docstrings(source, 'python') (python_parser/parser_folder/utils.py:
+    31-68): re-emit the stdlib tokenize stream without comments and without string tokens that
+    open a logical line (after INDENT / NEWLINE, or at column 0), then drop blank lines."""
+    import io
+    import tokenize
+
+    out, prev, last_line, last_col = "", tokenize.INDENT, -1, 0
+    for tok in tokenize.generate_tokens(io.StringIO(source).readline):
+        ttype, text, (sl, sc), (el, ec), _ = tok
+        if sl > last_line:
+            last_col = 0
+        if sc > last_col:
+            out += " " * (sc - last_col)
+        if ttype == tokenize.COMMENT:
+            pass
+        elif ttype == tokenize.STRING:
+            if prev != tokenize.INDENT and prev != tokenize.NEWLINE and sc > 0:
+                out += text
+        else:
+            out += text
+        prev, last_col, last_line = ttype, ec, el
+    return "\n".join(x for x in out.split("\n") if x.strip() != "")
 
 
 def get_identifiers(code, lang):
     """run_parser.py:272-281 — (identifiers as [[name]], code_tokens): the unique valid names of
-    the data-flow graph (C; host/dfg.cpp) and the comment-stripped leaves."""
+    the data-flow graph (host/dfg.cpp) and the comment-stripped leaves.  For Python,
+    extract_dataflow (run_parser.py:190-199) first turns literal '\n' into newlines and strips
+    comments and docstrings with the tokenize-based remover (left as is if that raises)."""
     from .utils import is_valid_variable_name
 
+    if lang == "python":
+        code = code.replace("\\n", "\n")
+        try:
+            code = remove_python_docstrings(code)
+        except Exception:
+            pass
     ex = Example(code, lang)
     toks = ex.leaves(identifiers=True)
     idents = [[n] for n in ex.dfg_names() if is_valid_variable_name(n, lang)]
@@ -46,7 +79,7 @@ def get_identifiers(code, lang):
 
 
 class _Scorer:
-    """Victim requests for one attacked example: ids built from chromosomes (host + device
+    """Victim requests for one attacked program: ids built from chromosomes (host + device
     splice) or from texts."""
 
     def __init__(self, attacker, code, lang="c"):
@@ -55,12 +88,28 @@ class _Scorer:
 
     def population(self, pops, mode):
         """pops: list of [(tgt, sub), ...] -> a request (Payload) of len(pops) queries."""
-        return self.a.model_tgt.prepare_population(self.ex, self.a.tokenizer_tgt, pops, mode,
-                                                   self.a.args.block_size)
+        return self.a._population(self.ex, pops, mode)
 
-    def texts(self, texts):
-        m = self.a.model_tgt
-        return m.prepare(m.dataset_from_texts(texts, self.a.tokenizer_tgt, self.a.args))
+
+def join_payloads(payloads):
+    """Concatenate requests of one victim into one (rows in order, queries summed)."""
+    from .model import Payload
+
+    ps = [p for p in payloads if p.n]
+    if len(ps) == 1:
+        return ps[0]
+    first = ps[0]
+    if isinstance(first.ids, np.ndarray):
+        ids = np.concatenate([p.ids for p in ps], 0)
+    else:
+        import torch
+
+        ids = torch.cat([p.ids for p in ps], 0)
+    lens = None if any(p.lens is None for p in ps) else np.concatenate([p.lens for p in ps])
+    extra = None
+    if first.extra is not None:
+        extra = tuple(np.concatenate([p.extra[k] for p in ps]) for k in range(len(first.extra)))
+    return Payload(ids, lens, sum(p.n for p in ps), extra)
 
 
 def answer(model, gen):
@@ -74,14 +123,18 @@ def answer(model, gen):
         return stop.value
 
 
-def _importance_gen(args, words_list, variable_names, tgt_model, tokenizer):
+def _importance_gen(args, words_list, variable_names, tgt_model, tokenizer, payload_fn=None):
     """get_importance_score as a request generator (attacker.py:48-83)."""
     positions = get_identifier_posistions_from_code(words_list, variable_names)
     if len(positions) == 0:
         return None, None, None
     masked_token_list, replace_token_positions = get_masked_code_by_position(words_list, positions)
-    texts = [" ".join(tokens) for tokens in [words_list] + masked_token_list]
-    logits, preds = yield tgt_model.prepare(tgt_model.dataset_from_texts(texts, tokenizer, args))
+    if payload_fn is not None:
+        req = payload_fn([words_list] + masked_token_list)
+    else:
+        texts = [" ".join(tokens) for tokens in [words_list] + masked_token_list]
+        req = tgt_model.prepare(tgt_model.dataset_from_texts(texts, tokenizer, args))
+    logits, preds = yield req
     orig_probs = logits[0]
     orig_label = preds[0]
     orig_prob = max(orig_probs)
@@ -104,7 +157,7 @@ def compute_fitness(chromesome, codebert_tgt, tokenizer_tgt, orig_prob, orig_lab
         new_logits, preds = codebert_tgt.score_prepared(
             [scorer.population([list(chromesome.items())], MODE_BATCH)])[0]
     else:
-        temp_code = map_chromesome(chromesome, code, "c")
+        temp_code = map_chromesome(chromesome, code, getattr(args, "lang", "c"))
         new_feature = convert_code_to_features(temp_code, tokenizer_tgt, true_label, args)
         new_logits, preds = codebert_tgt.get_results(CodeDataset([new_feature]), args.eval_batch_size)
     fitness_value = orig_prob - new_logits[0][orig_label]
@@ -118,7 +171,18 @@ class Attacker:
     receives (probs, preds) back: greedy_attack / ga_attack answer every request with its own
     call (the reference loop, Python's global `random`), while drivers.run_gi_attack_batched
     keeps many examples' generators in flight and answers all their pending requests with ONE
-    device batch (each example on its own `random.Random(seed + index)`)."""
+    device batch (each example on its own `random.Random(seed + index)`).
+
+    The same generators serve the task variants through a few hooks:
+      Devign (CodeBERT)       CodeXGLUE/Defect-detection/code/attacker.py        lang 'c'
+      Authorship-Attribution  CodeXGLUE/Authorship-Attribution/code/attacker.py  lang 'python',
+                              raw-text featurisation (the Model of task 'authorship'), no -3
+                              exit for an empty gene pool in ga_attack (:147-150)
+      Clone (pairs)           CloneAttacker below
+      GraphCodeBERT variants  the GraphModel victims (graph.py) behind the same hooks
+    """
+
+    ga_empty_check = True  # ga_attack returns -3 when no substitutable name occurs as a word
 
     def __init__(self, args, model_tgt, tokenizer_tgt, model_mlm, tokenizer_mlm, use_bpe,
                  threshold_pred_score) -> None:
@@ -134,6 +198,14 @@ class Attacker:
         # the GraphCodeBERT Devign and CodeBERT clone attackers hard-code 64
         # (GraphCodeBERT/Defect-detection/code/attacker.py:246)
         self.ga_batch = None
+
+    # ---- hooks ---------------------------------------------------------------------------------
+    def _population(self, ex, pops, mode):
+        return self.model_tgt.prepare_population(ex, self.tokenizer_tgt, pops, mode,
+                                                 self.args.block_size)
+
+    def _importance_payload(self):
+        return None  # texts through Model.dataset_from_texts
 
     # ------------------------------------------------------------------------------------------
     def ga_attack(self, example, code, substituions, initial_replace=None):
@@ -174,7 +246,7 @@ class Attacker:
         nb_changed_pos = 0
         is_success = -1
         variable_substitue_dict = {w: substituions[w] for w in names_positions_dict.keys()}
-        if len(variable_substitue_dict) == 0:
+        if self.ga_empty_check and len(variable_substitue_dict) == 0:
             return code, prog_length, adv_code, true_label, orig_label, temp_label, -3, \
                 variable_names, None, None, None, None
 
@@ -237,7 +309,7 @@ class Attacker:
             mutate_fitness_values = []
             for index, logits in enumerate(mutate_logits):
                 if mutate_preds[index] != orig_label:
-                    adv_code = map_chromesome(_temp_mutants[index], code, "c", scorer.ex)
+                    adv_code = map_chromesome(_temp_mutants[index], code, self.lang, scorer.ex)
                     for old_word in _temp_mutants[index].keys():
                         if old_word == _temp_mutants[index][old_word]:
                             nb_changed_var += 1   # counts UNchanged names (reference quirk)
@@ -281,7 +353,8 @@ class Attacker:
                 variable_names, None, None, None, None
 
         importance_score, replace_token_positions, names_positions_dict = yield from \
-            _importance_gen(self.args, words, variable_names, m, self.tokenizer_tgt)
+            _importance_gen(self.args, words, variable_names, m, self.tokenizer_tgt,
+                            self._importance_payload())
         if importance_score is None:
             return code, prog_length, adv_code, true_label, orig_label, temp_label, -3, \
                 variable_names, None, None, None, None
@@ -349,8 +422,109 @@ class Attacker:
             replaced_words
 
 
+class AuthorshipAttacker(Attacker):
+    """CodeXGLUE/Authorship-Attribution/code/attacker.py: the Devign attacker on Python code with a
+    66-way victim (argmax predictions), raw-text featurisation (the 'authorship' Model) and no -3
+    exit for an empty gene pool in ga_attack (:147-150: the reference then runs its GA loop on an
+    empty chromosome and fails inside mutate, which this class reproduces by raising)."""
+
+    ga_empty_check = False
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.lang = "python"
+
+
+class CloneAttacker(Attacker):
+    """CodeXGLUE/Clone-detection-BigCloneBench/code/attacker.py: a pair (code1, code2) is one
+    query; the victim reads [ids(code1) | ids(code2)] as two block-size rows and a 2-way pair
+    head.  Only code1 is perturbed.  Differences from the Devign attacker this class keeps:
+      * signatures greedy_attack(example, substitutes, code) / ga_attack(example, substitutes,
+        code, initial_replace) with code = (id1, id2, code1, code2) (:89, :285); the returned
+        code is that tuple;
+      * Java leaves / mutants (get_identifiers(code1, 'java'), get_example(..., 'java'));
+      * code2's half of every mutant row: tokenize(' '.join(code2.split())) (:128-129);
+      * importance features from WORDS: convert_examples_to_features is handed whole words of
+        code1 (masked with '<unk>') and of " ".join(get_identifiers(code2)[1]) split like
+        _tokenize, so each word becomes ONE id through convert_tokens_to_ids (the unk id unless
+        the word is itself a vocabulary token) (:48-71 with run.py:102-119);
+      * 64 GA mutants per iteration whatever eval_batch_size is (:226)."""
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.lang = "java"
+        self.ga_batch = 64
+        self._code2 = None
+
+    # ---- reference signatures ---------------------------------------------------------------
+    def ga_attack(self, example, substitutes, code, initial_replace=None):
+        return answer(self.model_tgt, self.ga_gen(example, substitutes, code, initial_replace,
+                                                  random))
+
+    def greedy_attack(self, example, substitutes, code):
+        return answer(self.model_tgt, self.greedy_gen(example, substitutes, code))
+
+    def ga_gen(self, example, substitutes, code, initial_replace=None, rng=random):
+        res = yield from self._bound(code, super().ga_gen(example, code[2], substitutes,
+                                                          initial_replace, rng))
+        return (code,) + tuple(res[1:])
+
+    def greedy_gen(self, example, substitutes, code):
+        res = yield from self._bound(code, super().greedy_gen(example, code[2], substitutes))
+        return (code,) + tuple(res[1:])
+
+    # ---- pair requests ------------------------------------------------------------------------
+    def _bound(self, code, gen):
+        """Run `gen` with this pair's code2 bound: code2's fixed half of every row and its
+        word-level importance half.  The binding is re-installed before every step, since the
+        batched driver interleaves many pairs' generators over one attacker (requests are built
+        before they are yielded, so each sees its own pair)."""
+        L = self.args.block_size
+        ids2, lens2 = self.tokenizer_tgt.featurize([code[3]], L)
+        _, toks2 = get_identifiers(code[3], self.lang)
+        words2 = " ".join(toks2).replace("\n", "").split(" ")
+        bound = (ids2[0], int(lens2[0]), self._word_row(words2))
+        self._code2 = bound
+        try:
+            req = next(gen)
+            while True:
+                ans = yield req
+                self._code2 = bound
+                req = gen.send(ans)
+        except StopIteration as stop:
+            return stop.value
+
+    def _word_row(self, words):
+        """[cls] + convert_tokens_to_ids(words[:L-2]) + [sep] + pad (run.py:102-119)."""
+        t, L = self.tokenizer_tgt, self.args.block_size
+        body = t.convert_tokens_to_ids(list(words[:L - 2]))
+        row = [t.cls_token_id] + list(body) + [t.sep_token_id]
+        return np.asarray(row + [t.pad_token_id] * (L - len(row)), dtype=np.int32)
+
+    def _population(self, ex, pops, mode):
+        m = self.model_tgt
+        ids1, lens1 = m.population_rows(ex, self.tokenizer_tgt, pops, mode, self.args.block_size)
+        ids2, len2, _ = self._code2
+        return m.prepare_pairs(ids1, lens1, ids2, len2)
+
+    def _importance_payload(self):
+        ids2w = self._code2[2]
+
+        def build(word_lists):
+            ids1 = np.stack([self._word_row(w) for w in word_lists])
+            lens1 = (ids1 != self.tokenizer_tgt.pad_token_id).sum(1).astype(np.int32)
+            lens2 = int((ids2w != self.tokenizer_tgt.pad_token_id).sum())
+            return self.model_tgt.prepare_pairs(ids1, lens1, ids2w, lens2)
+
+        return build
+
+
 class MHM_Attacker:
     """MHM-NS baseline (attacker.py:457-738)."""
+
+    # __replaceUID_random drops random-vocabulary candidates that already name a variable
+    # (attacker.py:732-733); the Authorship-Attribution copy does not
+    skip_known_uids = True
 
     def __init__(self, args, model_tgt, model_mlm, tokenizer_mlm, _token2idx, _idx2token) -> None:
         self.classifier = model_tgt
@@ -361,8 +535,8 @@ class MHM_Attacker:
         self.tokenizer_mlm = tokenizer_mlm
         self.lang = getattr(args, "lang", "c")
 
-    # The MCMC loop is written once, as a generator: every victim query is a `yield (ids, lens)`
-    # that receives `(probs, preds)` back.  `_run` answers each request with its own get_results
+    # The MCMC loop is written once, as a generator: every victim query is a `yield <Payload>`
+    # (the victim's request API, model.py) that receives `(probs, preds)` back.  `_run` answers each request with its own get_results
     # call (the reference's one-example-at-a-time behaviour); `mcmc_batched` answers the pending
     # requests of many examples with ONE device batch.  Rows are scored batch-invariantly, so the
     # two give identical results; `rng` is the Python `random` module (sequential, as the
@@ -372,13 +546,7 @@ class MHM_Attacker:
              replace, attack_type):
         gen = self._run_gen(tokenizer, substituions, code, _label, _n_candi, _max_iter,
                             _prob_threshold, replace, attack_type, random)
-        try:
-            req = next(gen)
-            while True:
-                req = gen.send(self.classifier.get_results(IdsDataset(*req),
-                                                           self.args.eval_batch_size))
-        except StopIteration as stop:
-            return stop.value
+        return answer(self.classifier, gen)
 
     def _run_gen(self, tokenizer, substituions, code, _label, _n_candi, _max_iter, _prob_threshold,
                  replace, attack_type, rng):
@@ -487,20 +655,15 @@ class MHM_Attacker:
                 nxt += 1
             if not live:
                 break
-            ids = np.concatenate([c[2][0] for c in live], 0)
-            lens = np.concatenate([c[2][1] for c in live], 0)
-            prob, pred = self.classifier.get_results(IdsDataset(ids, lens),
-                                                     self.args.eval_batch_size)
-            still, off = [], 0
-            for c in live:
-                n = c[2][0].shape[0]
-                c[3] += n
+            answers = self.classifier.score_prepared([c[2] for c in live])
+            still = []
+            for c, ans in zip(live, answers):
+                c[3] += c[2].n
                 try:
-                    c[2] = c[1].send((prob[off:off + n], pred[off:off + n]))
+                    c[2] = c[1].send(ans)
                     still.append(c)
                 except StopIteration as stop:
                     finish(c[0], stop.value, c[3])
-                off += n
             live = still
         return out
 
@@ -512,14 +675,7 @@ class MHM_Attacker:
         tok = self.tokenizer_mlm
         L = self.args.block_size
         pops = [[(selected_uid, c)] for c in candi_pairs]
-        ids0, lens0 = tok.featurize([_tokens], L)
-        if pops:
-            idsm, lensm = ex.mutant_ids(tok, pops, L, MODE_SINGLE)
-            ids = np.concatenate([ids0, idsm], 0)
-            lens = np.concatenate([lens0, lensm], 0)
-        else:
-            ids, lens = ids0, lens0
-        prob, pred = yield (ids, lens)
+        prob, pred = yield self._candidates_request(ex, tok, _tokens, pops, L)
         candi_tokens = [_tokens] + [None] * len(pops)
 
         def text(i):
@@ -548,6 +704,18 @@ class MHM_Attacker:
                 "old_pred": pred[0], "new_pred": pred[i],
                 "nb_changed_pos": _tokens.count(selected_uid)}
 
+    def _candidates_request(self, ex, tok, _tokens, pops, L):
+        """One request: the unmodified code, then get_example(code, uid, c) per candidate."""
+        m = self.classifier
+        first = m.prepare(m.dataset_from_texts([_tokens], tok, self.args))
+        if not pops:
+            return first
+        if hasattr(m, "population_rows"):
+            rows = m.population_rows(ex, tok, pops, MODE_SINGLE, L)
+            return join_payloads([first, type(first)(rows[0], rows[1], len(pops))])
+        texts = [ex.mutant_text(p, MODE_SINGLE) for p in pops]
+        return join_payloads([first, m.prepare(m.dataset_from_texts(texts, tok, self.args))])
+
     def _replace_uid(self, rng, _tokens, _label=None, _uid={}, substitute_dict={}, _n_candi=30,
                      _prob_threshold=0.95, _candi_mode="random"):
         assert _candi_mode.lower() in ["random", "nearby"]
@@ -571,7 +739,7 @@ class MHM_Attacker:
         candi_token = [selected_uid]
         pairs = []
         for c in rng.sample(self.idx2token, _n_candi):
-            if c in _uid.keys():
+            if self.skip_known_uids and c in _uid.keys():
                 continue
             if isUID(c):
                 candi_token.append(c)
@@ -587,3 +755,25 @@ class MHM_Attacker:
             _prefix, _iter, tag, _res["old_uid"], _res["new_uid"], _res["old_pred"],
             _res["new_pred"], _res["old_prob"][_res["old_pred"]],
             _res["new_prob"][_res["old_pred"]], _res["alpha"]), flush=True)
+
+
+class AuthorshipMHM_Attacker(MHM_Attacker):
+    """CodeXGLUE/Authorship-Attribution/code/attacker.py:425-700: Python leaves, the raw-text
+    victim, the substitutes passed last (`mcmc(tokenizer, code, _label, ..., subs={})`, the call
+    form of Authorship-Attribution/code/mhm.py:199-206), and no skip of known variable names
+    among the random candidates of mcmc_random."""
+
+    skip_known_uids = False
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.lang = "python"
+
+    def mcmc(self, tokenizer, code=None, _label=None, _n_candi=30, _max_iter=100,
+             _prob_threshold=0.95, subs={}):
+        return super().mcmc(tokenizer, subs, code, _label, _n_candi, _max_iter, _prob_threshold)
+
+    def mcmc_random(self, tokenizer, code=None, _label=None, _n_candi=30, _max_iter=100,
+                    _prob_threshold=0.95, subs={}):
+        return super().mcmc_random(tokenizer, subs, code, _label, _n_candi, _max_iter,
+                                   _prob_threshold)

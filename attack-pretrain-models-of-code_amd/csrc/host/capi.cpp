@@ -48,6 +48,24 @@ void featurize_words(ah::Tokenizer& t, const std::vector<std::string>& words, in
   *len = n + 2 - pads;
 }
 
+// convert_code_to_features WITHOUT the whitespace normalisation (the Authorship-Attribution
+// victim tokenises the raw source: CodeXGLUE/Authorship-Attribution/code/attacker.py:31-37)
+void featurize_raw(ah::Tokenizer& t, const std::string& code, int32_t L, int32_t* ids,
+                   int32_t* len) {
+  std::vector<int32_t> toks;
+  t.encode(code, toks);
+  const int32_t n = std::min<int32_t>((int32_t)toks.size(), L - 2);
+  ids[0] = t.cls_id;
+  int32_t pads = 0;
+  for (int32_t k = 0; k < n; ++k) {
+    ids[1 + k] = toks[k];
+    pads += toks[k] == t.pad_id;
+  }
+  ids[1 + n] = t.sep_id;
+  for (int32_t k = n + 2; k < L; ++k) ids[k] = t.pad_id;
+  *len = n + 2 - pads;
+}
+
 bool build_mutant(ah_example* e, int32_t mode, int32_t b, int32_t end, const char* const* tgts,
                   const char* const* subs, std::string& out) {
   if (mode == AH_MODE_SINGLE) {
@@ -120,6 +138,20 @@ int32_t ah_featurize_batch(ah_tokenizer* t, int32_t n, const char* const* codes,
   return n;
 }
 
+int32_t ah_featurize_batch_raw(ah_tokenizer* t, int32_t n, const char* const* codes, int32_t L,
+                               int32_t* ids_out, int32_t* lens_out) {
+  if (!t || !codes || !ids_out || !lens_out || L < 2) return fail("bad argument");
+  for (int32_t i = 0; i < n; ++i)
+    featurize_raw(t->t, codes[i], L, ids_out + (size_t)i * L, lens_out + i);
+  return n;
+}
+
+int32_t ah_tokens_to_ids(ah_tokenizer* t, int32_t n, const char* const* tokens, int32_t* ids_out) {
+  if (!t || (n && (!tokens || !ids_out))) return fail("bad argument");
+  for (int32_t i = 0; i < n; ++i) ids_out[i] = t->t.token_to_id(tokens[i]);
+  return n;
+}
+
 ah_example* ah_example_new(const char* code, int32_t lang) {
   if (!code || lang < 0 || lang > 2) {
     fail("bad argument");
@@ -170,11 +202,14 @@ int32_t ah_example_mutants(ah_example* e, ah_tokenizer* t, int32_t mode, int32_t
                            const char* const* subs, int32_t L, int32_t* ids_out,
                            int32_t* lens_out) {
   if (!e || !t || !pair_off || !ids_out || !lens_out || L < 2) return fail("bad argument");
+  const bool raw = (mode & AH_MODE_RAW) != 0;
+  mode &= ~AH_MODE_RAW;
   std::string code;
   for (int32_t m = 0; m < n_mut; ++m) {
     if (!build_mutant(e, mode, pair_off[m], pair_off[m + 1], tgts, subs, code))
       return fail("single mode needs 1 pair per mutant");
-    featurize_words(t->t, ah::py_split(code), L, ids_out + (size_t)m * L, lens_out + m);
+    if (raw) featurize_raw(t->t, code, L, ids_out + (size_t)m * L, lens_out + m);
+    else featurize_words(t->t, ah::py_split(code), L, ids_out + (size_t)m * L, lens_out + m);
   }
   return n_mut;
 }

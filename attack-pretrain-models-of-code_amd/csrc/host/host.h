@@ -33,6 +33,11 @@ class Tokenizer {
   const std::vector<int32_t>& word_ids(const std::string& word, bool first);
   int32_t cls_id = 0, sep_id = 2, pad_id = 1, unk_id = 3, mask_id = 50264;
   const std::string& id_to_token(int32_t id) const { return inv_[id]; }
+  // convert_tokens_to_ids of one token string (unk_id when it is not in the vocabulary)
+  int32_t token_to_id(const std::string& token) const {
+    auto it = vocab_.find(token);
+    return it == vocab_.end() ? unk_id : it->second;
+  }
   size_t vocab_size() const { return inv_.size(); }
   // decode byte-level tokens to text (tokenizer._decode / convert_tokens_to_string)
   std::string decode(const int32_t* ids, int n) const;

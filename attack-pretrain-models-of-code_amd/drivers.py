@@ -1,8 +1,13 @@
 """Attack drivers: the per-example loops of gi_attack.py (greedy, then GA on failure) and
-mhm_attack.py (MHM-NS), over the engine.
+mhm_attack.py (MHM-NS), over the engine, for the three CodeBERT victims:
 
-Follows CodeXGLUE/Defect-detection/code/gi_attack.py:154-218 and mhm_attack.py:160-236: the
-original example's features come from the fixture's `func` (run.py:79-86), substitutes from its
+  devign      CodeXGLUE/Defect-detection/code/gi_attack.py:154-218, mhm_attack.py:160-236
+  clone       CodeXGLUE/Clone-detection-BigCloneBench/code/attack.py:160-231 (pairs; the attack
+              perturbs code1; `code` = (id1, id2, code1, code2))
+  authorship  CodeXGLUE/Authorship-Attribution/code/attack.py:199-266, mhm.py:160-233 (Python,
+              66 authors, raw-text features; labels from valid.txt, codes from valid_subs.jsonl)
+
+The original example's features come from the fixture (run.py of each task), substitutes from its
 `substitutes`; one Recorder CSV row per example; success rate over examples the victim classified
 correctly.  Also the multi-GPU form: examples are pulled from a dynamic queue shared by all ranks
 (an atomic counter in the torch.distributed store; no tensor traffic) and the per-rank statistics
@@ -17,7 +22,8 @@ import time
 
 import numpy as np
 
-from .attacker import Attacker, MHM_Attacker
+from .attacker import (Attacker, AuthorshipAttacker, AuthorshipMHM_Attacker, CloneAttacker,
+                       MHM_Attacker, get_identifiers)
 from .host import Tokenizer
 from .utils import Recorder, build_vocab, set_seed
 
@@ -33,46 +39,78 @@ class AttackArgs:
     csv_store_path: str | None = None
     rng: str = "global"   # "global": one random stream in example order (reference);
                           # "per_example": random.seed(seed + index) before each example
+    task: str = "devign"  # devign | clone | authorship (CodeBERT victims)
 
 
-def load_fixture(path, start=0, end=None):
+def load_fixture(path, start=0, end=None, labels_path=None):
+    """codes, substitutes, labels of a test_subs / valid_subs jsonl.  Devign: `func`, `target`;
+    clone: code = (id1, id2, code1, code2), `label` (Clone-detection-BigCloneBench/code/run.py:
+    160-175); authorship: `code` with literal '\\n' turned into newlines (attack.py:205-211), the
+    label from the `code <CODESPLIT> label` lines of `labels_path` (run.py:112-116)."""
     codes, subs, labels = [], [], []
+    ext = None
+    if labels_path is not None:
+        ext = [int(line.split(" <CODESPLIT> ")[1]) for line in open(labels_path)]
     with open(path) as f:
         for i, line in enumerate(f):
             if i < start or (end is not None and i >= end):
                 continue
             js = json.loads(line)
-            codes.append(js["func"] if "func" in js else js["code"])
+            if "code1" in js:
+                codes.append((js.get("id1"), js.get("id2"), js["code1"], js["code2"]))
+            elif "func" in js:
+                codes.append(js["func"])
+            else:
+                codes.append(js["code"].replace("\\n", "\n"))
             subs.append(js["substitutes"])
-            labels.append(int(js.get("target", js.get("label", 0))))
+            labels.append(ext[i] if ext is not None else int(js.get("target", js.get("label", 0))))
     return codes, subs, labels
 
 
-def _example(tok, code, label, block):
-    """TextDataset item: (ids, label) of ' '.join(func.split()) (run.py:79-86)."""
+def _example(tok, code, label, block, task="devign"):
+    """TextDataset item of each task: devign (ids of ' '.join(func.split()), label) (run.py:79-86);
+    clone ([ids(code1) | ids(code2)], label) (Clone-detection-BigCloneBench/code/run.py:65-119);
+    authorship (ids of the raw code, label) (Authorship-Attribution/code/run.py:81-89)."""
     import torch
 
-    ids, _ = tok.featurize([code], block)
-    return torch.from_numpy(ids[0].astype(np.int64)), torch.tensor(label)
+    if task == "clone":
+        ids, _ = tok.featurize([code[2], code[3]], block)
+        row = np.concatenate([ids[0], ids[1]])
+    else:
+        ids, _ = tok.featurize([code], block, raw=task == "authorship")
+        row = ids[0]
+    return torch.from_numpy(row.astype(np.int64)), torch.tensor(label)
+
+
+ATTACKERS = {"devign": Attacker, "clone": CloneAttacker, "authorship": AuthorshipAttacker}
+
+
+def make_attacker(args, model, tok):
+    return ATTACKERS[getattr(args, "task", "devign")](args, model, tok, None, tok, use_bpe=1,
+                                                      threshold_pred_score=0)
 
 
 def attack_one(attacker, tok, code, subs, label, args):
-    example = _example(tok, code, label, args.block_size)
-    res = attacker.greedy_attack(example, code, subs)
+    task = getattr(args, "task", "devign")
+    example = _example(tok, code, label, args.block_size, task)
+    first = (subs, code) if task == "clone" else (code, subs)  # clone: (example, subs, code)
+    res = attacker.greedy_attack(example, *first)
     attack_type = "Greedy"
     if res[6] == -1 and args.use_ga:
-        res = attacker.ga_attack(example, code, subs, initial_replace=res[11])
+        res = attacker.ga_attack(example, *first, initial_replace=res[11])
         attack_type = "GA"
     return res, attack_type
 
 
 def attack_one_gen(attacker, tok, code, subs, label, args, rng):
     """attack_one as a request generator (gi_attack.py:177-186): greedy, then GA on -1."""
-    example = _example(tok, code, label, args.block_size)
-    res = yield from attacker.greedy_gen(example, code, subs)
+    task = getattr(args, "task", "devign")
+    example = _example(tok, code, label, args.block_size, task)
+    first = (subs, code) if task == "clone" else (code, subs)
+    res = yield from attacker.greedy_gen(example, *first)
     attack_type = "Greedy"
     if res[6] == -1 and args.use_ga:
-        res = yield from attacker.ga_gen(example, code, subs, res[11], rng)
+        res = yield from attacker.ga_gen(example, *first, res[11], rng)
         attack_type = "GA"
     return res, attack_type
 
@@ -115,8 +153,7 @@ def run_gi_attack_batched(model, codes, subs, labels, args: AttackArgs, indices=
     so each record is exactly the sequential run with rng="per_example" (same outcome, mutants,
     adversarial code and query count); records come back in example order."""
     tok = tok or Tokenizer()
-    attacker = Attacker(args, model, tok, None, tok, use_bpe=1, threshold_pred_score=0)
-    attacker.ga_batch = getattr(args, "ga_batch", None)
+    attacker = make_attacker(args, model, tok)
     recorder = Recorder(args.csv_store_path) if args.csv_store_path else None
     order = list(range(len(codes))) if indices is None else list(indices)
     pos = 0
@@ -167,7 +204,7 @@ def run_gi_attack(model, codes, subs, labels, args: AttackArgs, indices=None, to
     """greedy (+GA) over the given examples; returns per-example records and totals.
     queue: optional callable returning the next example index (or None when drained)."""
     tok = tok or Tokenizer()
-    attacker = Attacker(args, model, tok, None, tok, use_bpe=1, threshold_pred_score=0)
+    attacker = make_attacker(args, model, tok)
     recorder = Recorder(args.csv_store_path) if args.csv_store_path else None
     if args.rng == "global":
         set_seed(args.seed)
@@ -208,16 +245,17 @@ def run_mhm_attack(model, codes, subs, labels, args: AttackArgs, indices=None, t
     `random.Random(args.seed + index)` — the same per-example seeding `rng="per_example"` gives
     the GA driver — and records stay in index order."""
     tok = tok or Tokenizer()
-    from .attacker import get_identifiers
-
+    task = getattr(args, "task", "devign")
     set_seed(args.seed)
-    code_tokens = [get_identifiers(c, args.lang)[1] for c in codes]
+    lang = "python" if task == "authorship" else args.lang
+    code_tokens = [get_identifiers(c, lang)[1] for c in codes]
     id2token, token2id = build_vocab(code_tokens, 5000)
-    attacker = MHM_Attacker(args, model, None, tok, token2id, id2token)
+    cls = AuthorshipMHM_Attacker if task == "authorship" else MHM_Attacker
+    attacker = cls(args, model, None, tok, token2id, id2token)
     order = list(range(len(codes))) if indices is None else list(indices)
     records, t0 = [], time.time()
     if max_inflight > 1:
-        exs = [_example(tok, codes[i], labels[i], args.block_size) for i in order]
+        exs = [_example(tok, codes[i], labels[i], args.block_size, task) for i in order]
         _, preds = model.get_results(exs, args.eval_batch_size) if exs else ([], [])
         by_index, jobs, job_index = {}, [], []
         for index, p in zip(order, preds):
@@ -235,15 +273,19 @@ def run_mhm_attack(model, codes, subs, labels, args: AttackArgs, indices=None, t
         records = [by_index[i] for i in order]
         order = []
     for index in order:
-        example = _example(tok, codes[index], labels[index], args.block_size)
+        example = _example(tok, codes[index], labels[index], args.block_size, task)
         q0 = model.query
         probs, preds = model.get_results([example], args.eval_batch_size)
         if preds[0] != labels[index]:
             records.append(dict(index=index, is_success=-4, queries=model.query - q0))
             continue
         fn = attacker.mcmc_random if original else attacker.mcmc
-        res = fn(tok, subs[index], _label=labels[index], code=codes[index], _n_candi=n_candi,
-                 _max_iter=max_iter, _prob_threshold=prob_threshold)
+        if task == "authorship":  # mhm.py:199-206: mcmc(tokenizer, code, _label=..., subs=...)
+            res = fn(tok, codes[index], _label=labels[index], _n_candi=n_candi,
+                     _max_iter=max_iter, _prob_threshold=prob_threshold, subs=subs[index])
+        else:
+            res = fn(tok, subs[index], _label=labels[index], code=codes[index], _n_candi=n_candi,
+                     _max_iter=max_iter, _prob_threshold=prob_threshold)
         ok = 1 if res["succ"] else (-1 if res["succ"] is not None else -3)
         records.append(dict(index=index, is_success=ok, queries=model.query - q0))
     correct = sum(r["is_success"] >= -1 for r in records)

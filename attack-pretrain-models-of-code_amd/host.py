@@ -11,6 +11,7 @@ from . import DATA_DIR, HOSTLIB_PATH
 
 LANG = {"c": 0, "java": 1, "python": 2}
 MODE_BATCH, MODE_SINGLE = 0, 1
+MODE_RAW = 16  # flag: featurise the raw mutant text (Authorship-Attribution victim)
 
 _LIB = None
 
@@ -32,6 +33,8 @@ def load_host_library(path=None) -> ctypes.CDLL:
     lib.ah_tokenize.argtypes = [vp, cp, vp, i32]
     lib.ah_decode.argtypes = [vp, vp, i32, vp, i32]
     lib.ah_featurize_batch.argtypes = [vp, i32, pp, i32, vp, vp]
+    lib.ah_featurize_batch_raw.argtypes = [vp, i32, pp, i32, vp, vp]
+    lib.ah_tokens_to_ids.argtypes = [vp, i32, pp, vp]
     lib.ah_example_new.restype = vp
     lib.ah_example_new.argtypes = [cp, i32]
     lib.ah_example_free.argtypes = [vp]
@@ -47,6 +50,7 @@ def load_host_library(path=None) -> ctypes.CDLL:
     lib.ah_last_error.restype = ctypes.c_char_p
     for f in ("ah_example_identifiers", "ah_example_dfg", "ah_remove_comments",
               "ah_tokenizer_special", "ah_tokenize", "ah_decode", "ah_featurize_batch",
+              "ah_featurize_batch_raw", "ah_tokens_to_ids",
               "ah_example_num_leaves", "ah_example_leaves", "ah_example_mutant_text",
               "ah_example_mutants", "ah_example_mutant_words", "ah_example_word_table"):
         getattr(lib, f).restype = i32
@@ -117,14 +121,25 @@ class Tokenizer:
         self.lib.ah_decode(self.h, _i32p(a), a.size, buf, need)
         return buf.value.decode("utf-8")
 
-    def featurize(self, codes: list[str], L: int):
-        """convert_code_to_features of each text -> (ids int32 [n, L], lens int32 [n])."""
+    def featurize(self, codes: list[str], L: int, raw: bool = False):
+        """convert_code_to_features of each text -> (ids int32 [n, L], lens int32 [n]).
+        raw: tokenize the text as is (Authorship-Attribution) instead of ' '.join(code.split())."""
         n = len(codes)
         ids = np.empty((n, L), dtype=np.int32)
         lens = np.empty((n,), dtype=np.int32)
-        if n and self.lib.ah_featurize_batch(self.h, n, _cstrs(codes), L, _i32p(ids), _i32p(lens)) < 0:
+        fn = self.lib.ah_featurize_batch_raw if raw else self.lib.ah_featurize_batch
+        if n and fn(self.h, n, _cstrs(codes), L, _i32p(ids), _i32p(lens)) < 0:
             _err("ah_featurize_batch")
         return ids, lens
+
+    def convert_tokens_to_ids(self, tokens):
+        """tokenizer.convert_tokens_to_ids (a token string not in the vocabulary -> unk id)."""
+        one = isinstance(tokens, str)
+        toks = [tokens] if one else list(tokens)
+        out = np.empty((max(len(toks), 1),), dtype=np.int32)
+        if toks and self.lib.ah_tokens_to_ids(self.h, len(toks), _cstrs(toks), _i32p(out)) < 0:
+            _err("ah_tokens_to_ids")
+        return int(out[0]) if one else out[:len(toks)].tolist()
 
 
 class Example:

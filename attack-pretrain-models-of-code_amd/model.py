@@ -82,6 +82,8 @@ class Model:
         self.args = args
         self.query = 0
         self.block_size = getattr(args, "block_size", None)
+        # the Authorship-Attribution victim tokenizes raw source (no ' '.join(code.split()))
+        self.raw = task == "authorship"
 
     # the reference calls model.eval()/.to(device) around get_results; keep them as no-ops
     def eval(self):
@@ -118,29 +120,56 @@ class Model:
         dev = torch.from_numpy(ids).to(f"cuda:{self.engine.device}")
         return Payload(dev, lens, n)
 
-    def prepare_population(self, example, tokenizer, population, mode: int, block_size: int):
-        """A population of chromosomes of one program (len(population) queries).
+    def population_rows(self, example, tokenizer, population, mode: int, block_size: int):
+        """Device ids [n, block] + host lens of a population of chromosomes of one program.
 
         The host library reduces every mutant to its word-id sequence (the mutant text is built
         exactly as get_example / get_example_batch would); ae_splice assembles the [n, block]
         ids on the GPU from the example's word table.  Identical ids to featurising the mutant
-        texts (tests/test_host.py, tests/test_engine_gpu.py)."""
+        texts (tests/test_host.py, tests/test_engine_gpu.py).  A raw-text victim (authorship)
+        tokenizes whole mutant texts on the host instead: without the whitespace normalisation
+        the token runs are not word-local."""
         import torch
 
         from .engine import splice
+        from .host import MODE_RAW
 
         n = len(population)
         dev = f"cuda:{self.engine.device}"
         if n == 0:
-            return Payload(torch.zeros((0, block_size), dtype=torch.int32, device=dev),
-                           np.zeros((0,), np.int32), 0)
+            return (torch.zeros((0, block_size), dtype=torch.int32, device=dev),
+                    np.zeros((0,), np.int32))
+        if self.raw:
+            ids, lens = example.mutant_ids(tokenizer, population, block_size, mode | MODE_RAW)
+            return torch.from_numpy(ids).to(dev), lens
         word_tok, word_off, mut_words, mut_off, lens = example.mutant_words(
             tokenizer, population, block_size, mode)
         ids, _ = splice(torch.from_numpy(word_tok).to(dev), torch.from_numpy(word_off).to(dev),
                         torch.from_numpy(mut_words).to(dev), torch.from_numpy(mut_off).to(dev),
                         n, block_size, tokenizer.cls_token_id, tokenizer.sep_token_id,
                         tokenizer.pad_token_id)
-        return Payload(ids, lens, n)
+        return ids, lens
+
+    def prepare_population(self, example, tokenizer, population, mode: int, block_size: int):
+        """A population of chromosomes of one program (len(population) queries)."""
+        ids, lens = self.population_rows(example, tokenizer, population, mode, block_size)
+        return Payload(ids, lens, len(population))
+
+    def prepare_pairs(self, ids1, lens1, ids2_row, len2) -> "Payload":
+        """Clone queries (Clone-detection-BigCloneBench/code/model.py:44): row i of ids1 paired
+        with the one fixed code2 row, interleaved code1, code2 per pair as the [2n, block] view
+        of the reference's [n, 2*block] ids."""
+        import torch
+
+        dev = f"cuda:{self.engine.device}"
+        a = ids1 if torch.is_tensor(ids1) else torch.from_numpy(np.ascontiguousarray(ids1))
+        a = a.to(dev, dtype=torch.int32)
+        n, L = a.shape
+        b = torch.from_numpy(np.ascontiguousarray(ids2_row, dtype=np.int32)).to(dev)
+        rows = torch.stack([a, b.expand(n, L)], 1).reshape(2 * n, L).contiguous()
+        lens = np.empty((2 * n,), np.int32)
+        lens[0::2], lens[1::2] = np.asarray(lens1, np.int32), int(len2)
+        return Payload(rows, lens, n)
 
     def score_prepared(self, payloads, threshold: float = 0.5):
         """Score payloads as one device batch; query += their total queries.  Returns one
@@ -185,7 +214,7 @@ class Model:
         text, CodeXGLUE/Defect-detection/code/attacker.py:38-45, batched in the host library)."""
         from .utils import IdsDataset
 
-        ids, lens = tokenizer.featurize(list(texts), args.block_size)
+        ids, lens = tokenizer.featurize(list(texts), args.block_size, raw=self.raw)
         return IdsDataset(ids, lens)
 
     def get_results_population(self, example, tokenizer, population, mode: int, block_size: int,
@@ -240,9 +269,21 @@ class HostIdsVictim:
             ids = ids.reshape(-1, self.block_size or ids.shape[1] // 2)
         return Payload(np.ascontiguousarray(ids, dtype=np.int32), None, n)
 
+    def population_rows(self, example, tokenizer, population, mode: int, block_size: int):
+        from .host import MODE_RAW
+
+        return example.mutant_ids(tokenizer, population, block_size,
+                                  mode | (MODE_RAW if self.task == "authorship" else 0))
+
     def prepare_population(self, example, tokenizer, population, mode: int, block_size: int):
-        ids, lens = example.mutant_ids(tokenizer, population, block_size, mode)
+        ids, lens = self.population_rows(example, tokenizer, population, mode, block_size)
         return Payload(ids, lens, len(population))
+
+    def prepare_pairs(self, ids1, lens1, ids2_row, len2) -> Payload:
+        ids1 = np.asarray(ids1, np.int32)
+        n, L = ids1.shape
+        rows = np.stack([ids1, np.broadcast_to(np.asarray(ids2_row, np.int32), (n, L))], 1)
+        return Payload(np.ascontiguousarray(rows.reshape(2 * n, L)), None, n)
 
     def score_prepared(self, payloads, threshold: float = 0.5):
         self.query += sum(p.n for p in payloads)
@@ -265,7 +306,8 @@ class HostIdsVictim:
     def dataset_from_texts(self, texts, tokenizer, args, label=0):
         from .utils import IdsDataset
 
-        ids, lens = tokenizer.featurize(list(texts), args.block_size)
+        ids, lens = tokenizer.featurize(list(texts), args.block_size,
+                                        raw=self.task == "authorship")
         return IdsDataset(ids, lens)
 
     def get_results_population(self, example, tokenizer, population, mode: int, block_size: int,

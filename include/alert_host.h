@@ -9,6 +9,8 @@
  *   ah_featurize(_batch)      <- convert_code_to_features
  *                                (CodeXGLUE/Defect-detection/code/attacker.py:38-45,
  *                                 run.py:79-86 convert_examples_to_features)
+ *   ah_featurize_batch_raw    <- the Authorship-Attribution convert_code_to_features (raw text)
+ *   ah_tokens_to_ids          <- tokenizer.convert_tokens_to_ids
  *   ah_example_leaves         <- get_identifiers(code, lang)[1] code tokens
  *                                (python_parser/run_parser.py:185-216,272-281)
  *   ah_example_mutant_text    <- get_example / get_example_batch (run_parser.py:218-266)
@@ -35,6 +37,8 @@ extern "C" {
 
 #define AH_MODE_BATCH 0  /* get_example_batch(code, chromosome) */
 #define AH_MODE_SINGLE 1 /* get_example(code, tgt, sub): exactly one pair per mutant */
+#define AH_MODE_RAW 16   /* ah_example_mutants flag: featurise the raw mutant text (no
+                            ' '.join(code.split()); Authorship-Attribution victim) */
 
 typedef struct ah_tokenizer ah_tokenizer;
 typedef struct ah_example ah_example;
@@ -49,6 +53,15 @@ int32_t ah_decode(ah_tokenizer *tok, const int32_t *ids, int32_t n, char *out, i
 /* convert_code_to_features of n texts: ids_out [n, L], lens_out [n] (non-pad length) */
 int32_t ah_featurize_batch(ah_tokenizer *tok, int32_t n, const char *const *codes, int32_t L,
                            int32_t *ids_out, int32_t *lens_out);
+
+/* convert_code_to_features of the RAW texts (tokenize(code) without whitespace normalisation,
+ * CodeXGLUE/Authorship-Attribution/code/attacker.py:31-37, run.py:81-89) */
+int32_t ah_featurize_batch_raw(ah_tokenizer *tok, int32_t n, const char *const *codes, int32_t L,
+                               int32_t *ids_out, int32_t *lens_out);
+/* tokenizer.convert_tokens_to_ids of n token strings (unk id when absent) — the clone attacker's
+ * importance features feed whole words through it
+ * (CodeXGLUE/Clone-detection-BigCloneBench/code/attacker.py:48-71 with run.py:102-119) */
+int32_t ah_tokens_to_ids(ah_tokenizer *tok, int32_t n, const char *const *tokens, int32_t *ids_out);
 
 ah_example *ah_example_new(const char *code, int32_t lang);
 void ah_example_free(ah_example *ex);

@@ -18,21 +18,23 @@ FIXTURE = ROOT / "data" / "devign" / "test_subs_0_400.jsonl"
 BLOCK = 128
 
 
-class IdsVictim:
-    """Devign-format victim: p = sigmoid(<ids, w> / 4); records every batch size it served."""
+def IdsVictim():
+    """Devign-format victim: p = sigmoid(<ids, w> / 4) behind the product request API
+    (HostIdsVictim); records every batch size it served in `.batches`."""
+    import _apmc  # noqa: F401
+    from apmc_amd.model import HostIdsVictim
 
-    def __init__(self):
-        self.w = np.random.default_rng(1).standard_normal(50265)
-        self.query = 0
-        self.batches = []
+    w = np.random.default_rng(1).standard_normal(50265)
+    batches = []
 
-    def get_results(self, dataset, batch_size=None):
-        self.query += len(dataset)
-        ids = dataset.ids if hasattr(dataset, "ids") else np.stack([np.asarray(d[0]) for d in dataset])
-        self.batches.append(ids.shape[0])
-        z = np.where(ids != 1, self.w[ids], 0.0).sum(1) / 4.0
-        p = (1.0 / (1.0 + np.exp(-z))).astype(np.float32)
-        return [[1 - x, x] for x in p], [1 if x > 0.5 else 0 for x in p]
+    def score(ids):
+        batches.append(ids.shape[0])
+        z = np.where(ids != 1, w[ids], 0.0).sum(1) / 4.0
+        return (1.0 / (1.0 + np.exp(-z))).astype(np.float32)[:, None]
+
+    v = HostIdsVictim(score)
+    v.batches = batches
+    return v
 
 
 @pytest.fixture(scope="module")
@@ -103,3 +105,46 @@ def test_driver_batched_mode_counts(setup):
     assert [r["index"] for r in out["records"]] == list(range(len(codes)))
     assert out["queries"] == victim.query - q0
     assert sum(r["is_success"] == -4 for r in out["records"]) == len(codes[::5])
+
+
+def test_authorship_driver_batched_equals_sequential():
+    """Authorship-Attribution MHM-NS (mhm.py:160-233): Python identifiers, raw-text features,
+    the 66-way argmax victim; the batched driver's records equal the reference loop run with the
+    same per-example seeds (random.seed(seed + index) before each chain)."""
+    import _apmc  # noqa: F401
+    from apmc_amd.drivers import AttackArgs, _example, load_fixture, run_mhm_attack
+    from apmc_amd.host import Tokenizer
+    from apmc_amd.model import HostIdsVictim
+
+    codes, subs, _ = load_fixture(ROOT / "data" / "authorship" / "valid_subs.jsonl", 0, 12,
+                                  labels_path=ROOT / "data" / "authorship" / "valid.txt")
+    w = np.random.default_rng(5).standard_normal((50265, 66))
+
+    def score(ids):
+        z = (w[ids] * (ids != 1)[..., None]).sum(1) / 3.0
+        z = np.exp(z - z.max(1, keepdims=True))
+        return (z / z.sum(1, keepdims=True)).astype(np.float32)
+
+    tok = Tokenizer()
+    probe = HostIdsVictim(score, task="authorship")
+    labels = [int(probe.get_results([_example(tok, c, 0, BLOCK, "authorship")])[1][0])
+              for c in codes]
+    args = AttackArgs(block_size=BLOCK, eval_batch_size=32, task="authorship", lang="python")
+    v_bat = HostIdsVictim(score, task="authorship")
+    bat = run_mhm_attack(v_bat, codes, subs, labels, args, tok=tok, max_iter=10, max_inflight=8)
+    # the sequential reference loop, re-seeded per example the way the batched chains are
+    import apmc_amd.drivers as D
+
+    v_seq = HostIdsVictim(score, task="authorship")
+    seq = []
+    for i in range(len(codes)):
+        orig_seed = args.seed
+        args_i = AttackArgs(block_size=BLOCK, eval_batch_size=32, task="authorship",
+                            lang="python", seed=orig_seed + i)
+        q0 = v_seq.query
+        out = D.run_mhm_attack(v_seq, codes, subs, labels, args_i, indices=[i], tok=tok,
+                               max_iter=10)
+        seq.append(dict(out["records"][0], index=i))
+        assert out["queries"] == v_seq.query - q0
+    assert [dict(r) for r in bat["records"]] == seq
+    assert {r["is_success"] for r in seq} & {1, -1}
