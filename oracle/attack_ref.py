@@ -8,6 +8,17 @@ featurised with the transformers tokenizer, and scored by a caller-supplied `sco
 callback (the victim's sigmoid probabilities).  The product Attacker (apmc_amd/attacker.py) must
 reproduce its outcomes, adversarial code, replaced names and query counts exactly under the same
 Python `random` seed.
+
+The same loops serve the other CodeBERT victims through `Victim(task=...)`:
+  * clone (CodeXGLUE/Clone-detection-BigCloneBench/code/attacker.py, run.py:94-119): a query is
+    the pair [features(code1 mutant) | features(code2)], each half block_size ids of the
+    whitespace-normalised text; the importance rows are built from WORDS (each word one
+    convert_tokens_to_ids lookup, code2's words from its identifier leaves, :40-71); Java leaves;
+    64 GA children per iteration (:226) and no empty-gene-pool exit;
+  * authorship (CodeXGLUE/Authorship-Attribution/code/run.py:81-88): the raw text is tokenised
+    (no whitespace normalisation), 66-way argmax predictions, Python leaves (comments and
+    docstrings removed first, python_parser/parser_folder/utils.py:30-70), no empty-gene-pool
+    exit (attacker.py:147-150).
 """
 from __future__ import annotations
 
@@ -20,23 +31,63 @@ from . import featurize_ref as fr
 
 
 class Victim:
-    """Counts queries like Model.get_results (model.py:38) and returns Devign probs/preds."""
+    """Counts queries like Model.get_results (model.py:38) and returns the task's probs/preds.
 
-    def __init__(self, score, block_size=512):
+    score(ids int32 [rows, L]) -> devign: p [n]; clone: [n, 2] softmax over the [2n, L] pair
+    rows; authorship: [n, 66] softmax."""
+
+    def __init__(self, score, block_size=512, task="devign", code2=None):
         self.score = score
         self.block = block_size
+        self.task = task
         self.query = 0
+        self.lang = {"devign": "c", "clone": "java", "authorship": "python"}[task]
+        self.ga_children = 64 if task == "clone" else None
+        self.empty_pool_exit = task == "devign"
+        if task == "clone":
+            tok = fr.tokenizer()
+            self._half2 = self._row(tok.tokenize(" ".join(code2.split())))
+            words2 = " ".join(fr.identifier_code_tokens(code2, "java")).replace("\n", "")
+            self._words2 = self._row(words2.split(" "))
+
+    def _row(self, tokens):
+        tok = fr.tokenizer()
+        t = [tok.cls_token] + list(tokens[:self.block - 2]) + [tok.sep_token]
+        ids = tok.convert_tokens_to_ids(t)
+        return ids + [tok.pad_token_id] * (self.block - len(ids))
 
     def texts(self, codes):
-        ids = np.array([fr.convert_code_to_features(c, self.block) for c in codes], dtype=np.int32)
-        return self.ids(ids)
+        tok = fr.tokenizer()
+        if self.task == "authorship":
+            rows = [self._row(tok.tokenize(c)) for c in codes]
+        elif self.task == "clone":
+            rows = [self._row(tok.tokenize(" ".join(c.split()))) + self._half2 for c in codes]
+        else:
+            rows = [fr.convert_code_to_features(c, self.block) for c in codes]
+        return self.ids(np.array(rows, dtype=np.int32))
+
+    def importance(self, word_lists):
+        """get_importance_score's rows: the joined words (devign / authorship), or for clone the
+        words themselves as tokens next to code2's word row."""
+        if self.task != "clone":
+            return self.texts([" ".join(t) for t in word_lists])
+        rows = [self._row(w) + self._words2 for w in word_lists]
+        return self.ids(np.array(rows, dtype=np.int32))
 
     def ids(self, ids):
-        self.query += len(ids)
-        p = np.asarray(self.score(ids), dtype=np.float32).reshape(-1)
-        probs = [[1 - x, x] for x in p]
-        preds = [1 if x > 0.5 else 0 for x in p]
-        return probs, preds
+        ids = np.asarray(ids, dtype=np.int32)
+        if self.task == "clone":
+            ids = ids.reshape(-1, self.block)
+            self.query += len(ids) // 2
+        else:
+            self.query += len(ids)
+        out = np.asarray(self.score(ids), dtype=np.float32)
+        if self.task == "devign":
+            p = out.reshape(-1)
+            return [[1 - x, x] for x in p], [1 if x > 0.5 else 0 for x in p]
+        if self.task == "clone":  # Clone-detection-BigCloneBench/code/model.py:81-82
+            return list(out), [0 if x > 0.5 else 1 for x in out[:, 0]]
+        return list(out), [int(np.argmax(x)) for x in out]  # Authorship model.py:84-89
 
 
 def _positions(words, names):
@@ -48,17 +99,18 @@ def _positions(words, names):
     return out
 
 
-def _words_of(code):
-    toks = fr.identifier_code_tokens(code, "c")
+def _words_of(code, lang="c"):
+    toks = fr.identifier_code_tokens(code, lang)
     processed = " ".join(toks)
     return len(toks), processed.replace("\n", "").split(" ")
 
 
 def greedy(victim, ids0, true_label, code, subs):
+    lang = getattr(victim, "lang", "c")
     probs, preds = victim.ids(ids0[None, :])
     orig_prob, orig_label = probs[0], preds[0]
     current = max(orig_prob)
-    prog_length, words = _words_of(code)
+    prog_length, words = _words_of(code, lang)
     names = list(subs.keys())
     if orig_label != true_label:
         return dict(is_success=-4, prog_length=prog_length)
@@ -72,7 +124,7 @@ def greedy(victim, ids0, true_label, code, subs):
         for p in pos[n]:
             masked.append(words[:p] + ["<unk>"] + words[p + 1:])
             where.append(p)
-    lg, pr = victim.texts([" ".join(t) for t in [words] + masked])
+    lg, pr = victim.importance([words] + masked)
     base = max(lg[0])
     imp = [base - x[pr[0]] for x in lg[1:]]
     at = {p: i for i, p in enumerate(where)}
@@ -83,14 +135,14 @@ def greedy(victim, ids0, true_label, code, subs):
         cands = list(subs[name])
         if not cands:
             continue
-        lg, pr = victim.texts([fr.get_example(final_code, name, s, "c") for s in cands])
+        lg, pr = victim.texts([fr.get_example(final_code, name, s, lang) for s in cands])
         best_gap, best = 0.0, None
         for i, pv in enumerate(lg):
             temp_label = pr[i]
             if temp_label != orig_label:
                 replaced[name] = cands[i]
                 return dict(is_success=1, prog_length=prog_length, temp_label=temp_label,
-                            adv_code=fr.get_example(final_code, name, cands[i], "c"),
+                            adv_code=fr.get_example(final_code, name, cands[i], lang),
                             nb_changed_var=n_var + 1, nb_changed_pos=n_pos + len(pos[name]),
                             replaced=replaced, scores=score)
             gap = current - pv[temp_label]
@@ -101,7 +153,7 @@ def greedy(victim, ids0, true_label, code, subs):
             n_pos += len(pos[name])
             current -= best_gap
             replaced[name] = best
-            final_code = fr.get_example(final_code, name, best, "c")
+            final_code = fr.get_example(final_code, name, best, lang)
         else:
             replaced[name] = name
     return dict(is_success=-1, prog_length=prog_length, temp_label=temp_label, adv_code=final_code,
@@ -109,10 +161,13 @@ def greedy(victim, ids0, true_label, code, subs):
 
 
 def ga(victim, ids0, true_label, code, subs, initial_replace=None, eval_batch_size=64):
+    lang = getattr(victim, "lang", "c")
+    if getattr(victim, "ga_children", None):
+        eval_batch_size = victim.ga_children
     probs, preds = victim.ids(ids0[None, :])
     orig_prob, orig_label = probs[0], preds[0]
     top = max(orig_prob)
-    prog_length, words = _words_of(code)
+    prog_length, words = _words_of(code, lang)
     names = list(subs.keys())
     if orig_label != true_label:
         return dict(is_success=-4, prog_length=prog_length)
@@ -120,7 +175,7 @@ def ga(victim, ids0, true_label, code, subs, initial_replace=None, eval_batch_si
         return dict(is_success=-3, prog_length=prog_length)
     pos = _positions(words, names)
     gene_pool = {n: subs[n] for n in pos}
-    if not gene_pool:
+    if not gene_pool and getattr(victim, "empty_pool_exit", True):
         return dict(is_success=-3, prog_length=prog_length)
     base = {n: n for n in gene_pool}
     population, fitness, temp_label = [base], [], None
@@ -129,7 +184,7 @@ def ga(victim, ids0, true_label, code, subs, initial_replace=None, eval_batch_si
             cands = list(gene_pool[name])
             if not cands:
                 continue
-            lg, pr = victim.texts([fr.get_example(code, name, s, "c") for s in cands])
+            lg, pr = victim.texts([fr.get_example(code, name, s, lang) for s in cands])
             best_gap, best = 0.0, -1
             for i, pv in enumerate(lg):
                 temp_label = pr[i]
@@ -142,7 +197,7 @@ def ga(victim, ids0, true_label, code, subs, initial_replace=None, eval_batch_si
         chrom = dict(base)
         chrom[name] = init
         population.append(chrom)
-        lg, pr = victim.texts([fr.get_example_batch(code, chrom, "c")])
+        lg, pr = victim.texts([fr.get_example_batch(code, chrom, lang)])
         fitness.append(top - lg[0][orig_label])
         temp_label = pr[0]
 
@@ -181,14 +236,14 @@ def ga(victim, ids0, true_label, code, subs, initial_replace=None, eval_batch_si
             kids.append(child)
         if not kids:
             continue
-        lg, pr = victim.texts([fr.get_example_batch(code, k, "c") for k in kids])
+        lg, pr = victim.texts([fr.get_example_batch(code, k, lang) for k in kids])
         fits = []
         for i, pv in enumerate(lg):
             if pr[i] != orig_label:
                 kid = kids[i]
                 same = [k for k in kid if kid[k] == k]
                 return dict(is_success=1, prog_length=prog_length, temp_label=pr[i],
-                            adv_code=fr.get_example_batch(code, kid, "c"),
+                            adv_code=fr.get_example_batch(code, kid, lang),
                             nb_changed_var=len(same), nb_changed_pos=sum(len(pos[k]) for k in same),
                             replaced=dict(kid))
             fits.append(top - pv[orig_label])

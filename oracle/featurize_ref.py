@@ -435,12 +435,42 @@ def remove_comments_and_docstrings(source, lang="c"):
     return "\n".join(temp)
 
 
+def remove_python_comments_and_docstrings(source):
+    """python_parser/parser_folder/utils.py:30-70, restated: re-emit the stdlib tokenize stream
+    with the original column spacing, dropping comments and every STRING token that starts a
+    logical line (after INDENT or NEWLINE, or at column 0); then drop blank lines."""
+    import io
+    import tokenize
+
+    pieces, prev, row, col = [], tokenize.INDENT, -1, 0
+    for tt, text, (srow, scol), (erow, ecol), _ in tokenize.generate_tokens(
+            io.StringIO(source).readline):
+        if srow > row:
+            col = 0
+        if scol > col:
+            pieces.append(" " * (scol - col))
+        if tt == tokenize.COMMENT:
+            pass
+        elif tt == tokenize.STRING:
+            if prev not in (tokenize.INDENT, tokenize.NEWLINE) and scol > 0:
+                pieces.append(text)
+        else:
+            pieces.append(text)
+        prev, row, col = tt, erow, ecol
+    return "\n".join(l for l in "".join(pieces).split("\n") if l.strip() != "")
+
+
 def identifier_code_tokens(code: str, lang: str = "c"):
     """get_identifiers(code, lang)[1] (run_parser.py:190-216,272-281): '\\n' -> newline, comments
-    removed, then the leaves."""
+    (and for Python docstrings; left as is when that raises) removed, then the leaves."""
     code = code.replace("\\n", "\n")
     if lang != "python":
         code = remove_comments_and_docstrings(code, lang)
+    else:
+        try:
+            code = remove_python_comments_and_docstrings(code)
+        except Exception:
+            pass
     return code_tokens(code, lang)
 
 

@@ -285,3 +285,33 @@ def test_mhm_batched_equals_sequential_on_engine(victim):
         if rs["succ"] is not None:
             assert rs["tokens"] == rb["tokens"], j
             assert rs["replace_info"] == rb["replace_info"], j
+
+
+@pytest.mark.parametrize("task", ["clone", "authorship"])
+def test_task_attack_matches_text_oracle(task):
+    """CodeBERT clone-pair victim (pair2 head over [code1 | code2] rows, CloneAttacker) and the
+    66-way authorship victim (raw-text features, AuthorshipAttacker) on the HIP engine, against
+    the text oracle scoring the same mutant texts with the same engine: identical outcomes,
+    query counts, adversarial code and replacements (block 512, batch 64 as the reference
+    scripts run).  Labels are the victim's own predictions so every example is attacked."""
+    from apmc_amd.drivers import _example
+    from apmc_amd.host import Tokenizer
+    from apmc_amd.model import Model
+    from test_task_attacks import compare_task, fixture
+
+    head, nl = ("pair2", 2) if task == "clone" else ("softmaxN", 66)
+    model = Model(synthetic_sd(seed=5, head=head, num_labels=nl, out_std=8.0), task=task)
+
+    def score(ids):
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        lens = (ids != 1).sum(1).astype(np.int32)
+        return model.engine.score(torch.from_numpy(ids).cuda(), lens).cpu().numpy()
+
+    codes, subs, _ = fixture(task, 6)
+    tok = Tokenizer()
+    labels = [int(p) for p in model.get_results([_example(tok, c, 0, CONFIG2_BLOCK, task)
+                                                 for c in codes])[1]]
+    seen = compare_task(task, model, score, codes, subs, labels, CONFIG2_BLOCK, CONFIG2_BATCH,
+                        6000, range(len(codes)))
+    print(task, seen)
+    assert {o for _, o in seen} & {1, -1}, seen
