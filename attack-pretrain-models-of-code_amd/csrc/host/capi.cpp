@@ -281,8 +281,7 @@ int32_t ah_example_identifiers(ah_example* e, char* buf, int32_t cap) {
 int32_t ah_example_dfg(ah_example* e, int32_t* rows, int32_t cap_rows, int32_t* from_idx,
                        int32_t cap_from) {
   if (!e) return fail("null example");
-  if (e->ex.lang != ah::LANG_C) return fail("data-flow graph: only C is built");
-  const std::vector<ah::DfgEdge> d = ah::dfg_c(e->ex.id_leaves);
+  const std::vector<ah::DfgEdge> d = ah::dfg_of(e->ex.id_leaves, e->ex.lang);
   int32_t nf = 0;
   for (auto& x : d) nf += (int32_t)x.from_idx.size();
   if (rows && cap_rows >= (int32_t)d.size() && from_idx && cap_from >= nf) {

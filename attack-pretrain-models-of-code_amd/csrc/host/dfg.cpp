@@ -154,13 +154,13 @@ class CTree {
     match_.assign(n_, -1);
     std::vector<int> st;
     for (size_t i = 0; i < n_; ++i) {
-      const std::string& t = lv[i].text;
+      const std::string& t = lv[i].raw;
       if (t == "(" || t == "[" || t == "{") st.push_back((int)i);
       else if (t == ")" || t == "]" || t == "}") {
         const char open = t == ")" ? '(' : t == "]" ? '[' : '{';
         // pop to the nearest matching opener (tolerates unbalanced macro text)
         for (int k = (int)st.size() - 1; k >= 0; --k)
-          if (lv[st[k]].text[0] == open) {
+          if (lv[st[k]].raw[0] == open) {
             match_[st[k]] = (int)i;
             match_[i] = st[k];
             st.resize(k);
@@ -202,9 +202,9 @@ class CTree {
   void add_leaf(int parent, size_t i) { attach(parent, leaf_node(i)); }
   const std::string& t(size_t i) const {
     static const std::string empty;
-    return i < n_ ? lv_[i].text : empty;
+    return i < n_ ? lv_[i].raw : empty;
   }
-  bool at(const char* s) const { return p_ < n_ && lv_[p_].text == s; }
+  bool at(const char* s) const { return p_ < n_ && lv_[p_].raw == s; }
   // consume the balanced group starting at p_ ('(' / '[' / '{') as generic leaves under parent
   void group(int parent) {
     const size_t e = (size_t)(match_[p_] >= 0 ? match_[p_] : (int)n_ - 1);
@@ -996,7 +996,7 @@ struct Walker {
 
   Walker(const std::vector<Node>& n, const std::vector<Leaf>& l) : nd(n), lv(l) {
     anon.resize(l.size());
-    for (size_t i = 0; i < l.size(); ++i) anon[i] = leaf_anon(l[i].text);
+    for (size_t i = 0; i < l.size(); ++i) anon[i] = leaf_anon(l[i].raw) && l[i].text == l[i].raw;
   }
 
   // tree_to_variable_index: non-anonymous leaves of a subtree (utils.py:98-113)
@@ -1052,7 +1052,7 @@ struct Walker {
         dfg.push_back({code, idx, false, {code}, it->second});
         return dfg;
       }
-      if (is_ident(code) && !n.tid && !primitive_types().count(code) && par >= 0 &&
+      if (is_ident(lv[idx].raw) && !n.tid && !primitive_types().count(code) && par >= 0 &&
           nd[par].type == N_DECLARATION) {
         states[code] = {idx};
         dfg.push_back({code, idx, false, {}, {}});
@@ -1098,7 +1098,7 @@ struct Walker {
         std::vector<States> others;
         bool flag = false, tag = false;
         for (int k : n.kids) {
-          const bool is_else = nd[k].type == N_LEAF && lv[nd[k].leaf].text == "else";
+          const bool is_else = nd[k].type == N_LEAF && lv[nd[k].leaf].raw == "else";
           if (is_else) tag = true;
           const bool in_if_list = is_else || nd[k].type == N_IF;
           if (!in_if_list && !flag) {
@@ -1144,7 +1144,7 @@ struct Walker {
       case N_PARAMETER_DECLARATION: {
         int c = n.decl;
         if (c < 0) return dfg;
-        while (!(nd[c].type == N_LEAF && is_ident(lv[nd[c].leaf].text))) {
+        while (!(nd[c].type == N_LEAF && is_ident(lv[nd[c].leaf].raw))) {
           c = nd[c].decl;  // parenthesized: its inner declarator is children[1] == decl
           if (c < 0) return dfg;
         }
@@ -1179,11 +1179,16 @@ std::vector<DfgEdge> dfg_c(const std::vector<Leaf>& leaves) {
   return d;
 }
 
+std::vector<DfgEdge> dfg_of(const std::vector<Leaf>& leaves, Lang lang) {
+  if (lang == LANG_JAVA) return dfg_java(leaves);
+  if (lang == LANG_PYTHON) return dfg_python(leaves);
+  return dfg_c(leaves);
+}
+
 std::vector<std::string> dfg_names(const std::vector<Leaf>& leaves, Lang lang) {
   std::vector<std::string> out;
-  if (lang != LANG_C) return out;
   std::unordered_set<std::string> seen;
-  for (const DfgEdge& e : dfg_c(leaves))
+  for (const DfgEdge& e : dfg_of(leaves, lang))
     if (seen.insert(e.code).second) out.push_back(e.code);
   return out;
 }

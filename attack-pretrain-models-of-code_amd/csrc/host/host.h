@@ -60,7 +60,10 @@ enum Lang { LANG_C = 0, LANG_JAVA = 1, LANG_PYTHON = 2 };
 
 struct Leaf {
   int sl, sc, el, ec;  // start/end line, byte column (tree-sitter Point semantics)
-  std::string text;    // index_to_code_token(start, end, lines)
+  std::string text;    // index_to_code_token(start, end, lines): the code the reference records
+  std::string raw;     // the token's own bytes (what the parser sees; differs from `text` on
+                       // lines with non-ASCII code points, where the byte-column slice shifts)
+  bool joined = false; // Python: a backslash line continuation precedes this leaf
 };
 
 // Leaves of `code` (already '\\n'-replaced by the caller when the reference does so).
@@ -99,6 +102,12 @@ struct DfgEdge {
 };
 // DFG of C leaves (dfg.cpp), sorted by idx as extract_dataflow returns it (run_parser.py:213)
 std::vector<DfgEdge> dfg_c(const std::vector<Leaf>& leaves);
+// DFG_java over Java leaves (dfg_java.cpp)
+std::vector<DfgEdge> dfg_java(const std::vector<Leaf>& leaves);
+// DFG_python over Python leaves (dfg_python.cpp)
+std::vector<DfgEdge> dfg_python(const std::vector<Leaf>& leaves);
+// the DFG of a language
+std::vector<DfgEdge> dfg_of(const std::vector<Leaf>& leaves, Lang lang);
 // unique DFG names in graph order (get_identifiers before the validity filter, run_parser.py:272)
 std::vector<std::string> dfg_names(const std::vector<Leaf>& leaves, Lang lang);
 

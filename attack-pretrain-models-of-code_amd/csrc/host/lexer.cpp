@@ -94,6 +94,7 @@ class Lexer {
       }
       if (lang_ == LANG_PYTHON && ch == '\\' && (c_.at(1) == '\n' || (c_.at(1) == '\r' && c_.at(2) == '\n'))) {
         c_.adv(c_.at(1) == '\n' ? 2 : 3);
+        joined_ = true;
         continue;
       }
       // comments
@@ -131,7 +132,9 @@ class Lexer {
     // start line tail, the middle lines and the end line head (line breaks dropped).  The
     // reference slices Python str lines with tree-sitter's BYTE columns, so on a line holding
     // non-ASCII code points the text is taken at code-point indices equal to the byte columns.
-    (void)b;
+    lf.raw = c_.s.substr(b, c_.i - b);
+    lf.joined = joined_;
+    joined_ = false;
     if (lf.sl == lf.el) {
       lf.text = utf8_encode(lines_cp_[lf.sl], lf.sc, lf.ec);
     } else {
@@ -324,12 +327,22 @@ class Lexer {
       }
       c_.adv(3);
     } else {
+      // one regex token that cannot hold a raw newline: an unterminated literal is a lexing
+      // error, tree-sitter skips the opening quote alone and lexes what follows as code
       c_.adv();
+      const size_t qi = c_.i, qls = c_.line_start;
+      const int ql = c_.line;
       while (!c_.eof() && c_.at() != q && c_.at() != '\n') {
         if (c_.at() == '\\') c_.adv();
         c_.adv();
       }
-      if (c_.at() == q) c_.adv();
+      if (c_.at() == q) {
+        c_.adv();
+      } else {
+        c_.i = qi;
+        c_.line = ql;
+        c_.line_start = qls;
+      }
     }
     kind_ = K_OPERAND;
     emit(b, sl, sc);
@@ -360,16 +373,70 @@ class Lexer {
       }
       c_.adv(3);
     } else {
+      // tree-sitter-python's external scanner: string content may begin with a raw newline
+      // (then it runs on to the next quote), but a newline after content is an error — the
+      // string is then only its opening quote, and what follows lexes as code
+      bool raw = false;
+      for (size_t k = 0; k < p; ++k) raw |= (c_.s[b + k] == 'r' || c_.s[b + k] == 'R');
       c_.adv();
-      while (!c_.eof() && c_.at() != q && c_.at() != '\n') {
-        if (c_.at() == '\\') c_.adv();
+      const size_t qi = c_.i;
+      const int ql = c_.line;
+      const size_t qls = c_.line_start;
+      bool has_content = false, broken = false;
+      while (!c_.eof()) {
+        const unsigned char d = c_.at();
+        if (d == '\\') {
+          if (raw) {
+            c_.adv();
+            if (c_.at() == q || c_.at() == '\\') c_.adv();
+          } else {
+            c_.adv(py_escape_len());
+            has_content = false;  // the scanner resumes after an escape token
+          }
+          continue;
+        }
+        if (d == q) {
+          c_.adv();
+          break;
+        }
+        if (d == '\n' && has_content) {
+          broken = true;
+          break;
+        }
         c_.adv();
+        has_content = true;
       }
-      if (c_.at() == q) c_.adv();
+      if (broken) {
+        c_.i = qi;
+        c_.line = ql;
+        c_.line_start = qls;
+      }
     }
     kind_ = K_OPERAND;
     emit(b, sl, sc);
     return true;
+  }
+
+  // length of the escape token at a backslash in a non-raw Python string (1: a lone '\\')
+  size_t py_escape_len() const {
+    auto hex = [&](size_t k) {
+      const unsigned char d = c_.at(k);
+      return (d >= '0' && d <= '9') || (d >= 'a' && d <= 'f') || (d >= 'A' && d <= 'F');
+    };
+    const unsigned char d = c_.at(1);
+    auto hexrun = [&](size_t n) {
+      for (size_t k = 0; k < n; ++k)
+        if (!hex(2 + k)) return false;
+      return true;
+    };
+    if (d == 'u') return hexrun(4) ? 6 : 1;
+    if (d == 'U') return hexrun(8) ? 10 : 1;
+    if (d == 'x') return hexrun(2) ? 4 : 1;
+    if (is_digit(d)) return (is_digit(c_.at(2)) && is_digit(c_.at(3))) ? 4 : 1;
+    if (d == '\n') return 2;
+    if (d == '\r') return c_.at(2) == '\n' ? 3 : 1;
+    if (d && std::strchr("'\"abfrntv\\", d)) return 2;
+    return 1;
   }
 
   void preprocessor() {
@@ -485,6 +552,7 @@ class Lexer {
   std::vector<std::vector<uint32_t>> lines_cp_;
   std::vector<Leaf> out_;
   int kind_ = K_OP, last_kind_ = K_OP;
+  bool joined_ = false;
 };
 
 }  // namespace

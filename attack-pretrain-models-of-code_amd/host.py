@@ -172,7 +172,7 @@ class Example:
 
     def dfg_names(self) -> list[str]:
         """Unique data-flow-graph names in graph order (get_identifiers before its validity
-        filter, run_parser.py:272-281).  C only; other languages return []."""
+        filter, run_parser.py:272-281): DFG_c / DFG_java / DFG_python by the example's language."""
         need = self.lib.ah_example_identifiers(self.h, None, 0)
         if need < 0:
             _err("ah_example_identifiers")
@@ -182,7 +182,8 @@ class Example:
 
     def dfg(self):
         """extract_dataflow(code, lang)[0] as (idx, computed, from_idx list) per entry, sorted by
-        leaf index (run_parser.py:190-216, DFG_c.py:10-191).  The entry's code is leaves(True)[idx]."""
+        leaf index (run_parser.py:190-216; DFG_c.py / DFG_java.py / DFG_python.py).  The entry's
+        code is leaves(True)[idx]."""
         n = self.lib.ah_example_dfg(self.h, None, 0, None, 0)
         if n < 0:
             _err("ah_example_dfg")

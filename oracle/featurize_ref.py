@@ -270,13 +270,17 @@ class _Lex:
                 self.adv()
             self.adv(3)
         else:
+            # an unterminated literal (raw newline) is a lexing error: only the quote is skipped
             self.adv()
+            saved = (self.i, self.line, self.line_start)
             while not self.eof() and self.at() != q and self.at() != "\n":
                 if self.at() == "\\":
                     self.adv()
                 self.adv()
             if self.at() == q:
                 self.adv()
+            else:
+                self.i, self.line, self.line_start = saved
         self.kind = 1
         self.emit(b, sl, sc)
 
@@ -299,16 +303,61 @@ class _Lex:
                 self.adv()
             self.adv(3)
         else:
+            # content may begin with a raw newline; a newline after content breaks the string
+            # (it is then only its opening quote)
+            raw = any(ch in "rR" for ch in self.s[b:b + p])
             self.adv()
-            while not self.eof() and self.at() != q and self.at() != "\n":
-                if self.at() == "\\":
+            saved = (self.i, self.line, self.line_start)
+            has_content = broken = False
+            while not self.eof():
+                d = self.at()
+                if d == "\\":
+                    if raw:
+                        self.adv()
+                        if self.at() in (q, "\\"):
+                            self.adv()
+                    else:
+                        self.adv(self._py_escape_len())
+                        has_content = False
+                    continue
+                if d == q:
                     self.adv()
+                    break
+                if d == "\n" and has_content:
+                    broken = True
+                    break
                 self.adv()
-            if self.at() == q:
-                self.adv()
+                has_content = True
+            if broken:
+                self.i, self.line, self.line_start = saved
         self.kind = 1
         self.emit(b, sl, sc)
         return True
+
+    def _py_escape_len(self):
+        """tree-sitter-python escape_sequence length at a backslash (1: a lone backslash)."""
+        hexd = "0123456789abcdefABCDEF"
+        d = self.at(1)
+
+        def run(n):
+            return all(self.at(2 + k) in hexd for k in range(n))
+
+        if d == "u":
+            return 6 if run(4) else 1
+        if d == "U":
+            return 10 if run(8) else 1
+        if d == "x":
+            return 4 if run(2) else 1
+        dig = "0123456789"
+        if d in dig:
+            return 4 if (self.at(2) in dig and self.at(3) in dig) else 1
+        if d == "\n":
+            return 2
+        if d == "\r":
+            return 3 if self.at(2) == "\n" else 1
+        if d in "'\"abfrntv\\":
+            return 2
+        return 1
 
     def preprocessor(self):
         b, sl, sc = self.i, self.line, self.col()

@@ -267,3 +267,118 @@ def test_dfg_identifiers_vs_reference_fixture_keys():
     assert tot == 2732
     assert exact / tot >= 0.89, (exact, tot)
     assert consistent / tot >= 0.98, (consistent, tot, residue[:5])
+
+
+CLONE = ROOT / "data" / "clone" / "test_subs_0_500.jsonl"
+AA = ROOT / "data" / "authorship" / "valid_subs.jsonl"
+
+
+def test_java_python_leaves_match_oracle():
+    """Java (BigCloneBench code1 and code2) and Python (authorship) leaves and identifier-pass
+    leaves of the C++ lexer equal the oracle's, including the broken-literal rules (a Java literal
+    cut by a raw newline is its quote alone; a Python string may start with a raw newline)."""
+    from apmc_amd.host import Example
+    n = 0
+    for js in load(CLONE):
+        for code in (js["code1"], js["code2"]):
+            ex = Example(code, "java")
+            assert ex.leaves() == ref.code_tokens(code.replace("\\n", "\n"), "java")
+            assert ex.leaves(identifiers=True) == ref.identifier_code_tokens(code, "java")
+            n += 1
+    for js in load(AA):
+        code = js["code"].replace("\\n", "\n")
+        assert Example(code, "python").leaves() == ref.code_tokens(code, "python")
+        n += 1
+    assert n == 1132
+
+
+def key_parity(task):
+    """dfg_key_parity for the Java (clone code1, CodeXGLUE/Clone-detection-BigCloneBench/
+    dataset/get_substitutes.py:74-165) and Python (authorship, CodeXGLUE/Authorship-Attribution/
+    dataset/get_substitutes.py:52-140) fixtures: (exact, consistent, subsequence, total).
+    subsequence = the keys are an ordered subsequence of our names (the only difference is names
+    the reference kept no substitute for)."""
+    from apmc_amd.attacker import get_identifiers
+    from apmc_amd.host import Tokenizer, remove_comments
+    from apmc_amd.utils import _tokenize, get_identifier_posistions_from_code, is_valid_variable_name
+    tok = Tokenizer()
+    lang = "java" if task == "clone" else "python"
+    exact = consistent = subseq = tot = 0
+    for js in load(CLONE if task == "clone" else AA):
+        tot += 1
+        keys = list(js["substitutes"].keys())
+        if task == "clone":
+            idents, toks = get_identifiers(remove_comments(js["code1"]), lang)
+        else:
+            idents, toks = get_identifiers(js["code"].replace("\\n", "\n"), lang)
+        words, sub_words, kk = _tokenize(" ".join(toks), tok)
+        names = [i[0] for i in idents if " " not in i[0].strip()]
+        pos = get_identifier_posistions_from_code(words, names)
+        ours = [n for n in pos if is_valid_variable_name(n, lang)]
+        it = iter(ours)
+        subseq += all(k in it for k in keys)
+        if ours == keys:
+            exact += 1
+            consistent += 1
+            continue
+        if keys and len(sub_words) > 380 and all(k in pos for k in keys):
+            last = max(kk[pos[k][0]][0] for k in keys)
+            if [n for n in ours if kk[pos[n][0]][0] <= last] == keys:
+                consistent += 1
+    return exact, consistent, subseq, tot
+
+
+def test_dfg_java_python_vs_reference_fixture_keys():
+    """DFG_java / DFG_python (dfg_java.cpp, dfg_python.cpp) against the reference's own keys.
+    Measured (DESIGN.md §5 lists the residue by cause): Java on all 4000 BigCloneBench fixtures
+    85.3% exact / 96.0% truncation-consistent / 97.8% subsequence; the 500 in data/ and the 132
+    authorship programs are asserted here."""
+    e, c, s, t = key_parity("clone")
+    assert t == 500 and e / t >= 0.84 and c / t >= 0.95 and s / t >= 0.96, (e, c, s, t)
+    e, c, s, t = key_parity("authorship")
+    assert t == 132 and e / t >= 0.53 and c / t >= 0.96 and s / t >= 0.97, (e, c, s, t)
+
+
+def _names(code, lang):
+    from apmc_amd.host import Example
+    return Example(code, lang).dfg_names()
+
+
+def test_dfg_java_known_answers():
+    """DFG_java quirks (python_parser/parser_folder/DFG_java.py) the identifier list depends on."""
+    # the bare method: name and parameters are definitions (recovered declaration)
+    assert _names("void f(int a, String b) { int c = a; }", "java") == ["f", "a", "b", "c"]
+    # a declarator whose value has no named leaf (`false`) defines the name without an entry:
+    # it enters the graph at its first use
+    assert _names("void f() { boolean x = false; int y = 1; g(y, x); }", "java") == \
+        ["f", "y", "x"]
+    # catch parameters and inferred lambda parameters are not definitions
+    assert _names("void f() { try { g(); } catch (Exception e) { e.h(); } }", "java") == ["f"]
+    assert _names("void f() { r(x -> x + 1); r((p, q) -> p); }", "java") == ["f"]
+    assert _names("void f() { r((int p) -> p); }", "java") == ["f", "p"]
+    # a method name called on an object is never walked; unqualified it is (if defined)
+    assert _names("void f() { int g = 1; o.g(); g(); }", "java") == ["f", "g"]
+    # enhanced for / assignment / update definitions
+    assert _names("void f() { for (String s : xs) { t = s; i++; } }", "java") == \
+        ["f", "s", "t", "i"]
+    # throws: later simple names are declarators after <= 1 parameter
+    assert _names("void f(int a) throws A, B { }", "java") == ["f", "a", "B"]
+    assert _names("void f(int a, int b) throws A, B { }", "java") == ["f", "a", "b"]
+
+
+def test_dfg_python_known_answers():
+    """DFG_python quirks (python_parser/parser_folder/DFG_python.py)."""
+    # parameters: plain identifiers define, *args / **kw / typed do not; default_parameter with
+    # a value without named leaves ([]) defines without an entry
+    assert _names("def f(a, b=1, c=[], *d, **e):\n    return a + c", "python") == \
+        ["a", "b", "c"]
+    # tuple assignment pairs children; attribute targets define every named leaf
+    assert _names("x, y = 1, 2\nself.z = x", "python") == ["x", "y", "self", "z"]
+    # comprehension variables are defined before the element is walked
+    assert _names("r = [v * 2 for v in xs]", "python") == ["r", "v"]
+    # for: the body is walked only when it is the last child — with an else clause neither the
+    # body nor the else clause reaches the graph
+    assert _names("for i in a:\n    k = i\nelse:\n    m = 1", "python") == ["i"]
+    assert _names("for i in a:\n    k = i", "python") == ["i", "k"]
+    # lambda parameters are not definitions (default parameters are)
+    assert _names("g = lambda u, w=1: u", "python") == ["g", "w"]
