@@ -448,7 +448,10 @@ class CloneAttacker(Attacker):
         code1 (masked with '<unk>') and of " ".join(get_identifiers(code2)[1]) split like
         _tokenize, so each word becomes ONE id through convert_tokens_to_ids (the unk id unless
         the word is itself a vocabulary token) (:48-71 with run.py:102-119);
-      * 64 GA mutants per iteration whatever eval_batch_size is (:226)."""
+      * 64 GA mutants per iteration whatever eval_batch_size is (:226); no -3 exit for an
+        empty gene pool in ga_attack (:157-166)."""
+
+    ga_empty_check = False
 
     def __init__(self, *a, **k):
         super().__init__(*a, **k)
@@ -474,16 +477,19 @@ class CloneAttacker(Attacker):
         return (code,) + tuple(res[1:])
 
     # ---- pair requests ------------------------------------------------------------------------
-    def _bound(self, code, gen):
-        """Run `gen` with this pair's code2 bound: code2's fixed half of every row and its
-        word-level importance half.  The binding is re-installed before every step, since the
-        batched driver interleaves many pairs' generators over one attacker (requests are built
-        before they are yielded, so each sees its own pair)."""
+    def _pair_state(self, code):
+        """code2's fixed half of every row, and its word-level importance half."""
         L = self.args.block_size
         ids2, lens2 = self.tokenizer_tgt.featurize([code[3]], L)
         _, toks2 = get_identifiers(code[3], self.lang)
         words2 = " ".join(toks2).replace("\n", "").split(" ")
-        bound = (ids2[0], int(lens2[0]), self._word_row(words2))
+        return ids2[0], int(lens2[0]), self._word_row(words2)
+
+    def _bound(self, code, gen):
+        """Run `gen` with this pair's code2 state bound.  The binding is re-installed before
+        every step, since the batched driver interleaves many pairs' generators over one
+        attacker (requests are built before they are yielded, so each sees its own pair)."""
+        bound = self._pair_state(code)
         self._code2 = bound
         try:
             req = next(gen)
@@ -710,7 +716,7 @@ class MHM_Attacker:
         first = m.prepare(m.dataset_from_texts([_tokens], tok, self.args))
         if not pops:
             return first
-        if hasattr(m, "population_rows"):
+        if getattr(m, "population_rows", None) is not None:
             rows = m.population_rows(ex, tok, pops, MODE_SINGLE, L)
             return join_payloads([first, type(first)(rows[0], rows[1], len(pops))])
         texts = [ex.mutant_text(p, MODE_SINGLE) for p in pops]
@@ -777,3 +783,63 @@ class AuthorshipMHM_Attacker(MHM_Attacker):
                     _prob_threshold=0.95, subs={}):
         return super().mcmc_random(tokenizer, subs, code, _label, _n_candi, _max_iter,
                                    _prob_threshold)
+
+
+class GraphAttacker(Attacker):
+    """GraphCodeBERT/Defect-detection/code/attacker.py: the Devign attacker over the GraphModel
+    victim; the GA draws 64 children per iteration whatever eval_batch_size is (:246)."""
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.ga_batch = 64
+
+
+class GraphAuthorshipAttacker(AuthorshipAttacker):
+    """GraphCodeBERT/Authorship-Attribution/code/attacker.py: the authorship attacker over the
+    GraphModel victim (task 'authorship'); every query — original, importance rows, mutants — is
+    featurised with run.py's data flow (DFG_GCB_RUN, attacker.py:18-52), which the victim's
+    dataset_from_texts applies.  GA children per iteration: eval_batch_size (:260)."""
+
+
+class GraphCloneAttacker(CloneAttacker):
+    """GraphCodeBERT/clonedetection/code/attacker.py: pairs of data-flow features (the
+    CodeBERT clone signatures and code tuple).
+      * mutants of code1 and code2 itself are featurised with run_parser's data flow, Java text
+        as is (attacker.py:33-72); the dataset example comes from run.py (pair_features
+        original=True), so the first query of an attack sees different features than its
+        mutants (the reference's quirk);
+      * importance rows: ' '.join(words) of code1 against the features of
+        ' '.join(get_identifiers(code2)[1]) (processed_code_2, :366-378 -> :84-85);
+      * GA children per iteration: eval_batch_size (:261)."""
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.ga_batch = None
+
+    def _pair_state(self, code):
+        from .graph import task_features
+
+        tok, args = self.tokenizer_tgt, self.args
+        _, toks2 = get_identifiers(code[3], self.lang)
+        f2 = task_features(code[3], tok, 0, args, "clone")
+        f2w = task_features(" ".join(toks2), tok, 0, args, "clone")
+        return f2, f2w
+
+    def _population(self, ex, pops, mode):
+        from .graph import task_features
+
+        tok, args = self.tokenizer_tgt, self.args
+        feats = [task_features(ex.mutant_text(p, mode), tok, 0, args, "clone") for p in pops]
+        return self.model_tgt.prepare_pair_population(feats, self._code2[0])
+
+    def _importance_payload(self):
+        from .graph import task_features
+
+        f2w = self._code2[1]
+        tok, args = self.tokenizer_tgt, self.args
+
+        def build(word_lists):
+            feats = [task_features(" ".join(w), tok, 0, args, "clone") for w in word_lists]
+            return self.model_tgt.prepare_pair_population(feats, f2w)
+
+        return build

@@ -280,8 +280,17 @@ int32_t ah_example_identifiers(ah_example* e, char* buf, int32_t cap) {
 
 int32_t ah_example_dfg(ah_example* e, int32_t* rows, int32_t cap_rows, int32_t* from_idx,
                        int32_t cap_from) {
+  return ah_example_dfg_variant(e, AH_DFG_RUN_PARSER, rows, cap_rows, from_idx, cap_from);
+}
+
+int32_t ah_example_dfg_variant(ah_example* e, int32_t variant, int32_t* rows, int32_t cap_rows,
+                               int32_t* from_idx, int32_t cap_from) {
   if (!e) return fail("null example");
-  const std::vector<ah::DfgEdge> d = ah::dfg_of(e->ex.id_leaves, e->ex.lang);
+  if (variant != AH_DFG_RUN_PARSER && variant != AH_DFG_GCB_RUN) return fail("unknown DFG variant");
+  if (variant == AH_DFG_GCB_RUN && e->ex.lang == ah::LANG_C)
+    return fail("the GraphCodeBERT run.py data flow has no C walk (parser/DFG.py)");
+  const std::vector<ah::DfgEdge> d =
+      ah::dfg_of(e->ex.id_leaves, e->ex.lang, (ah::DfgVariant)variant);
   int32_t nf = 0;
   for (auto& x : d) nf += (int32_t)x.from_idx.size();
   if (rows && cap_rows >= (int32_t)d.size() && from_idx && cap_from >= nf) {

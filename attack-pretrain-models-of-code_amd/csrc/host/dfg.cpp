@@ -1179,10 +1179,24 @@ std::vector<DfgEdge> dfg_c(const std::vector<Leaf>& leaves) {
   return d;
 }
 
-std::vector<DfgEdge> dfg_of(const std::vector<Leaf>& leaves, Lang lang) {
-  if (lang == LANG_JAVA) return dfg_java(leaves);
-  if (lang == LANG_PYTHON) return dfg_python(leaves);
-  return dfg_c(leaves);
+std::vector<DfgEdge> dfg_of(const std::vector<Leaf>& leaves, Lang lang, DfgVariant variant) {
+  if (variant == DFG_RUN_PARSER) {
+    if (lang == LANG_JAVA) return dfg_java(leaves);
+    if (lang == LANG_PYTHON) return dfg_python(leaves);
+    return dfg_c(leaves);
+  }
+  std::vector<DfgEdge> d =
+      lang == LANG_JAVA ? dfg_java(leaves, true) : dfg_python(leaves, true);
+  // GraphCodeBERT/*/code/run.py:96-106: keep the entries that have an edge or are an edge's source
+  std::set<int> linked;
+  for (const DfgEdge& e : d) {
+    if (!e.from_idx.empty()) linked.insert(e.idx);
+    linked.insert(e.from_idx.begin(), e.from_idx.end());
+  }
+  std::vector<DfgEdge> out;
+  for (DfgEdge& e : d)
+    if (linked.count(e.idx)) out.push_back(std::move(e));
+  return out;
 }
 
 std::vector<std::string> dfg_names(const std::vector<Leaf>& leaves, Lang lang) {

@@ -51,6 +51,7 @@ struct JNode {
   int parent = -1;
   int a = -1, b = -1, c = -1;
   bool pname = false;  // J_LEAF: the identifier child of a formal_parameter
+  bool tid = false;    // J_LEAF: a type name (type_identifier / scoped type), not an identifier
   std::vector<int> kids;
 };
 
@@ -201,6 +202,10 @@ class JTree {
   void leaves_to(int parent, size_t e) {
     while (more() && p_ < e) add_leaf(parent, p_++);
   }
+  // leaves of a type (modifiers, annotations, type arguments) up to e: names are type names
+  void type_leaves(int parent, size_t e) {
+    while (more() && p_ < e) nodes[add_leaf(parent, p_++)].tid = true;
+  }
   void group_leaves(int parent) {  // a balanced group at p_ as plain leaves
     const size_t e = close_of(p_);
     while (more() && p_ <= e) add_leaf(parent, p_++);
@@ -312,7 +317,7 @@ class JTree {
     if (typed) {
       lvd = make(J_LVD);
       attach(root, lvd);
-      leaves_to(lvd, name);
+      type_leaves(lvd, name);
       const int d = make(J_DECLARATOR);
       attach(lvd, d);
       nodes[d].a = add_leaf(d, p_++);
@@ -407,7 +412,7 @@ class JTree {
       return;
     }
     const size_t name = end - 1;
-    leaves_to(f, name);
+    type_leaves(f, name);
     if (spread) {
       const int d = make(J_DECLARATOR);
       attach(f, d);
@@ -425,7 +430,7 @@ class JTree {
     const int g = make(kind);
     attach(parent, g);
     const size_t q = skip_type(skip_modifiers(p_));
-    leaves_to(g, q);
+    type_leaves(g, q);
     while (more()) {
       if (!is_ident(t(p_))) break;
       declarator(g);
@@ -532,7 +537,8 @@ class JTree {
     }
     const int g = make(J_GENERIC);  // method_declaration / constructor_declaration
     attach(parent, g);
-    leaves_to(g, name + 1);
+    type_leaves(g, name);
+    add_leaf(g, p_++);
     formal_parameters(g);
     while (more() && !at("{") && !at(";")) add_leaf(g, p_++);
     if (at("{")) block(g);
@@ -687,7 +693,7 @@ class JTree {
         size_t nm = c;
         while (nm >= p_ + 2 && t(nm - 1) == "]" && t(nm - 2) == "[") nm -= 2;
         if (nm > p_ && is_ident(t(nm - 1))) {
-          leaves_to(g, nm - 1);
+          type_leaves(g, nm - 1);
           nodes[g].a = add_leaf(g, p_++);
         }
         leaves_to(g, c);
@@ -749,6 +755,7 @@ class JTree {
           attach(r, res);
           const size_t q = skip_type(skip_modifiers(p_));
           if (q && is_ident(t(q)) && t(q + 1) == "=") {
+            type_leaves(res, q);
             leaves_to(res, q + 2);
             attach(res, expr());
           } else {
@@ -768,7 +775,12 @@ class JTree {
       if (at("(")) {
         const int fp = make(J_GENERIC);  // catch_formal_parameter: not a definition
         attach(c, fp);
-        group_leaves(fp);
+        const size_t close = close_of(p_);
+        size_t nm = close;  // the name: the last identifier before ')'
+        while (nm > p_ && !is_ident(t(nm - 1))) --nm;
+        add_leaf(fp, p_++);
+        type_leaves(fp, nm > p_ ? nm - 1 : p_);
+        leaves_to(fp, close + 1);
       }
       if (at("{")) block(c);
     }
@@ -889,7 +901,7 @@ class JTree {
       if (op == "instanceof") {
         if (at("final")) add_leaf(g, p_++);
         const size_t q = skip_type(p_);
-        if (q) leaves_to(g, q);
+        if (q) type_leaves(g, q);
         if (is_ident(t(p_)) && binary_prec(t(p_ + 1)) < 0 && !is_assign_op(t(p_ + 1)) &&
             t(p_ + 1) != "(" && t(p_ + 1) != ".")
           add_leaf(g, p_++);  // pattern binding
@@ -931,7 +943,10 @@ class JTree {
     }
     if (cast_ahead()) {
       const int g = make(J_GENERIC);
-      group_leaves(g);
+      const size_t close = close_of(p_);
+      add_leaf(g, p_++);
+      type_leaves(g, close);
+      if (p_ == close) add_leaf(g, p_++);
       if (lambda_ahead()) attach(g, lambda());
       else attach(g, unary());
       return g;
@@ -958,16 +973,16 @@ class JTree {
     add_leaf(g, p_++);  // 'new'
     if (at("<")) {
       const size_t r = skip_type_args(p_);
-      if (r) leaves_to(g, r);
+      if (r) type_leaves(g, r);
     }
     while (at("@")) leaves_to(g, skip_annotation(p_));
     if (primitive_word(t(p_)) || is_ident(t(p_))) {
-      add_leaf(g, p_++);
+      nodes[add_leaf(g, p_++)].tid = true;
       for (;;) {
         if (at("<")) {
           const size_t r = skip_type_args(p_);
           if (r) {
-            leaves_to(g, r);
+            type_leaves(g, r);
             continue;
           }
           if (t(p_ + 1) == ">") {  // diamond
@@ -979,7 +994,7 @@ class JTree {
         }
         if (at(".") && is_ident(t(p_ + 1))) {
           add_leaf(g, p_++);
-          add_leaf(g, p_++);
+          nodes[add_leaf(g, p_++)].tid = true;
           continue;
         }
         break;
@@ -1148,8 +1163,12 @@ struct JWalker {
   const std::vector<JNode>& nd;
   const std::vector<Leaf>& lv;
   std::vector<char> anon;
+  // GraphCodeBERT's parser/DFG.py DFG_java: every named leaf outside the states is an entry
+  // (identifiers define themselves on first sight), and method_invocation has no special case
+  bool ms = false;
 
-  JWalker(const std::vector<JNode>& n, const std::vector<Leaf>& l) : nd(n), lv(l) {
+  JWalker(const std::vector<JNode>& n, const std::vector<Leaf>& l, bool ms_variant)
+      : nd(n), lv(l), ms(ms_variant) {
     anon.resize(l.size());
     // anonymous = node type == recorded code: a keyword / punctuation token whose byte-column
     // slice is intact
@@ -1188,6 +1207,9 @@ struct JWalker {
         auto it = st.find(code);
         if (it != st.end()) {
           dfg.push_back({code, idx, false, {code}, it->second});
+        } else if (ms) {
+          if (!n.tid && is_ident(lv[idx].raw)) st[code] = {idx};
+          dfg.push_back({code, idx, false, {}, {}});
         } else if (n.pname) {
           st[code] = {idx};
           dfg.push_back({code, idx, false, {}, {}});
@@ -1273,7 +1295,7 @@ struct JWalker {
         return dfg;
       }
       case J_INVOKE:
-        if (n.a >= 0) {
+        if (n.a >= 0 && !ms) {
           dfg_append(dfg, walk(n.a, st));
           dfg_append(dfg, walk(n.b, st));
           dfg_sort(dfg);
@@ -1290,10 +1312,10 @@ struct JWalker {
 
 }  // namespace
 
-std::vector<DfgEdge> dfg_java(const std::vector<Leaf>& leaves) {
+std::vector<DfgEdge> dfg_java(const std::vector<Leaf>& leaves, bool ms) {
   JTree tree(leaves);
   const int root = tree.parse();
-  JWalker w(tree.nodes, leaves);
+  JWalker w(tree.nodes, leaves, ms);
   DfgStates states;
   std::vector<DfgEdge> d = w.walk(root, states);
   dfg_sort(d);

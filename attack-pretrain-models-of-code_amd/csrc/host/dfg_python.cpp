@@ -879,12 +879,17 @@ class PyTree {
 struct PWalker {
   const std::vector<PNode>& nd;
   const std::vector<Leaf>& lv;
-  std::vector<char> anon, str;
+  std::vector<char> anon, str, ident;
+  // GraphCodeBERT's parser/DFG.py DFG_python: strings are not skipped and every named leaf
+  // outside the states is an entry (identifiers define themselves on first sight)
+  bool ms = false;
 
-  PWalker(const std::vector<PNode>& n, const std::vector<Leaf>& l, const std::vector<char>& kw)
-      : nd(n), lv(l) {
+  PWalker(const std::vector<PNode>& n, const std::vector<Leaf>& l, const std::vector<char>& kw,
+          bool ms_variant)
+      : nd(n), lv(l), ms(ms_variant) {
     anon.resize(l.size());
     str.resize(l.size());
+    ident.resize(l.size());
     for (size_t i = 0; i < l.size(); ++i) {
       const std::string& r = l[i].raw;
       bool a;
@@ -894,6 +899,7 @@ struct PWalker {
       // node type == recorded code only while the byte-column slice is intact
       anon[i] = a && l[i].text == r;
       str[i] = is_string(r);
+      ident[i] = !a && is_name(r) && r != "True" && r != "False" && r != "None";
     }
   }
 
@@ -944,11 +950,14 @@ struct PWalker {
     switch (n.type) {
       case P_LEAF: {
         const int idx = n.leaf;
-        if (anon[idx] || str[idx]) return dfg;
+        if (anon[idx] || (str[idx] && !ms)) return dfg;
         const std::string& code = lv[idx].text;
         auto it = st.find(code);
         if (it != st.end()) {
           dfg.push_back({code, idx, false, {code}, it->second});
+        } else if (ms) {
+          if (ident[idx]) st[code] = {idx};
+          dfg.push_back({code, idx, false, {}, {}});
         } else if (n.parent >= 0 && nd[n.parent].type == P_PARAMS && is_name(lv[idx].raw)) {
           st[code] = {idx};
           dfg.push_back({code, idx, false, {}, {}});
@@ -1044,11 +1053,11 @@ struct PWalker {
 
 }  // namespace
 
-std::vector<DfgEdge> dfg_python(const std::vector<Leaf>& leaves) {
+std::vector<DfgEdge> dfg_python(const std::vector<Leaf>& leaves, bool ms) {
   if (leaves.empty()) return {};
   PyTree tree(leaves);
   const int root = tree.parse();
-  PWalker w(tree.nodes, leaves, tree.kw);
+  PWalker w(tree.nodes, leaves, tree.kw, ms);
   DfgStates states;
   std::vector<DfgEdge> d = w.walk(root, states);
   dfg_sort(d);

@@ -102,12 +102,16 @@ struct DfgEdge {
 };
 // DFG of C leaves (dfg.cpp), sorted by idx as extract_dataflow returns it (run_parser.py:213)
 std::vector<DfgEdge> dfg_c(const std::vector<Leaf>& leaves);
-// DFG_java over Java leaves (dfg_java.cpp)
-std::vector<DfgEdge> dfg_java(const std::vector<Leaf>& leaves);
-// DFG_python over Python leaves (dfg_python.cpp)
-std::vector<DfgEdge> dfg_python(const std::vector<Leaf>& leaves);
-// the DFG of a language
-std::vector<DfgEdge> dfg_of(const std::vector<Leaf>& leaves, Lang lang);
+// DFG_java / DFG_python over Java / Python leaves (dfg_java.cpp, dfg_python.cpp); ms = the
+// GraphCodeBERT parser/DFG.py variant of the walk (GraphCodeBERT/*/code/parser/DFG.py)
+std::vector<DfgEdge> dfg_java(const std::vector<Leaf>& leaves, bool ms = false);
+std::vector<DfgEdge> dfg_python(const std::vector<Leaf>& leaves, bool ms = false);
+// the DFG of a language: variant 0 = python_parser/run_parser.py extract_dataflow; variant 1 =
+// GraphCodeBERT/*/code/run.py extract_dataflow (parser/DFG.py walk, then only entries that have
+// or are the source of an edge); C has variant 0 only
+enum DfgVariant { DFG_RUN_PARSER = 0, DFG_GCB_RUN = 1 };
+std::vector<DfgEdge> dfg_of(const std::vector<Leaf>& leaves, Lang lang,
+                            DfgVariant variant = DFG_RUN_PARSER);
 // unique DFG names in graph order (get_identifiers before the validity filter, run_parser.py:272)
 std::vector<std::string> dfg_names(const std::vector<Leaf>& leaves, Lang lang);
 

@@ -6,6 +6,12 @@ mhm_attack.py (MHM-NS), over the engine, for the three CodeBERT victims:
               perturbs code1; `code` = (id1, id2, code1, code2))
   authorship  CodeXGLUE/Authorship-Attribution/code/attack.py:199-266, mhm.py:160-233 (Python,
               66 authors, raw-text features; labels from valid.txt, codes from valid_subs.jsonl)
+and their GraphCodeBERT counterparts (GraphModel victims, data-flow features):
+  gcb_devign      GraphCodeBERT/Defect-detection/code/gi_attack.py:154-218 — with its extra
+                  get_results([example]) per example (:161), one more query than the attack's
+  gcb_clone       GraphCodeBERT/clonedetection/code/attack.py:170-223 (the CodeXGLUE
+                  BigCloneBench pairs and substitutes; GraphCodeBERT ships none of its own)
+  gcb_authorship  GraphCodeBERT/Authorship-Attribution/code/gi_attack.py:176-218
 
 The original example's features come from the fixture (run.py of each task), substitutes from its
 `substitutes`; one Recorder CSV row per example; success rate over examples the victim classified
@@ -23,7 +29,8 @@ import time
 import numpy as np
 
 from .attacker import (Attacker, AuthorshipAttacker, AuthorshipMHM_Attacker, CloneAttacker,
-                       MHM_Attacker, get_identifiers)
+                       GraphAttacker, GraphAuthorshipAttacker, GraphCloneAttacker, MHM_Attacker,
+                       get_identifiers)
 from .host import Tokenizer
 from .utils import Recorder, build_vocab, set_seed
 
@@ -39,7 +46,10 @@ class AttackArgs:
     csv_store_path: str | None = None
     rng: str = "global"   # "global": one random stream in example order (reference);
                           # "per_example": random.seed(seed + index) before each example
-    task: str = "devign"  # devign | clone | authorship (CodeBERT victims)
+    task: str = "devign"  # devign | clone | authorship (CodeBERT) | gcb_devign | gcb_clone |
+                          # gcb_authorship (GraphCodeBERT)
+    code_length: int = 512        # GraphCodeBERT rows: code_length + data_flow_length tokens
+    data_flow_length: int = 128
 
 
 def load_fixture(path, start=0, end=None, labels_path=None):
@@ -67,12 +77,21 @@ def load_fixture(path, start=0, end=None, labels_path=None):
     return codes, subs, labels
 
 
-def _example(tok, code, label, block, task="devign"):
+def _example(tok, code, label, block, task="devign", args=None):
     """TextDataset item of each task: devign (ids of ' '.join(func.split()), label) (run.py:79-86);
     clone ([ids(code1) | ids(code2)], label) (Clone-detection-BigCloneBench/code/run.py:65-119);
-    authorship (ids of the raw code, label) (Authorship-Attribution/code/run.py:81-89)."""
+    authorship (ids of the raw code, label) (Authorship-Attribution/code/run.py:81-89); the
+    GraphCodeBERT tasks: the reference's dataset tuples of data-flow features (run.py of each)."""
     import torch
 
+    if task.startswith("gcb_"):
+        from .graph import CodePairDataset, GraphCodeDataset, pair_features, task_features
+
+        t = task[4:]
+        if t == "clone":
+            return CodePairDataset([pair_features(code[2], code[3], tok, label, args,
+                                                  original=True)], args)[0]
+        return GraphCodeDataset([task_features(code, tok, label, args, t)], args)[0]
     if task == "clone":
         ids, _ = tok.featurize([code[2], code[3]], block)
         row = np.concatenate([ids[0], ids[1]])
@@ -82,7 +101,9 @@ def _example(tok, code, label, block, task="devign"):
     return torch.from_numpy(row.astype(np.int64)), torch.tensor(label)
 
 
-ATTACKERS = {"devign": Attacker, "clone": CloneAttacker, "authorship": AuthorshipAttacker}
+ATTACKERS = {"devign": Attacker, "clone": CloneAttacker, "authorship": AuthorshipAttacker,
+             "gcb_devign": GraphAttacker, "gcb_clone": GraphCloneAttacker,
+             "gcb_authorship": GraphAuthorshipAttacker}
 
 
 def make_attacker(args, model, tok):
@@ -90,10 +111,16 @@ def make_attacker(args, model, tok):
                                                       threshold_pred_score=0)
 
 
+def _is_clone(task):
+    return task in ("clone", "gcb_clone")
+
+
 def attack_one(attacker, tok, code, subs, label, args):
     task = getattr(args, "task", "devign")
-    example = _example(tok, code, label, args.block_size, task)
-    first = (subs, code) if task == "clone" else (code, subs)  # clone: (example, subs, code)
+    example = _example(tok, code, label, args.block_size, task, args)
+    if task == "gcb_devign":  # GraphCodeBERT/Defect-detection/code/gi_attack.py:161
+        attacker.model_tgt.get_results([example], args.eval_batch_size)
+    first = (subs, code) if _is_clone(task) else (code, subs)  # clone: (example, subs, code)
     res = attacker.greedy_attack(example, *first)
     attack_type = "Greedy"
     if res[6] == -1 and args.use_ga:
@@ -105,8 +132,10 @@ def attack_one(attacker, tok, code, subs, label, args):
 def attack_one_gen(attacker, tok, code, subs, label, args, rng):
     """attack_one as a request generator (gi_attack.py:177-186): greedy, then GA on -1."""
     task = getattr(args, "task", "devign")
-    example = _example(tok, code, label, args.block_size, task)
-    first = (subs, code) if task == "clone" else (code, subs)
+    example = _example(tok, code, label, args.block_size, task, args)
+    if task == "gcb_devign":  # the driver's extra get_results([example]) (gi_attack.py:161)
+        yield attacker.model_tgt.prepare([example])
+    first = (subs, code) if _is_clone(task) else (code, subs)
     res = yield from attacker.greedy_gen(example, *first)
     attack_type = "Greedy"
     if res[6] == -1 and args.use_ga:
@@ -255,7 +284,7 @@ def run_mhm_attack(model, codes, subs, labels, args: AttackArgs, indices=None, t
     order = list(range(len(codes))) if indices is None else list(indices)
     records, t0 = [], time.time()
     if max_inflight > 1:
-        exs = [_example(tok, codes[i], labels[i], args.block_size, task) for i in order]
+        exs = [_example(tok, codes[i], labels[i], args.block_size, task, args) for i in order]
         _, preds = model.get_results(exs, args.eval_batch_size) if exs else ([], [])
         by_index, jobs, job_index = {}, [], []
         for index, p in zip(order, preds):
@@ -273,7 +302,7 @@ def run_mhm_attack(model, codes, subs, labels, args: AttackArgs, indices=None, t
         records = [by_index[i] for i in order]
         order = []
     for index in order:
-        example = _example(tok, codes[index], labels[index], args.block_size, task)
+        example = _example(tok, codes[index], labels[index], args.block_size, task, args)
         q0 = model.query
         probs, preds = model.get_results([example], args.eval_batch_size)
         if preds[0] != labels[index]:

@@ -2,12 +2,24 @@
 `Model` whose forward averages data-flow node embeddings (ae_score_graph).
 
 Mirrors:
-  convert_code_to_features (GCB)   GraphCodeBERT/Defect-detection/code/attacker.py:30-63
-  pair features (clone)            GraphCodeBERT/clonedetection/code/attacker.py:33-72
+  convert_code_to_features (GCB)   GraphCodeBERT/Defect-detection/code/attacker.py:30-63,
+                                   GraphCodeBERT/Authorship-Attribution/code/attacker.py:52-88
+  pair features (clone)            GraphCodeBERT/clonedetection/code/attacker.py:33-72; the
+                                   original example: clonedetection/code/run.py:148-192
   GraphCodeDataset / CodePairDataset  utils.py:540-639
   Model.forward / get_results      GraphCodeBERT/Defect-detection/code/model.py:24-60,
                                    GraphCodeBERT/clonedetection/code/model.py:41-85
-  extract_dataflow                 python_parser/run_parser.py:190-216 (DFG from csrc/host/dfg.cpp)
+  extract_dataflow                 python_parser/run_parser.py:190-216 (variant DFG_RUN_PARSER) and
+                                   GraphCodeBERT/*/code/run.py:72-109 (DFG_GCB_RUN: parser/DFG.py
+                                   walk + edge filter) — both in csrc/host/dfg*.cpp
+
+Which builder, language and whitespace handling each GraphCodeBERT victim uses (TASK_FEATURES):
+  devign      C,      ' '.join(code.split()), run_parser      (attacker.py:30-32, run.py:89-92)
+  clone       Java,   text as is,             run_parser for attack-time mutants; the original
+                                              pair from run.py (DFG_GCB_RUN, truncation -3 and
+                                              at most 509 code tokens)
+  authorship  Python, text as is,             DFG_GCB_RUN for every query (attacker.py imports
+                                              run.extract_dataflow)
 
 The reference builds a bool [L, L] mask per query in Python loops and ships it to the GPU as
 L*L bytes; here the mask is built with numpy slices and shipped bit-packed (uint32 [L, L/32],
@@ -18,10 +30,13 @@ from __future__ import annotations
 
 import numpy as np
 
-from .host import Example
+from .host import DFG_GCB_RUN, DFG_RUN_PARSER, Example
 from .model import Model, Payload
 
 DFG_REL = ("comesFrom", "computedFrom")
+# task -> (language, normalise whitespace, data-flow builder of the attack-time queries)
+TASK_FEATURES = {"devign": ("c", True, DFG_RUN_PARSER), "clone": ("java", False, DFG_RUN_PARSER),
+                 "authorship": ("python", False, DFG_GCB_RUN)}
 
 
 class GraphInputFeatures:
@@ -38,13 +53,15 @@ class GraphInputFeatures:
         self.label = label
 
 
-def extract_dataflow(code: str, lang: str = "c"):
+def extract_dataflow(code: str, lang: str = "c", variant: int = DFG_RUN_PARSER):
     """run_parser.py:190-216 -> (DFG sorted by leaf index, index_table, code_tokens).  DFG entries
-    are (code, idx, relation, [from names], [from idx]) as DFG_c builds them; index_table is not
-    reproduced (no caller on the query path reads it) and is returned as None."""
+    are (code, idx, relation, [from names], [from idx]) as DFG_c / DFG_java / DFG_python build
+    them; index_table is not reproduced (no caller on the query path reads it) and is returned
+    as None.  variant=DFG_GCB_RUN: GraphCodeBERT run.py's builder (parser/DFG.py + edge filter)."""
     ex = Example(code, lang)
     toks = ex.leaves(identifiers=True)
-    dfg = [(toks[i], i, DFG_REL[int(comp)], [toks[j] for j in fr], fr) for i, comp, fr in ex.dfg()]
+    dfg = [(toks[i], i, DFG_REL[int(comp)], [toks[j] for j in fr], fr)
+           for i, comp, fr in ex.dfg(variant)]
     return dfg, None, toks
 
 
@@ -74,17 +91,24 @@ def _leaf_ids(tokenizer):
     return c
 
 
-def convert_code_to_features(code, tokenizer, label, args, lang: str = "c"):
+def convert_code_to_features(code, tokenizer, label, args, lang: str = "c", normalize: bool = True,
+                             variant: int = DFG_RUN_PARSER, run_trunc: bool = False):
     """GraphCodeBERT/Defect-detection/code/attacker.py:30-63 (code_length + data_flow_length
-    row; DFG nodes appended as <unk> ids at position 0; pads at position pad_id)."""
-    code = " ".join(code.split())
-    dfg, _, code_tokens = extract_dataflow(code, lang)
+    row; DFG nodes appended as <unk> ids at position 0; pads at position pad_id).  normalize:
+    ' '.join(code.split()) first (Devign only); run_trunc: clonedetection/code/run.py:166's
+    truncation (one token fewer, at most 509 code tokens)."""
+    if normalize:
+        code = " ".join(code.split())
+    dfg, _, code_tokens = extract_dataflow(code, lang, variant)
     leaf = _leaf_ids(tokenizer)
     runs = [leaf(x, idx == 0) for idx, x in enumerate(code_tokens)]
     ends = np.cumsum([0] + [len(r) for r in runs])  # ori2cur_pos[i] = (ends[i], ends[i+1])
     flat = [y for r in runs for y in r]
     total = args.code_length + args.data_flow_length
-    flat = flat[:total - 2 - min(len(dfg), args.data_flow_length)]
+    if run_trunc:
+        flat = flat[:total - 3 - min(len(dfg), args.data_flow_length)][:512 - 3]
+    else:
+        flat = flat[:total - 2 - min(len(dfg), args.data_flow_length)]
     pad, cls, sep, unk = (tokenizer.pad_token_id, tokenizer.cls_token_id, tokenizer.sep_token_id,
                           tokenizer.unk_token_id)
     source_ids = [cls] + flat + [sep]
@@ -100,6 +124,23 @@ def convert_code_to_features(code, tokenizer, label, args, lang: str = "c"):
     dfg_to_code = [(int(ends[x[1]]) + 1, int(ends[x[1] + 1]) + 1) for x in dfg]
     # input_tokens (strings) are not read by any query-path consumer
     return GraphInputFeatures(None, source_ids, position_idx, dfg_to_code, dfg_to_dfg, 0, label)
+
+
+def task_features(code, tokenizer, label, args, task: str, **kw):
+    """convert_code_to_features with the language / whitespace / builder of a task's attacker."""
+    lang, normalize, variant = TASK_FEATURES[task]
+    kw.setdefault("variant", variant)
+    return convert_code_to_features(code, tokenizer, label, args, lang, normalize, **kw)
+
+
+def pair_features(code1, code2, tokenizer, label, args, original: bool = False):
+    """One clone query: GraphPairFeatures of (code1, code2).  original=True builds them as
+    clonedetection/code/run.py does for the dataset example (DFG_GCB_RUN, run.py truncation);
+    otherwise as attacker.py:33-72 does for every mutant (run_parser builder)."""
+    kw = dict(variant=DFG_GCB_RUN, run_trunc=True) if original else {}
+    f1 = task_features(code1, tokenizer, label, args, "clone", **kw)
+    f2 = task_features(code2, tokenizer, label, args, "clone", **kw)
+    return GraphPairFeatures(f1, f2, label)
 
 
 def graph_mask(input_ids, position_idx, dfg_to_code, dfg_to_dfg, L: int | None = None) -> np.ndarray:
@@ -227,8 +268,12 @@ def _pack_items(dataset, pair: bool):
 
 
 class GraphModel(Model):
-    """GraphCodeBERT victim: task "devign" (sigmoid head, GraphCodeBERT/Defect-detection) or
-    "clone" (pair head over interleaved code1/code2 rows, GraphCodeBERT/clonedetection)."""
+    """GraphCodeBERT victim: task "devign" (sigmoid head, GraphCodeBERT/Defect-detection),
+    "clone" (pair head over interleaved code1/code2 rows, GraphCodeBERT/clonedetection) or
+    "authorship" (66-way softmax, GraphCodeBERT/Authorship-Attribution/code/model.py:29-60)."""
+
+    # mutant rows are data-flow features, never spliced token ids (MHM_Attacker checks this)
+    population_rows = None
 
     def __init__(self, encoder, config=None, tokenizer=None, args=None, task: str = "devign",
                  precision: str = "fp32", device: int = 0):
@@ -289,6 +334,13 @@ class GraphModel(Model):
 
     def dataset_from_texts(self, texts, tokenizer, args, label=0):
         """Mutant texts -> GraphCodeDataset (the GCB attacker featurises every mutant text with
-        convert_code_to_features, GraphCodeBERT/Defect-detection/code/attacker.py:30-63)."""
-        return GraphCodeDataset([convert_code_to_features(t, tokenizer, label, args)
+        convert_code_to_features, GraphCodeBERT/Defect-detection/code/attacker.py:30-63, with the
+        task's language and builder).  Clone pairs are built by GraphCloneAttacker."""
+        if self.task == "clone":
+            raise ValueError("clone queries are pairs: build them with pair_features")
+        return GraphCodeDataset([task_features(t, tokenizer, label, args, self.task)
                                  for t in texts], args)
+
+    def prepare_pair_population(self, feats1, f2) -> Payload:
+        """Clone queries of mutated code1 features against one fixed code2 (rows interleaved)."""
+        return self.prepare(CodePairDataset([GraphPairFeatures(f, f2, 0) for f in feats1]))

@@ -12,6 +12,8 @@ from . import DATA_DIR, HOSTLIB_PATH
 LANG = {"c": 0, "java": 1, "python": 2}
 MODE_BATCH, MODE_SINGLE = 0, 1
 MODE_RAW = 16  # flag: featurise the raw mutant text (Authorship-Attribution victim)
+DFG_RUN_PARSER = 0  # python_parser/run_parser.py extract_dataflow
+DFG_GCB_RUN = 1     # GraphCodeBERT/*/code/run.py extract_dataflow (parser/DFG.py + edge filter)
 
 _LIB = None
 
@@ -46,9 +48,11 @@ def load_host_library(path=None) -> ctypes.CDLL:
     lib.ah_example_word_table.argtypes = [vp, vp, i32, vp, i32, ctypes.POINTER(i32)]
     lib.ah_example_identifiers.argtypes = [vp, vp, i32]
     lib.ah_example_dfg.argtypes = [vp, vp, i32, vp, i32]
+    lib.ah_example_dfg_variant.argtypes = [vp, i32, vp, i32, vp, i32]
     lib.ah_remove_comments.argtypes = [cp, vp, i32]
     lib.ah_last_error.restype = ctypes.c_char_p
-    for f in ("ah_example_identifiers", "ah_example_dfg", "ah_remove_comments",
+    for f in ("ah_example_identifiers", "ah_example_dfg", "ah_example_dfg_variant",
+              "ah_remove_comments",
               "ah_tokenizer_special", "ah_tokenize", "ah_decode", "ah_featurize_batch",
               "ah_featurize_batch_raw", "ah_tokens_to_ids",
               "ah_example_num_leaves", "ah_example_leaves", "ah_example_mutant_text",
@@ -180,18 +184,19 @@ class Example:
         self.lib.ah_example_identifiers(self.h, buf, need)
         return [p.decode("utf-8") for p in buf.raw[:need].split(b"\0")[:-1]] if need else []
 
-    def dfg(self):
+    def dfg(self, variant: int = DFG_RUN_PARSER):
         """extract_dataflow(code, lang)[0] as (idx, computed, from_idx list) per entry, sorted by
-        leaf index (run_parser.py:190-216; DFG_c.py / DFG_java.py / DFG_python.py).  The entry's
+        leaf index (run_parser.py:190-216; DFG_c.py / DFG_java.py / DFG_python.py), or with
+        variant=DFG_GCB_RUN GraphCodeBERT run.py's (parser/DFG.py + edge filter).  The entry's
         code is leaves(True)[idx]."""
-        n = self.lib.ah_example_dfg(self.h, None, 0, None, 0)
+        n = self.lib.ah_example_dfg_variant(self.h, variant, None, 0, None, 0)
         if n < 0:
-            _err("ah_example_dfg")
+            _err("ah_example_dfg_variant")
         rows = np.zeros((max(n, 1), 4), dtype=np.int32)
         cap = 16
         while True:
             fr = np.zeros((cap,), dtype=np.int32)
-            r = self.lib.ah_example_dfg(self.h, _i32p(rows), n, _i32p(fr), cap)
+            r = self.lib.ah_example_dfg_variant(self.h, variant, _i32p(rows), n, _i32p(fr), cap)
             if r >= 0:
                 break
             cap = -r - 1

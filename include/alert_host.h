@@ -18,6 +18,8 @@
  *   ah_example_mutant_words   <- the same, as word-id sequences for the device splice (ae_splice)
  *   ah_example_identifiers    <- get_identifiers(code, lang)[0] (run_parser.py:272-281)
  *   ah_example_dfg            <- extract_dataflow(code, lang)[0] (run_parser.py:190-216, DFG_c.py)
+ *   ah_example_dfg_variant    <- the same, or GraphCodeBERT/{clonedetection,Authorship-Attribution}/code/run.py extract_dataflow
+ *                                (parser/DFG.py + edge filter)
  *   ah_remove_comments        <- remove_comments_and_docstrings (parser_folder/utils.py:30-87)
  * All strings are UTF-8, NUL-terminated.  Functions return >= 0 on success (a count) or a
  * negative code; ah_last_error() describes the last failure of the calling thread.
@@ -93,14 +95,26 @@ int32_t ah_example_word_table(ah_example *ex, int32_t *word_tok, int32_t cap_tok
 
 /* get_identifiers(code, lang) before its validity filter (python_parser/run_parser.py:272-281):
  * the unique names of the data-flow graph in graph order, over the comment-stripped leaves
- * (which = 1).  NUL-separated; returns bytes needed.  C only (other languages: empty). */
+ * (which = 1).  NUL-separated; returns bytes needed. */
 int32_t ah_example_identifiers(ah_example *ex, char *buf, int32_t cap);
-/* extract_dataflow(code, lang)[0] (run_parser.py:190-216 + DFG_c.py:10-191), sorted by leaf
- * index.  rows [n, 4] = (leaf idx, 1 if computedFrom else 0, offset, count) into from_idx.
- * Returns n (call with NULL buffers to size them; -(n_from)-1 if cap_from is too small).
- * C only (other languages return an error). */
+/* extract_dataflow(code, lang)[0] (run_parser.py:190-216 + DFG_c.py / DFG_java.py /
+ * DFG_python.py), sorted by leaf index.  rows [n, 4] = (leaf idx, 1 if computedFrom else 0,
+ * offset, count) into from_idx.  Returns n (call with NULL buffers to size them; -(n_from)-1 if
+ * cap_from is too small). */
 int32_t ah_example_dfg(ah_example *ex, int32_t *rows, int32_t cap_rows, int32_t *from_idx,
                        int32_t cap_from);
+/* The same for one of two data-flow builders of the reference:
+ *   AH_DFG_RUN_PARSER  python_parser/run_parser.py extract_dataflow (== ah_example_dfg): the
+ *                      attack-time mutants of every GraphCodeBERT attacker except authorship
+ *   AH_DFG_GCB_RUN     GraphCodeBERT/{clonedetection,Authorship-Attribution}/code/run.py
+ *                      extract_dataflow: parser/DFG.py's DFG_java / DFG_python (every named leaf
+ *                      an entry, identifiers defined at first sight, no method_invocation case),
+ *                      then only entries with an edge or that are an edge's source (run.py:96-106);
+ *                      Java and Python only */
+#define AH_DFG_RUN_PARSER 0
+#define AH_DFG_GCB_RUN 1
+int32_t ah_example_dfg_variant(ah_example *ex, int32_t variant, int32_t *rows, int32_t cap_rows,
+                               int32_t *from_idx, int32_t cap_from);
 /* remove_comments_and_docstrings(code, 'c'|'java') (parser_folder/utils.py:30-87); returns
  * bytes needed incl. NUL. */
 int32_t ah_remove_comments(const char *code, char *out, int32_t cap);

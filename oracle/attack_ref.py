@@ -40,10 +40,13 @@ class Victim:
         self.score = score
         self.block = block_size
         self.task = task
+        self.base = task[4:] if task.startswith("gcb_") else task
         self.query = 0
-        self.lang = {"devign": "c", "clone": "java", "authorship": "python"}[task]
-        self.ga_children = 64 if task == "clone" else None
-        self.empty_pool_exit = task == "devign"
+        self.lang = {"devign": "c", "clone": "java", "authorship": "python"}[self.base]
+        # GA children per iteration: 64 in the CodeBERT clone (attacker.py:226) and GraphCodeBERT
+        # Devign (attacker.py:246) attackers, eval_batch_size elsewhere
+        self.ga_children = 64 if task in ("clone", "gcb_devign") else None
+        self.empty_pool_exit = task in ("devign", "gcb_devign")
         if task == "clone":
             tok = fr.tokenizer()
             self._half2 = self._row(tok.tokenize(" ".join(code2.split())))
@@ -81,11 +84,13 @@ class Victim:
             self.query += len(ids) // 2
         else:
             self.query += len(ids)
-        out = np.asarray(self.score(ids), dtype=np.float32)
-        if self.task == "devign":
+        return self.format(np.asarray(self.score(ids), dtype=np.float32))
+
+    def format(self, out):
+        if self.base == "devign":
             p = out.reshape(-1)
             return [[1 - x, x] for x in p], [1 if x > 0.5 else 0 for x in p]
-        if self.task == "clone":  # Clone-detection-BigCloneBench/code/model.py:81-82
+        if self.base == "clone":  # Clone-detection-BigCloneBench/code/model.py:81-82
             return list(out), [0 if x > 0.5 else 1 for x in out[:, 0]]
         return list(out), [int(np.argmax(x)) for x in out]  # Authorship model.py:84-89
 

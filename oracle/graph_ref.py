@@ -24,9 +24,11 @@ from . import featurize_ref
 from . import roberta_cpu
 
 
-def convert_code_to_features(dfg, code_tokens, code_length=512, data_flow_length=128):
+def convert_code_to_features(dfg, code_tokens, code_length=512, data_flow_length=128,
+                             run_trunc=False):
     """dfg: [(code, idx, rel, [names], [idx])] sorted by idx; code_tokens: leaf strings.
-    Returns (input_ids, position_idx, dfg_to_code, dfg_to_dfg) exactly as attacker.py:30-63."""
+    Returns (input_ids, position_idx, dfg_to_code, dfg_to_dfg) exactly as attacker.py:30-63
+    (run_trunc: GraphCodeBERT/clonedetection/code/run.py:166's truncation)."""
     tokenizer = featurize_ref.tokenizer()
     dfg = list(dfg)
     code_tokens = [tokenizer.tokenize('@ ' + x)[1:] if idx != 0 else tokenizer.tokenize(x)
@@ -36,7 +38,12 @@ def convert_code_to_features(dfg, code_tokens, code_length=512, data_flow_length
     for i in range(len(code_tokens)):
         ori2cur_pos[i] = (ori2cur_pos[i - 1][1], ori2cur_pos[i - 1][1] + len(code_tokens[i]))
     code_tokens = [y for x in code_tokens for y in x]
-    code_tokens = code_tokens[:code_length + data_flow_length - 2 - min(len(dfg), data_flow_length)]
+    if run_trunc:
+        code_tokens = code_tokens[:code_length + data_flow_length - 3
+                                  - min(len(dfg), data_flow_length)][:512 - 3]
+    else:
+        code_tokens = code_tokens[:code_length + data_flow_length - 2
+                                  - min(len(dfg), data_flow_length)]
     source_tokens = [tokenizer.cls_token] + code_tokens + [tokenizer.sep_token]
     source_ids = tokenizer.convert_tokens_to_ids(source_tokens)
     position_idx = [i + tokenizer.pad_token_id + 1 for i in range(len(source_tokens))]
@@ -96,3 +103,65 @@ def graph_score(sd, inputs_ids, attn_mask, position_idx, kind="sigmoid1", layers
     h = roberta_cpu.encoder_forward(sd, inputs_ids, pos=position_idx, attn_mask=attn_mask,
                                     layers=layers, inputs_embeds=inputs_embeddings)
     return roberta_cpu.head_forward(sd, h, kind).numpy()
+
+
+class GraphTextVictim:
+    """Text-driven GraphCodeBERT victim for oracle/attack_ref.py's greedy / ga: every query text
+    is featurised here (the product's data-flow graph of the text, then this file's features and
+    mask) and scored by `score(ids, pos, bits) -> head outputs` (pair rows interleaved).
+
+    task: gcb_devign (C, ' '.join(split()), run_parser flow), gcb_clone (Java pairs: mutants and
+    code2 with the run_parser flow; the dataset example with GraphCodeBERT run.py's flow and
+    truncation; importance rows against ' '.join(leaves of code2)), gcb_authorship (Python,
+    run.py's flow for every query)."""
+
+    def __init__(self, score, task, code0, code_length=512, data_flow_length=128, code2=None):
+        from . import attack_ref
+
+        self._fmt = attack_ref.Victim(None, code_length + data_flow_length, task=task)
+        self.lang, self.base = self._fmt.lang, self._fmt.base
+        self.ga_children, self.empty_pool_exit = self._fmt.ga_children, self._fmt.empty_pool_exit
+        self.task, self.score, self.code0, self.code2 = task, score, code0, code2
+        self.cl, self.dl = code_length, data_flow_length
+        self.query = 0
+        if task == "gcb_clone":
+            self.code2_words = " ".join(featurize_ref.identifier_code_tokens(code2, "java"))
+
+    def _feats(self, code, variant, run_trunc=False):
+        from apmc_amd.graph import extract_dataflow
+
+        if self.base == "devign":
+            code = " ".join(code.split())
+        dfg, _, toks = extract_dataflow(code, self.lang, variant)
+        ids, pos, d2c, d2d = convert_code_to_features(dfg, toks, self.cl, self.dl, run_trunc)
+        L = len(ids)
+        m = graph_mask(ids, pos, d2c, d2d, L)
+        return ids, pos, np.packbits(m, axis=-1, bitorder="little").view("<i4")
+
+    def _variant(self):
+        return 1 if self.base == "authorship" else 0
+
+    def _run(self, feats):
+        n = len(feats) // 2 if self.base == "clone" else len(feats)
+        self.query += n
+        out = self.score(np.array([f[0] for f in feats], np.int32),
+                         np.array([f[1] for f in feats], np.int32),
+                         np.stack([f[2] for f in feats]))
+        return self._fmt.format(np.asarray(out, dtype=np.float32))
+
+    def texts(self, codes):
+        if self.base == "clone":
+            f2 = self._feats(self.code2, 0)
+            return self._run([f for c in codes for f in (self._feats(c, 0), f2)])
+        return self._run([self._feats(c, self._variant()) for c in codes])
+
+    def importance(self, word_lists):
+        if self.base == "clone":
+            f2 = self._feats(self.code2_words, 0)
+            return self._run([f for w in word_lists for f in (self._feats(" ".join(w), 0), f2)])
+        return self.texts([" ".join(w) for w in word_lists])
+
+    def ids(self, _ids0):
+        if self.base == "clone":  # the dataset example: run.py's data flow and truncation
+            return self._run([self._feats(self.code0, 1, True), self._feats(self.code2, 1, True)])
+        return self.texts([self.code0])

@@ -90,10 +90,47 @@ def test_greedy_then_ga_matches_text_oracle(victim, chunk):
         _OUTCOMES.append((kind, res[6]))
 
 
+# a GA success at config-2 shape: fixture example 55 with this victim and the per-example seed
+# (found by tools/debug/find_ga_success.py: 1 GA success among the 289 config-2-sized examples)
+GA_SUCCESS_INDEX = 55
+
+
+def test_config2_ga_success_matches_text_oracle(victim):
+    from apmc_amd.drivers import AttackArgs, _example, load_fixture, make_attacker
+    from apmc_amd.host import Tokenizer
+
+    codes, subs, labels = load_fixture(FIXTURE, 0, 200)
+    tok = Tokenizer()
+    args = AttackArgs(block_size=CONFIG2_BLOCK, eval_batch_size=CONFIG2_BATCH)
+    att = make_attacker(args, victim, tok)
+    i = GA_SUCCESS_INDEX
+    code, sb, lab = codes[i], subs[i], labels[i]
+    random.seed(args.seed + i)
+    q0 = victim.query
+    ex = _example(tok, code, lab, CONFIG2_BLOCK)
+    res = att.greedy_attack(ex, code, sb)
+    assert res[6] == -1
+    res = att.ga_attack(ex, code, sb, initial_replace=res[11])
+    q_prod = victim.query - q0
+    random.seed(args.seed + i)
+    v = attack_ref.Victim(_score_fn(victim), CONFIG2_BLOCK)
+    ids0 = ex[0].numpy().astype(np.int32)
+    ref = attack_ref.greedy(v, ids0, lab, code, sb)
+    assert ref["is_success"] == -1
+    ref = attack_ref.ga(v, ids0, lab, code, sb, initial_replace=ref["replaced"],
+                        eval_batch_size=CONFIG2_BATCH)
+    assert res[6] == ref["is_success"] == 1
+    assert q_prod == v.query
+    assert res[2] == ref["adv_code"]
+    assert (res[9], res[10]) == (ref["nb_changed_var"], ref["nb_changed_pos"])
+    assert dict(res[11]) == ref["replaced"]
+    _OUTCOMES.append(("ga", res[6]))
+
+
 def test_config2_sample_exercises_both_attacks():
-    """The 16 config-2 examples above include a greedy success and a GA success."""
-    if len(_OUTCOMES) < 16:
-        pytest.skip("needs the four chunks of test_greedy_then_ga_matches_text_oracle")
+    """The config-2 examples above include a greedy success and a GA success."""
+    if len(_OUTCOMES) < 17:
+        pytest.skip("needs the chunks of test_greedy_then_ga_matches_text_oracle and the GA case")
     assert ("greedy", 1) in _OUTCOMES and ("ga", 1) in _OUTCOMES, _OUTCOMES
 
 
@@ -313,5 +350,38 @@ def test_task_attack_matches_text_oracle(task):
                                                  for c in codes])[1]]
     seen = compare_task(task, model, score, codes, subs, labels, CONFIG2_BLOCK, CONFIG2_BATCH,
                         6000, range(len(codes)))
+    print(task, seen)
+    assert {o for _, o in seen} & {1, -1}, seen
+
+
+@pytest.mark.parametrize("task", ["gcb_clone", "gcb_authorship", "gcb_devign"])
+def test_gcb_task_attack_matches_text_oracle(task):
+    """GraphCodeBERT victims on the HIP engine (graph forward, L = 512 + 128 = 640): the
+    GraphCloneAttacker / GraphAuthorshipAttacker / GraphAttacker and the gcb_* drivers against
+    the text oracle (oracle/graph_ref.GraphTextVictim) scoring the same texts with the same
+    engine: identical outcomes, query counts, adversarial code and replacements."""
+    from apmc_amd.drivers import AttackArgs, _example, load_fixture
+    from apmc_amd.graph import GraphModel
+    from apmc_amd.host import Tokenizer
+    from test_task_attacks import compare_gcb_with, fixture
+
+    base = task[4:]
+    head, nl = {"clone": ("pair2", 2), "authorship": ("softmaxN", 66),
+                "devign": ("sigmoid1", 1)}[base]
+    args = AttackArgs(block_size=512, eval_batch_size=32, task=task, code_length=512,
+                      data_flow_length=128)
+    model = GraphModel(synthetic_sd(seed=5, head=head, num_labels=nl, out_std=8.0), task=base,
+                       args=args)
+    if base == "devign":
+        codes, subs, _ = load_fixture(FIXTURE, 0, 120)
+        pick = _pick(codes, subs, 4)
+    else:
+        codes, subs, _ = fixture(base, 4)
+        pick = list(range(4))
+    tok = Tokenizer()
+    labels = [0] * len(codes)
+    for i in pick:
+        labels[i] = int(model.get_results([_example(tok, codes[i], 0, 512, task, args)])[1][0])
+    seen = compare_gcb_with(task, model, model.score_packed, codes, subs, labels, args, 9000, pick)
     print(task, seen)
     assert {o for _, o in seen} & {1, -1}, seen

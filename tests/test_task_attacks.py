@@ -101,3 +101,129 @@ def test_task_attack_matches_text_oracle_cpu(task):
     victim = HostIdsVictim(score, task=task, block_size=BLOCK)
     seen = compare_task(task, victim, score, codes, subs, labels, BLOCK, 16, 4000, range(12))
     assert ("Greedy", 1) in seen and any(k == "GA" for k, _ in seen), seen
+
+
+# ---------------------------------------------------------------- GraphCodeBERT victims (CPU)
+GCB_ARGS = dict(code_length=192, data_flow_length=64)
+
+
+def graph_stand_in(base):
+    """numpy scores of (ids, pos, mask bits) rows: token and mask terms, so a feature or mask
+    difference between product and oracle changes the scores."""
+    rng = np.random.default_rng(13)
+    w = rng.standard_normal(50265)
+    w66 = rng.standard_normal((50265, 66))
+
+    def row_terms(ids, pos, bits):
+        tok = np.where(pos > 1, w[ids], 0.0).sum(1)
+        mk = (bits.astype(np.int64) % 7).sum(axis=(1, 2)) * 1e-3
+        return tok, mk
+
+    def score(ids, pos, bits):
+        tok, mk = row_terms(ids, pos, bits)
+        if base == "clone":
+            z = (tok + mk).reshape(-1, 2)
+            p = 1.0 / (1.0 + np.exp(-(z[:, 0] - z[:, 1]) / 0.5))
+            return np.stack([p, 1 - p], 1).astype(np.float32)
+        if base == "devign":
+            return (1.0 / (1.0 + np.exp(-(tok + mk) / 3.0))).astype(np.float32)[:, None]
+        z = (w66[ids] * (pos > 1)[..., None]).sum(1) / 20.0 + mk[:, None]
+        z = np.exp(z - z.max(1, keepdims=True))
+        return (z / z.sum(1, keepdims=True)).astype(np.float32)
+    return score
+
+
+def host_graph_victim(score, base):
+    """The product GraphModel request API over a numpy scorer (no engine on this host)."""
+    import _apmc  # noqa: F401
+    from apmc_amd.graph import GraphModel
+
+    class HostGraphVictim(GraphModel):
+        def __init__(self):  # noqa: D107 — no engine
+            self.task, self.query, self.raw = base, 0, False
+            self.args = None
+
+        def score_packed(self, ids, pos, bits):
+            return np.asarray(score(ids, pos, bits))
+
+    return HostGraphVictim()
+
+
+def compare_gcb(task, codes, subs, labels, batch, seed0, idx):
+    from apmc_amd.drivers import AttackArgs
+
+    base = task[4:]
+    args = AttackArgs(block_size=256, eval_batch_size=batch, task=task, **GCB_ARGS)
+    score = graph_stand_in(base)
+    victim = host_graph_victim(score, base)
+    victim.args = args
+    return compare_gcb_with(task, victim, score, codes, subs, labels, args, seed0, idx)
+
+
+def compare_gcb_with(task, victim, score, codes, subs, labels, args, seed0, idx):
+    """Product attack (sequential driver step) vs the text oracle on examples `idx`."""
+    from apmc_amd.drivers import attack_one, make_attacker
+    from apmc_amd.host import Tokenizer
+    from oracle.graph_ref import GraphTextVictim
+
+    base = task[4:]
+    batch = args.eval_batch_size
+    tok = Tokenizer()
+    gcb = dict(code_length=args.code_length, data_flow_length=args.data_flow_length)
+    att = make_attacker(args, victim, tok)
+    seen = []
+    for i in idx:
+        code, sb, lab = codes[i], subs[i], labels[i]
+        random.seed(seed0 + i)
+        q0 = victim.query
+        res, kind = attack_one(att, tok, code, sb, lab, args)
+        q_prod = victim.query - q0
+        random.seed(seed0 + i)
+        text = code[2] if base == "clone" else code
+        v = GraphTextVictim(score, task, text, code2=code[3] if base == "clone" else None, **gcb)
+        extra = 0
+        if task == "gcb_devign":  # the driver's extra get_results([example])
+            v.ids(None)
+            extra = 1
+        ids0 = np.zeros(1, np.int32)  # unused: GraphTextVictim.ids featurises the text
+        ref = attack_ref.greedy(v, ids0, lab, text, sb)
+        ref_kind = "Greedy"
+        if ref["is_success"] == -1:
+            ref = attack_ref.ga(v, ids0, lab, text, sb, initial_replace=ref["replaced"],
+                                eval_batch_size=batch)
+            ref_kind = "GA"
+        assert (res[6], kind) == (ref["is_success"], ref_kind), i
+        assert q_prod == v.query, (i, kind, q_prod, v.query, extra)
+        if res[6] == 1:
+            assert res[2] == ref["adv_code"], i
+            assert dict(res[11]) == ref["replaced"], i
+        seen.append((kind, res[6]))
+    return seen
+
+
+@pytest.mark.parametrize("task", ["gcb_clone", "gcb_authorship", "gcb_devign"])
+def test_gcb_task_attack_matches_text_oracle_cpu(task):
+    """GraphCodeBERT attackers (GraphCloneAttacker / GraphAuthorshipAttacker / GraphAttacker and
+    the gcb_* drivers) against the text oracle (oracle/graph_ref.GraphTextVictim) on a numpy
+    scorer of the packed rows: same outcomes, query counts (incl. the gcb_devign driver's extra
+    query, GraphCodeBERT/Defect-detection/code/gi_attack.py:161, and its 64-child GA),
+    adversarial code and replacements.  Labels are the scorer's own predictions."""
+    import _apmc  # noqa: F401
+    from apmc_amd.drivers import AttackArgs, _example, load_fixture
+    from apmc_amd.host import Tokenizer
+
+    base = task[4:]
+    if base == "devign":
+        codes, subs, _ = load_fixture(ROOT / "data" / "devign" / "test_subs_0_400.jsonl", 0, 40)
+        pick = [i for i in range(40) if 1 <= len(subs[i]) <= 4 and len(codes[i]) < 900][:5]
+    else:
+        codes, subs, _ = fixture(base, 6)
+        pick = list(range(6))
+    tok = Tokenizer()
+    args = AttackArgs(block_size=256, eval_batch_size=16, task=task, **GCB_ARGS)
+    probe = host_graph_victim(graph_stand_in(base), base)
+    labels = [0] * len(codes)
+    for i in pick:
+        labels[i] = int(probe.get_results([_example(tok, codes[i], 0, 256, task, args)])[1][0])
+    seen = compare_gcb(task, codes, subs, labels, 16, 8000, pick)
+    assert {o for _, o in seen} & {1, -1}, seen
