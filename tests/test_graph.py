@@ -144,3 +144,55 @@ def test_graph_clone_pairs_match_oracle(gpu, tok):
     probs, preds = model.get_results(ds, 64)
     np.testing.assert_allclose(np.asarray(probs), ref, atol=PROB_TOL, rtol=0)
     assert preds == [0 if p[0] > 0.5 else 1 for p in ref]
+
+
+# ---------------------------------------------------------------- transformers golden at L=640
+def _golden():
+    return dict(np.load(ROOT / "tests" / "golden" / "graph_golden.npz"))
+
+
+def _unpack(bits):
+    L = bits.shape[-1] * 32
+    return np.unpackbits(bits.view(np.uint8), axis=-1, bitorder="little")[..., :L].astype(bool)
+
+
+def test_golden_graph_features_are_reproduced(tok):
+    """The golden's inputs (tests/golden/make_golden_graph.py) are today's features of the same
+    fixture functions at L = 640 (code_length 512 + data_flow_length 128)."""
+    from apmc_amd.graph import convert_code_to_features, graph_mask, pack_mask
+    g = _golden()
+    funcs = _funcs(60)
+    args = types.SimpleNamespace(code_length=512, data_flow_length=128)
+    for row, i in enumerate(g["gcb_pick"]):
+        f = convert_code_to_features(funcs[i][0], tok, 0, args)
+        assert f.input_ids == g["gcb_ids"][row].tolist()
+        assert f.position_idx == g["gcb_pos"][row].tolist()
+        m = graph_mask(f.input_ids, f.position_idx, f.dfg_to_code, f.dfg_to_dfg)
+        np.testing.assert_array_equal(pack_mask(m), g["gcb_bits"][row])
+
+
+@pytest.mark.parametrize("name,seed,head,nl", [("devign", 6, "sigmoid1", 1),
+                                               ("clone", 7, "pair2", 2)])
+def test_oracle_graph_forward_matches_transformers_golden(name, seed, head, nl):
+    """oracle/graph_ref.graph_score (node averaging + roberta_cpu with the 3-D mask and explicit
+    positions) against transformers' RobertaModel(inputs_embeds, 4-D additive mask, position_ids)
+    at L = 640: pins the oracle the GPU graph tests compare the engine with."""
+    g = _golden()
+    sd = synthetic_sd(seed=seed, head=head, num_labels=nl)
+    got = graph_ref.graph_score(sd, g["gcb_ids"], _unpack(g["gcb_bits"]), g["gcb_pos"], head)
+    np.testing.assert_allclose(got, g[f"gcb_{name}_probs"], atol=1e-5, rtol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["fp32", "f32x3"])
+def test_engine_graph_forward_matches_transformers_golden(precision):
+    """ae_score_graph at L = 640 against the transformers golden (devign sigmoid and clone pair
+    heads), probabilities within 1e-4."""
+    from apmc_amd.graph import GraphModel
+    g = _golden()
+    for name, seed, head, nl, task in [("devign", 6, "sigmoid1", 1, "devign"),
+                                       ("clone", 7, "pair2", 2, "clone")]:
+        m = GraphModel(synthetic_sd(seed=seed, head=head, num_labels=nl), task=task,
+                       precision=precision)
+        got = m.score_packed(g["gcb_ids"], g["gcb_pos"], g["gcb_bits"])
+        np.testing.assert_allclose(got, g[f"gcb_{name}_probs"], atol=PROB_TOL, rtol=0)
