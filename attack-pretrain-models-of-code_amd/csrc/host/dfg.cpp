@@ -788,7 +788,12 @@ class CTree {
       size_t q = p_;
       while (q < n_ && t(q) != "{" && t(q) != ";") ++q;
       if (q < n_ && t(q) == "{") {
-        nodes[d].type = N_FUNCTION_DEFINITION;
+        // a body whose '{' is never closed (truncated Devign functions, cut between statements)
+        // does not reduce to a function_definition: tree-sitter's recovery leaves the declarator
+        // under an ERROR node, so a pointer declarator then defines every leaf of its function
+        // declarator (the function name, parameter types and names) as DFG_c does outside a
+        // definition.  A function cut inside an open '(' recovers as a definition.
+        nodes[d].type = match_[q] >= 0 || open_paren_at_eof() ? N_FUNCTION_DEFINITION : N_GENERIC;
         flush_strays(d);
         attach(d, decl);
         nodes[d].decl = decl;
@@ -812,6 +817,12 @@ class CTree {
     init_declarators(d, n_);
     if (at(";")) add_leaf(d, p_++);
     attach(parent, d);
+  }
+
+  bool open_paren_at_eof() const {
+    for (size_t i = 0; i < n_; ++i)
+      if (lv_[i].raw == "(" && match_[i] < 0) return true;
+    return false;
   }
 
   bool contains_function_declarator(int x) const {
