@@ -10,7 +10,8 @@
 //     a·w ≈ a_hi·w_hi + a_hi·w_lo + a_lo·w_hi          (3 bf16 MFMAs, f32 accumulate)
 // from ONE load of the four planes.
 //
-// gfx950 mapping:
+// Two kernels: gemm_pp_kernel (below; production for N % 256 == 0, i.e. every encoder GEMM) and
+// gemm_pk_kernel (other widths; its gfx950 mapping:)
 //   * tile 256 x BN (BN = 256: 8 waves as 2 x 4, wave tile 128 x 64; BN = 128: 4 x 2, 64 x 64),
 //     one 512-thread workgroup per CU, LDS NST x (256 + BN) x 128 B (NST = 3 stages for BN = 128,
 //     2 for BN = 256)
@@ -28,6 +29,8 @@
 //     otherwise drain it before every fragment read); raw s_barrier; XCD-aware tile order
 //   * epilogues: +bias -> f32, +bias+residual -> f32, +bias -> tanh -> f32, +bias -> GELU -> packed
 //     bf16 planes (the FFN2 operand)
+#include <type_traits>
+
 #include "common.h"
 
 
@@ -382,6 +385,383 @@ __global__ __launch_bounds__(512, 1) void gemm_pk_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Ping-pong 256 x 256 packed GEMM (gemm_pp_kernel).
+//
+// The same product over the same packed planes as gemm_pk_kernel, with the main loop built so
+// that a SIMD's matrix pipe is fed by one wave while its other wave moves data:
+//   * 8 waves = two groups of four (wave w sits on SIMD w % 4, so each SIMD holds one wave of
+//     each group); group g owns rows 128 g .. 128 g + 127 of the tile, wave (g, wn) a 128 x 64
+//     block.  Group 1 executes one extra s_barrier before the loop, so between any two barriers
+//     one group runs MFMAs while the other reads fragments and issues DMA (and vice versa).
+//   * a 128-B K-tile (NP 2: 32 k of hi | lo; NP 1: 64 k) is consumed in four phases, one
+//     64 x 32 quadrant of the wave's block each: (m-half 0, n-half 0) reading A(mh 0) and
+//     W(nh 0); (0, 1) reading W(nh 1); (1, 1) reading A(mh 1); (1, 0) reading nothing.
+//   * two 64-KiB LDS stages (K-tiles kt and kt+1).  K-tile kt+2 goes into kt's stage one
+//     quarter per phase (2 DMA pieces per wave each, issued between the wave's own MFMAs of the
+//     phase, where their issue cost hides), every quarter >= 2 phases after its last
+//     LDS read: A(mh 0) at phase 2 and W(nh 0) at phase 3 of kt, W(nh 1) at phase 0 and A(mh 1)
+//     at phase 1 of kt+1.  Each quarter is waited for (counted vmcnt(6), never 0 in steady
+//     state) one phase before the phase that reads it, so a barrier separates every issuer's
+//     wait from the read — what the staggered groups need.  (A deeper ring — 10 quarter slots
+//     in 160 KiB, quarters DMA'd 8 phases ahead — measured 3-7 % slower: DMA latency is not
+//     what bounds this loop; nor do two phases per K-tile (half the barriers) help.)
+//   * measured (tools/gemm_bench.py, DIAG 7 = the same MFMAs with no barrier, read or DMA):
+//     the matrix pipe alone sustains ~1.86 GHz-equivalent under this load (spec peak assumes
+//     2.4 GHz); the full main loop runs at 84-87 % of that MFMA-only time.
+//   * the MFMA computes the transposed product D^T = W·A^T, so lane l holds 4 consecutive
+//     output columns of output row l % 32 per register quad.  The epilogue writes them (after
+//     bias / GELU / plane split) into the free LDS as the output's own byte image, one 64-row
+//     half of the wave's block at a time, then copies whole 256-B row segments out with 16-B
+//     lanes (+ residual / tanh on the coalesced side).
+namespace {
+template <int N>
+__device__ __forceinline__ void pp_wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else static_assert(N == 0, "unsupported vmcnt");
+}
+}  // namespace
+
+// DIAG (timing experiments only, through ae_bench_gemm_packed; results WRONG): 1 = no DMA after
+// the prologue, 2 = no MFMAs, 3 = no fragment reads after K-tile 0, 4 = no epilogue, 5 = no
+// vmcnt waits in the loop, 6 = MFMAs + barriers only (no DMA / reads / waits after K-tile 0),
+// 7 = MFMAs only (6 without barriers).  Production instantiations have DIAG = 0.
+template <int NP, int EPI, int DIAG>
+__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
+    const __bf16* __restrict__ A, const __bf16* __restrict__ W, const float* __restrict__ bias,
+    const float* __restrict__ R, float* __restrict__ C, __bf16* __restrict__ Cp, int M, int N,
+    int K, int group_m) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char pk_smem[];
+  constexpr int BM = 256, BN = 256, ROWB = PK_ROWB;
+  constexpr int A_BYTES = BM * ROWB, STAGE = (BM + BN) * ROWB;  // 64 KiB per K-tile
+  constexpr int KB = 64 / NP;                                     // k per K-tile
+  constexpr int NS = KB / 16;                                     // 16-deep MFMA steps
+  constexpr int T = NP == 2 ? 3 : 1;                              // MFMAs per product
+
+  const int tiles_n = (N + BN - 1) / BN;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int per_group = group_m * tiles_n;
+  const int g = t / per_group, first_m = g * group_m;
+  const int gsize = min(tiles_m - first_m, group_m);
+  const int tm0 = first_m + (t - g * per_group) % gsize, tn0 = (t - g * per_group) / gsize;
+  const int m0 = tm0 * BM, n0 = tn0 * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;  // group = wm
+  const int li = lane & 31, lh = lane >> 5;
+  const size_t lda = (size_t)NP * K;
+
+  // ---- DMA pieces (8 rows x 128 B each): per K-tile every wave issues 8, as 4 quarters:
+  // [0,1] A(mh 0) rows {0..63, 128..191}, [2,3] W(nh 0) rows {64 q + 0..31},
+  // [4,5] W(nh 1) rows {64 q + 32..63}, [6,7] A(mh 1) rows {64..127, 192..255}
+  const char* src[8];
+  uint32_t dst[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int pidx = 2 * wave + (j & 1);  // 0..15 within the quarter
+    const bool is_a = j < 2 || j >= 6;
+    const int r0 = is_a ? (pidx >> 3) * 128 + (pidx & 7) * 8 + (j >= 6 ? 64 : 0)
+                        : (pidx >> 2) * 64 + (pidx & 3) * 8 + (j >= 4 ? 32 : 0);
+    const int r = r0 + (lane >> 3);
+    const int cs = (lane & 7) ^ ((r >> 1) & 7);
+    if (is_a) {
+      const int gr = m0 + r < M ? m0 + r : M - 1;
+      src[j] = reinterpret_cast<const char*>(A + gr * lda) + 16 * cs;
+      dst[j] = r0 * ROWB;
+    } else {
+      const int gr = n0 + r < N ? n0 + r : N - 1;
+      src[j] = reinterpret_cast<const char*>(W + gr * lda) + 16 * cs;
+      dst[j] = A_BYTES + r0 * ROWB;
+    }
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)pk_smem;
+  const int nk = K / KB;
+  auto issue = [&](int q, int kt) {  // quarter q (pieces 2q, 2q+1) of K-tile kt
+    dma16(src[2 * q] + (size_t)kt * ROWB, lds0 + (kt & 1) * STAGE + dst[2 * q]);
+    dma16(src[2 * q + 1] + (size_t)kt * ROWB, lds0 + (kt & 1) * STAGE + dst[2 * q + 1]);
+  };
+
+
+  floatx16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  const int sw = (li >> 1) & 7;  // fragment rows are 32-aligned + li
+  const int a_row = (wm * 128 + li) * ROWB;
+  const int w_row = A_BYTES + (wn * 64 + li) * ROWB;
+  bf16x8 fa[2][NS][NP];   // A fragments of the current m-half: [tm in half][step][plane]
+  bf16x8 fw[2][NS][NP];   // W fragments: [n-half][step][plane]
+
+  auto read_a = [&](const unsigned char* st, int mh, int kt) {
+    if ((DIAG == 3 || DIAG >= 6) && kt > 0) return;
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+          fa[tt][s][p] = *reinterpret_cast<const bf16x8*>(
+              st + a_row + (2 * mh + tt) * 32 * ROWB + 16 * ((4 * p + 2 * s + lh) ^ sw));
+  };
+  auto read_w = [&](const unsigned char* st, int nh, int kt) {
+    if ((DIAG == 3 || DIAG >= 6) && kt > 0) return;
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+        fw[nh][s][p] = *reinterpret_cast<const bf16x8*>(
+            st + w_row + nh * 32 * ROWB + 16 * ((4 * p + 2 * s + lh) ^ sw));
+  };
+  // a quadrant's MFMAs; DMA quarter q of K-tile kd (if dma) rides in the MFMA issue gaps —
+  // one piece after each third of the MFMAs — instead of in the load section (measured: the
+  // glds issue cost then hides behind the matrix pipe; in the load section it serialises)
+  auto mfma_quad = [&](int mh, int nh, auto qc, bool dma, int kd) {
+    constexpr int q = decltype(qc)::value;
+    constexpr int NM = NS * 2 * T;  // MFMAs of the quadrant
+    if (DIAG == 2) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          asm volatile("" ::"v"(fw[nh][s][p]));
+#pragma unroll
+          for (int tt = 0; tt < 2; ++tt) asm volatile("" ::"v"(fa[tt][s][p]));
+        }
+      if (dma) issue(q, kd);
+      return;
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+      const int s = i / (2 * T), tt = (i / T) % 2, term = i % T;
+      floatx16& c = acc[2 * mh + tt][nh];
+      const bf16x8& x = (T == 3 && term == 1) ? fw[nh][s][NP - 1] : fw[nh][s][0];
+      const bf16x8& y = (T == 3 && term == 0) ? fa[tt][s][NP - 1] : fa[tt][s][0];
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, c, 0, 0, 0);
+      if (DIAG != 1 && DIAG < 6 && dma && (i == NM / 3 - 1 || i == 2 * NM / 3 - 1)) {
+        const int j = 2 * q + (i == NM / 3 - 1 ? 0 : 1);
+        __builtin_amdgcn_sched_barrier(0);
+        dma16(src[j] + (size_t)kd * ROWB, lds0 + (kd & 1) * STAGE + dst[j]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // end of a load section: the fragment reads retire before the MFMAs that use them
+  auto sync_compute = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    if (DIAG != 7) __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto sync_load = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    if (DIAG != 7) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue: K-tile 0 whole and K-tile 1's first two quarters (the loop issues the rest)
+  if (nk > 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) issue(q, 0);
+  }
+  if (nk > 1) {
+    issue(0, 1);
+    issue(1, 1);
+    pp_wait_vm<8>();  // K-tile 0's A(mh 0) + W(nh 0) landed (this wave's pieces)
+  } else {
+    pp_wait_vm<0>();
+  }
+  if (DIAG == 1 || DIAG >= 6) pp_wait_vm<0>();
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) sync_load();  // group 1 runs one phase behind
+
+  auto wait6 = [&](bool full) {
+    if (DIAG == 5 || DIAG == 1 || DIAG >= 6) return;
+    if (full) pp_wait_vm<6>();
+    else pp_wait_vm<0>();
+  };
+  for (int kt = 0; kt < nk; ++kt) {
+    const unsigned char* st = pk_smem + (kt & 1) * STAGE;
+    const bool next1 = kt + 1 < nk, next2 = kt + 2 < nk;
+    // phase 0: quadrant (0, 0); wait for W(nh 1) of kt; W(nh 1) of kt+1 into its stage
+    wait6(next1);
+    read_a(st, 0, kt);
+    read_w(st, 0, kt);
+    sync_compute();
+    mfma_quad(0, 0, std::integral_constant<int, 2>(), next1, kt + 1);
+    sync_load();
+    // phase 1: quadrant (0, 1); wait for A(mh 1) of kt; A(mh 1) of kt+1 into its stage
+    wait6(next1);
+    read_w(st, 1, kt);
+    sync_compute();
+    mfma_quad(0, 1, std::integral_constant<int, 3>(), next1, kt + 1);
+    sync_load();
+    // phase 2: quadrant (1, 1); A(mh 0) of kt+2 into kt's stage
+    read_a(st, 1, kt);
+    sync_compute();
+    mfma_quad(1, 1, std::integral_constant<int, 0>(), next2, kt + 2);
+    sync_load();
+    // phase 3: quadrant (1, 0); wait for A(mh 0) + W(nh 0) of kt+1; W(nh 0) of kt+2
+    wait6(next2);
+    sync_compute();
+    mfma_quad(1, 0, std::integral_constant<int, 1>(), next2, kt + 2);
+    sync_load();
+  }
+  if (DIAG != 0) pp_wait_vm<0>();
+  if (wm == 0) sync_load();
+  if (DIAG == 7) __builtin_amdgcn_s_barrier();  // same barrier count in both groups; every LDS read and DMA done
+  if (DIAG == 4) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) keep_f32(acc[a][b][r]);
+    return;
+  }
+
+  // ---- epilogue.  acc[tm][tn] register 4 j + i of lane l = output row wm*128 + tm*32 + (l & 31),
+  // column wn*64 + tn*32 + 8 j + 4 (l >> 5) + i.  Per 64-row half (tm pair), the wave writes its
+  // 64 x 64 block into its own 16-KiB LDS region in the output's byte image — f32 rows of 256 B,
+  // or packed rows (NP 2: two 128-B [hi 32 | lo 32] blocks; NP 1: 128 B of hi) — with the 16-B
+  // chunk index XOR-ed by (row & 15) (conflict-free 16-row groups), then stores it with 16-B
+  // lanes, whole row segments per instruction.
+  constexpr int RB = EPI == PK_EPI_GELU_PACKED ? 64 * 2 * NP : 256;  // bytes of a row segment
+  constexpr int CPR = RB / 16;                                       // 16-B chunks per row
+  unsigned char* reg = pk_smem + wave * 16384;
+  const int cb0 = n0 + wn * 64;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int lr = tt * 32 + li;  // row within the half
+#pragma unroll
+      for (int tn = 0; tn < 2; ++tn) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const floatx16& c = acc[2 * half + tt][tn];
+          const int cc = tn * 32 + 8 * j + 4 * lh;  // column within the wave's 64
+          if (EPI == PK_EPI_GELU_PACKED) {
+            const int col = cb0 + cc < N ? cb0 + cc : N - 4;
+            const floatx4 bv = *reinterpret_cast<const floatx4*>(bias + col);
+            ushortx4 h, l;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float y = gelu_erfc_fast(c[4 * j + i] + bv[i]);
+              const __bf16 hv = (__bf16)y;
+              h[i] = __builtin_bit_cast(unsigned short, hv);
+              l[i] = f2bf(y - (float)hv);
+            }
+            // byte of column cc's hi in the packed row: block tn, element 8 j + 4 lh
+            const int hb = tn * 64 * NP + 2 * (8 * j + 4 * lh);
+            const int ch = ((hb >> 4) ^ (lr & 15)) & (CPR - 1);
+            *reinterpret_cast<ushortx4*>(reg + lr * RB + ch * 16 + (hb & 15)) = h;
+            if (NP == 2) {
+              const int lb = hb + 64;
+              const int cl = ((lb >> 4) ^ (lr & 15)) & (CPR - 1);
+              *reinterpret_cast<ushortx4*>(reg + lr * RB + cl * 16 + (lb & 15)) = l;
+            }
+          } else {
+            floatx4 v;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = c[4 * j + i];
+            const int ch = (cc >> 2) ^ (lr & 15);
+            *reinterpret_cast<floatx4*>(reg + lr * RB + ch * 16) = v;
+          }
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own region: no barrier
+    constexpr int RPI = 64 / CPR;  // rows per store instruction
+#pragma unroll
+    for (int k = 0; k < 64 / RPI; ++k) {
+      const int lr = k * RPI + lane / CPR, c = lane % CPR;
+      const int row = m0 + wm * 128 + half * 64 + lr;
+      const bool ok = row < M;
+      const uint4 v = *reinterpret_cast<const uint4*>(reg + lr * RB + ((c ^ (lr & 15)) & (CPR - 1)) * 16);
+      if (EPI == PK_EPI_GELU_PACKED) {
+        // 16 B of the packed row: column block (c*16 / (64 NP)), all within the wave's 64 columns
+        const int col = cb0 + (c * 16) / (2 * NP);  // first column this chunk belongs to (>= block start)
+        if (ok && col < N) {
+          __bf16* dstp = Cp + (size_t)row * NP * N + (size_t)(cb0 >> 5) * 32 * NP + c * 8;
+          *reinterpret_cast<uint4*>(dstp) = v;
+        }
+      } else {
+        const int col = cb0 + 4 * c;
+        if (ok && col < N) {
+          const size_t o = (size_t)row * N + col;
+          floatx4 f = __builtin_bit_cast(floatx4, v);
+          f += *reinterpret_cast<const floatx4*>(bias + col);
+          if (EPI == PK_EPI_TANH)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) f[i] = tanhf(f[i]);
+          if (EPI == PK_EPI_RES) f += *reinterpret_cast<const floatx4*>(R + o);
+          *reinterpret_cast<floatx4*>(C + o) = f;
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // region reads done before it is rewritten
+  }
+}
+
+namespace {
+template <int NP, int EPI, int DIAG>
+hipError_t pp_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R, float* C,
+                     __bf16* Cp, int M, int N, int K, int group_m, hipStream_t st) {
+  constexpr int lds = 2 * (256 + 256) * PK_ROWB;  // 128 KiB
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_pp_kernel<NP, EPI, DIAG>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  hipLaunchKernelGGL((gemm_pp_kernel<NP, EPI, DIAG>), dim3(tiles), dim3(512), lds, st, A, W, bias,
+                     R, C, Cp, M, N, K, group_m);
+  return hipGetLastError();
+}
+
+template <int NP, int DIAG>
+hipError_t pp_epi(int epi, const __bf16* A, const __bf16* W, const float* bias, const float* R,
+                  float* C, __bf16* Cp, int M, int N, int K, int group_m, hipStream_t st) {
+  if constexpr (DIAG != 0) {  // diagnostic builds: split-bf16, bias / GELU epilogues only
+    if (NP != 2 || (epi != PK_EPI_BIAS && epi != PK_EPI_GELU_PACKED)) return hipErrorInvalidValue;
+    if (epi == PK_EPI_BIAS)
+      return pp_launch<2, PK_EPI_BIAS, DIAG>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
+    return pp_launch<2, PK_EPI_GELU_PACKED, DIAG>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
+  }
+  switch (epi) {
+    case PK_EPI_BIAS:
+      return pp_launch<NP, PK_EPI_BIAS, 0>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
+    case PK_EPI_GELU_PACKED:
+      return pp_launch<NP, PK_EPI_GELU_PACKED, 0>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
+    case PK_EPI_RES:
+      return pp_launch<NP, PK_EPI_RES, 0>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
+    default: return pp_launch<NP, PK_EPI_TANH, 0>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
+  }
+}
+
+template <int DIAG>
+hipError_t pp_dispatch(const unsigned short* A, const unsigned short* W, const float* bias,
+                       const float* R, float* C, unsigned short* Cp, int M, int N, int K, int epi,
+                       int np, int group_m, hipStream_t st) {
+  auto bf = [](const unsigned short* p) { return reinterpret_cast<const __bf16*>(p); };
+  __bf16* cp = reinterpret_cast<__bf16*>(Cp);
+  if (np == 2) return pp_epi<2, DIAG>(epi, bf(A), bf(W), bias, R, C, cp, M, N, K, group_m, st);
+  return pp_epi<1, DIAG>(epi, bf(A), bf(W), bias, R, C, cp, M, N, K, group_m, st);
+}
+}  // namespace
+
 namespace {
 constexpr int PK_GROUP_M = 4;  // grouped tile order: 4 > 8 > 16 > 32 M-tiles by A/B (round 1)
 
@@ -456,6 +836,9 @@ extern "C" hipError_t ae_launch_gemm_packed(const unsigned short* A, const unsig
                                             int np, hipStream_t st) {
   if (M <= 0) return hipSuccess;
   if (!pk_shape_ok(M, N, K, np)) return hipErrorInvalidValue;
+  // the ping-pong 256 x 256 kernel for every width it tiles exactly (all encoder GEMMs: 768,
+  // 2304, 3072 — for N = 768 its 1.5 rounds of 256^2 tiles still beat 3 rounds of 256 x 128)
+  if (N % 256 == 0) return pp_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
   return pk_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, pick_bn(M, N), st);
 }
 
@@ -467,7 +850,21 @@ extern "C" hipError_t ae_bench_gemm_packed(const unsigned short* A, const unsign
                                            unsigned short* Cp, int M, int N, int K, int epi,
                                            int np, int bn, int diag, hipStream_t st) {
   if (M <= 0) return hipSuccess;
-  if (!pk_shape_ok(M, N, K, np) || (bn != 0 && bn != 128 && bn != 256)) return hipErrorInvalidValue;
+  if (!pk_shape_ok(M, N, K, np) || (bn != 0 && bn != 128 && bn != 256 && bn != 512))
+    return hipErrorInvalidValue;
+  if (bn == 512) {  // the ping-pong 256 x 256 kernel
+    switch (diag) {
+      case 0: return pp_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
+      case 1: return pp_dispatch<1>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
+      case 2: return pp_dispatch<2>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
+      case 3: return pp_dispatch<3>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
+      case 4: return pp_dispatch<4>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
+      case 5: return pp_dispatch<5>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
+      case 6: return pp_dispatch<6>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
+      case 7: return pp_dispatch<7>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
+      default: return hipErrorInvalidValue;
+    }
+  }
   if (bn == 0) bn = pick_bn(M, N);
   switch (diag) {
     case 0: return pk_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, bn, st);

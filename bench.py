@@ -18,7 +18,8 @@ before the timed region); `cpu_baseline` is oracle/roberta_cpu.py (PyTorch-CPU f
 restatement of the reference's scoring) on the host cores this job may use.  Sub-objects: the
 exact-fp32 mode of the same step (`fp32_mode`), the end-to-end config-2 GA attack over all of
 test_subs_0_400 (`attack`), config 1 (greedy, 16 functions) on GPU and CPU (`config1`), masked-LM
-substitute generation (`substitutes`) and the MHM-NS baseline (`mhm`).
+substitute generation (`substitutes`), the MHM-NS baseline (`mhm`) and config 5 (`authorship`:
+CodeBERT GA vs MHM-NS, GraphCodeBERT GA).
 """
 import argparse
 import glob
@@ -37,6 +38,7 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32-input MFMA dense peak
 BF16_MFMA_PEAK_TFLOPS = 2516.6  # dense bf16 (spec, no sparsity)
 METRIC = "victim queries/sec + attacked examples/min (node), CodeBERT Devign GA attack"
 FIXTURE = ROOT / "data" / "devign" / "test_subs_0_400.jsonl"
+AA_FIXTURE = ROOT / "data" / "authorship" / "valid_subs.jsonl"
 # attack-sensitive synthetic victim (the attack parity tests' weights): a larger classifier
 # out_proj spreads probabilities so that substitutions can flip predictions
 VICTIM_SEED, VICTIM_OUT_STD = 5, 8.0
@@ -67,6 +69,10 @@ def parse_args():
                     help="examples of the batched MHM-NS leg (config 5 baseline; 0 disables)")
     ap.add_argument("--mhm-seq-examples", type=int, default=4,
                     help="examples of the sequential MHM-NS comparison run")
+    ap.add_argument("--aa-examples", type=int, default=132,
+                    help="authorship programs of the config-5 leg (GA vs MHM-NS; 0 disables)")
+    ap.add_argument("--aa-gcb-examples", type=int, default=32,
+                    help="of them, attacked by GA on the GraphCodeBERT victim too (0 disables)")
     ap.add_argument("--no-fp32-mode", action="store_true")
     return ap.parse_args()
 
@@ -380,6 +386,95 @@ def mhm_leg(dev, n_examples, seq_examples, rank, world, precision):
     return res
 
 
+def _gather_sum_max(vals, dev, world, nsum):
+    """all-gather one float64 vector per rank; sum the first nsum entries, max the rest."""
+    import numpy as np
+    import torch
+    v = np.asarray(vals, dtype=np.float64)
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor(v, device=dev)
+        g = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(g, t)
+        allv = torch.stack(g).cpu().numpy()
+    else:
+        allv = v[None]
+    return np.concatenate([allv[:, :nsum].sum(0), allv[:, nsum:].max(0)])
+
+
+def aa_leg(dev, n_examples, n_gcb, rank, world, precision):
+    """Config 5 (Authorship-Attribution, 66 classes): the ALERT greedy->GA attack
+    (CodeXGLUE/Authorship-Attribution/code/attack.py: block 512, eval_batch_size 32) against the
+    MHM-NS sampling baseline (mhm.py: n_candi 30, max_iter 100, eval_batch_size 64) on the same
+    CodeBERT victim and programs of valid_subs.jsonl, then the GraphCodeBERT victim's GA
+    (GraphCodeBERT/Authorship-Attribution, code_length 512 + data_flow_length 128) on the first
+    n_gcb programs.  Synthetic victims (seed 5, out_proj std 8) do not know the authors, so each
+    program's label is the victim's own prediction (every program is attacked)."""
+    from apmc_amd.dist import DynamicQueue, call_key
+    from apmc_amd.drivers import AttackArgs, _example, load_fixture, run_gi_attack_batched, \
+        run_mhm_attack
+    from apmc_amd.graph import GraphModel
+    from apmc_amd.host import Tokenizer
+    from apmc_amd.model import Model
+    from apmc_amd.weights import synthetic_state_dict
+
+    codes, subs, _ = load_fixture(AA_FIXTURE, 0, n_examples)
+    tok = Tokenizer()
+    sd = synthetic_state_dict(seed=VICTIM_SEED, head="softmaxN", num_labels=66,
+                              out_std=VICTIM_OUT_STD)
+    model = Model(sd, task="authorship", precision=precision, device=dev.index)
+    labels = [int(p) for p in model.get_results(
+        [_example(tok, c, 0, 512, "authorship") for c in codes])[1]]
+    res = {"workload": f"Authorship-Attribution valid_subs.jsonl programs [0, {len(codes)}), "
+                       "66-way CodeBERT victim (synthetic, labels = its own predictions)",
+           "precision": precision}
+
+    def summary(vals, examples_key="examples"):
+        ex, cnt, suc, q, wall = vals
+        return {"examples": int(ex), "attacked": int(cnt), "successes": int(suc),
+                "success_rate": round(suc / cnt, 4) if cnt else None,
+                "victim_queries": int(q), "wall_s": round(wall, 2),
+                "victim_queries_per_s": round(q / wall, 1) if wall else None,
+                "attacked_examples_per_min": round(60 * ex / wall, 2) if wall else None}
+
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    args = AttackArgs(block_size=512, eval_batch_size=32, seed=123456, rng="per_example",
+                      task="authorship")
+    queue = DynamicQueue(len(codes), key=call_key("bench_aa_ga_queue"))
+    out = run_gi_attack_batched(model, codes, subs, labels, args, queue=queue, max_inflight=64)
+    res["ga"] = summary(_gather_sum_max([out["examples"], out["total_cnt"], out["success"],
+                                         out["queries"], out["wall_s"]], dev, world, 4))
+    res["ga"]["mode"] = "greedy -> GA (attack.py), cross-example batched"
+    margs = AttackArgs(block_size=512, eval_batch_size=64, seed=123456, task="authorship")
+    mine = list(range(rank, len(codes), world))
+    out = run_mhm_attack(model, codes, subs, labels, margs, indices=mine, max_iter=100,
+                         prob_threshold=1, max_inflight=max(1, len(mine)))
+    res["mhm"] = summary(_gather_sum_max([out["examples"], out["total_cnt"], out["success"],
+                                          out["queries"], out["wall_s"]], dev, world, 4))
+    res["mhm"]["mode"] = "MHM-NS (mhm.py), cross-example batched chains"
+    model.engine.close()
+    if n_gcb > 0:
+        gargs = AttackArgs(block_size=512, eval_batch_size=32, seed=123456, rng="per_example",
+                           task="gcb_authorship", code_length=512, data_flow_length=128)
+        gmodel = GraphModel(sd, task="authorship", args=gargs, precision=precision,
+                            device=dev.index)
+        gcodes, gsubs = codes[:n_gcb], subs[:n_gcb]
+        glabels = [int(gmodel.get_results([_example(tok, c, 0, 512, "gcb_authorship", gargs)])[1][0])
+                   for c in gcodes]
+        queue = DynamicQueue(len(gcodes), key=call_key("bench_aa_gcb_queue"))
+        out = run_gi_attack_batched(gmodel, gcodes, gsubs, glabels, gargs, queue=queue,
+                                    max_inflight=64)
+        res["gcb_ga"] = summary(_gather_sum_max([out["examples"], out["total_cnt"],
+                                                 out["success"], out["queries"], out["wall_s"]],
+                                                dev, world, 4))
+        res["gcb_ga"]["mode"] = ("GraphCodeBERT victim, greedy -> GA (GraphAuthorshipAttacker), "
+                                 f"programs [0, {len(gcodes)}), L = 640 with the data-flow mask")
+        gmodel.engine.close()
+    return res
+
+
 def subs_leg(dev, seconds, rank, world, precision):
     """Config-3 workload: masked-LM substitute generation (get_substitutes.py) over the Devign
     fixture functions in order (12-layer codebert-shaped MLM, synthetic weights), items pulled
@@ -540,8 +635,8 @@ def main():
         "roofline": {
             "bound": "mfma",
             "kernel": {"fp32": "gemm_f32_nt_kernel<EPI_BIAS_GELU>",
-                       "f32x3": "gemm_pk_kernel<256, 2, EPI_GELU_PACKED>",
-                       "bf16": "gemm_pk_kernel<256, 1, EPI_GELU_PACKED>"}[args.precision]
+                       "f32x3": "gemm_pp_kernel<2, EPI_GELU_PACKED>",
+                       "bf16": "gemm_pp_kernel<1, EPI_GELU_PACKED>"}[args.precision]
                       + " (FFN1 [T,768]x[768,3072])",
             "achieved": round(achieved, 3) if achieved else None,
             "peak": peak,
@@ -568,6 +663,9 @@ def main():
                                      0 if args.no_cpu_baseline else args.cpu_e2e_seconds)
     if args.subs_seconds > 0:
         res["substitutes"] = subs_leg(dev, args.subs_seconds, rank, world, args.precision)
+    if args.aa_examples > 0:
+        res["authorship"] = aa_leg(dev, args.aa_examples, args.aa_gcb_examples, rank, world,
+                                   args.precision)
     if args.mhm_examples > 0:
         res["mhm"] = mhm_leg(dev, args.mhm_examples, args.mhm_seq_examples, rank, world,
                              args.precision)

@@ -3,7 +3,8 @@ lib/libalert_engine.so (not part of the public C-ABI; the engine tests cover the
 
 Packed-plane GEMM (gemm_planes.hip): C = A·W^T over packed bf16 planes must equal the float64 sum
 of the split products A_hi·W_hi + A_hi·W_lo + A_lo·W_hi (f32 accumulation: |Δ| ≤ 1e-5·Σ|a||w|), for
-ragged M, both tile widths, both plane counts and every epilogue."""
+ragged M, both tile widths, the ping-pong 256 x 256 kernel, both plane counts and every
+epilogue."""
 import ctypes
 
 import numpy as np
@@ -58,6 +59,14 @@ def _p(t):
     (1000, 384, 64, 1, 3, "128"),
     (700, 256, 256, 1, 1, "256"),
     (64, 2304, 768, 2, 0, ""),
+    # ping-pong 256 x 256 kernel (tile code 512): ragged M / N, one- and two-K-tile loops
+    (300, 256, 128, 2, 0, "512"),
+    (512, 768, 768, 2, 2, "512"),
+    (257, 512, 192, 2, 1, "512"),
+    (1000, 384, 64, 1, 3, "512"),
+    (700, 256, 256, 1, 1, "512"),
+    (64, 2304, 768, 2, 3, "512"),
+    (600, 3072, 768, 2, 1, "512"),
 ])
 def test_gemm_packed_matches_split_products(gpu, M, N, K, np_, epi, bn):
     lib = _lib()
