@@ -15,6 +15,9 @@ Per example (one `item` of the jsonl):
      product of the first 4 candidates of the first 12 rows (<= 24 rows), score each by masked-LM
      perplexity (ae_mlm_nll) and sort ascending (utils.py:209-248);
   5. the union, minus names already in the function and invalid names, is the entry.
+GraphCodeBERT's variant (cosine=False; GraphCodeBERT/Defect-detection/preprocess/get_substitutes.py
+:72-134, where the cosine block is commented out) skips step 3: all 60 candidates of every
+occurrence go straight to step 4 (no re-encodes).
 Every reference call of the MLM is made without attention_mask, so every call here uses the
 attend-pad form.  The per-item output (`item["substitutes"]`) has the reference's schema; list order
 inside an entry follows Python set iteration in the reference and is not reproduced (compare as
@@ -36,14 +39,16 @@ K_TOP = 60  # get_substitutes.py:63
 
 
 class SubstituteGenerator:
-    """`engine` is an Engine built with_mlm=True (head "none" is enough)."""
+    """`engine` is an Engine built with_mlm=True (head "none" is enough).  cosine=False is the
+    GraphCodeBERT preprocessing (no naturalness re-encode: every top-60 candidate is kept)."""
 
     def __init__(self, engine, tokenizer: Tokenizer | None = None, block_size: int = 512,
-                 lang: str = "c"):
+                 lang: str = "c", cosine: bool = True):
         self.engine = engine
         self.tok = tokenizer or Tokenizer()
         self.block_size = block_size
         self.lang = lang
+        self.cosine = cosine
         self.tokens_per_call = 1 << 18  # candidate tokens per re-encode call (workspace bound)
         self.stats = {"examples": 0, "occurrences": 0, "encoded_seqs": 0, "encoded_tokens": 0,
                       "bpe_batches": 0, "encoder_flop": 0.0}
@@ -107,7 +112,8 @@ class SubstituteGenerator:
         # rows 1 .. L-1 (word_predictions[1:len(sub_words)+1], get_substitutes.py:66-67)
         preds = preds[1:].cpu().numpy()
         n_pred = preds.shape[0]
-        orig = self.engine.encode(ids_dev[None], np.array([L], np.int32), attend_pad=True)[0]
+        orig = (self.engine.encode(ids_dev[None], np.array([L], np.int32), attend_pad=True)[0]
+                if self.cosine else None)
         if trace is not None:
             trace["ids"] = ids_np.copy()
             trace["topk_ids"] = preds.copy()
@@ -129,7 +135,7 @@ class SubstituteGenerator:
         # independent, so batching changes nothing but float rounding); one host sync per chunk
         per_call = max(1, min(16, self.tokens_per_call // (K_TOP * L)))
         sims_of = {}
-        for c0 in range(0, len(occ), per_call):
+        for c0 in range(0, len(occ) if self.cosine else 0, per_call):
             chunk = occ[c0:c0 + per_call]
             r_lo = min(k0 for _, _, k0, _ in chunk) + 1
             r_hi = max(k1e for _, _, _, k1e in chunk) + 1
@@ -154,8 +160,12 @@ class SubstituteGenerator:
         all_subs: dict[str, list[str]] = {}
         for o in occ:
             tgt_word, one_pos, k0, k1e = o
-            sims = sims_of[o]
             cand_ids = preds[k0:k1e]  # [span, 60]
+            if not self.cosine:  # GraphCodeBERT: get_substitues on all 60 candidates
+                self.stats["occurrences"] += 1
+                all_subs.setdefault(tgt_word, []).extend(self._words(cand_ids, trace))
+                continue
+            sims = sims_of[o]
             if trace is not None:
                 trace["sims"].append((tgt_word, one_pos, [float(v) for v in sims],
                                       [tuple(int(x) for x in c) for c in cand_ids.T]))

@@ -95,9 +95,11 @@ def get_substitues(substitutes, tokenizer, sd, layers, use_bpe, substitutes_scor
 
 @torch.no_grad()
 def substitutes_for_example(sd, tokenizer, code_tokens, variable_names, is_valid, block_size=512,
-                            layers=12, trace=None):
+                            layers=12, trace=None, cosine=True):
     """get_substitutes.py:54-137 for one item; returns the `substitutes` dict (lists in set
-    order).  is_valid(name) -> bool is is_valid_variable_name(name, 'c')."""
+    order).  is_valid(name) -> bool is is_valid_variable_name(name, 'c').  cosine=False restates
+    GraphCodeBERT/Defect-detection/preprocess/get_substitutes.py:72-134 (cosine block commented
+    out: get_substitues over all 60 candidates, use_bpe 1, threshold 0)."""
     processed_code = " ".join(code_tokens)
     words, sub_words, keys = _tokenize(processed_code, tokenizer)
     sub_words = [tokenizer.cls_token] + sub_words[:block_size - 2] + [tokenizer.sep_token]
@@ -126,6 +128,10 @@ def substitutes_for_example(sd, tokenizer, code_tokens, variable_names, is_valid
                 continue
             substitutes = word_predictions[k0:k1]
             word_pred_scores = word_pred_scores_all[k0:k1]
+            if not cosine:
+                all_substitues += get_substitues(substitutes, tokenizer, sd, layers, 1,
+                                                 word_pred_scores, 0, trace)
+                continue
             orig_word_embed = orig_embeddings[0][k0 + 1:k1 + 1]
             subwords_leng, nums_candis = substitutes.size()
             new_ids = input_ids_.repeat(nums_candis, 1)

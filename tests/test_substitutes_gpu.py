@@ -123,3 +123,55 @@ def test_substitutes_match_oracle_on_fixture_functions(setup):
             compared += 1
             assert set(got.get(word, [])) == set(exp.get(word, [])), word
     assert compared >= 8 and excused <= compared // 4, (compared, excused)
+
+
+def test_gcb_no_cosine_substitutes_match_oracle_12_layers(gpu):
+    """GraphCodeBERT's preprocessing variant (cosine=False: GraphCodeBERT/Defect-detection/
+    preprocess/get_substitutes.py:72-134 — every top-60 candidate goes to get_substitues, no
+    naturalness re-encode) on the full 12-layer codebert-shaped MLM and functions up to 400
+    sub-words.  Exact sets, except words whose span has a near tie at a rank the outcome reads
+    (60th/61st logit of any row; 4th/5th of the rows get_bpe_substitues takes)."""
+    from apmc_amd.attacker import get_identifiers
+    from apmc_amd.engine import Engine
+    from apmc_amd.host import Tokenizer, remove_comments
+    from apmc_amd.substitutes import SubstituteGenerator
+    from apmc_amd.utils import _tokenize, get_identifier_posistions_from_code, \
+        is_valid_variable_name
+    from apmc_amd.weights import synthetic_state_dict
+    from oracle import featurize_ref as fref
+    from oracle import substitutes_ref as sref
+
+    sd = synthetic_state_dict(seed=4, head="none", with_mlm=True)
+    eng = Engine(sd, head="none", with_mlm=True, precision="fp32")
+    tok = Tokenizer()
+    gen = SubstituteGenerator(eng, tok, block_size=512, cosine=False)
+    rtok = fref.tokenizer()
+    compared = excused = 0
+    for js in _items(6, 400):
+        idents, code_tokens = get_identifiers(remove_comments(js["func"]), "c")
+        names = [i[0] for i in idents if " " not in i[0].strip()]
+        tr_g, tr_o = {}, {}
+        got = gen.generate_from_tokens(code_tokens, names, trace=tr_g)
+        exp = sref.substitutes_for_example(sd, rtok, code_tokens, names,
+                                           lambda s: is_valid_variable_name(s, "c"),
+                                           block_size=512, layers=12, trace=tr_o, cosine=False)
+        assert (tr_g["ids"] == tr_o["ids"]).all()
+        top61 = torch.topk(tr_o["logits"], 61, -1).values.numpy()[1:]
+        tied = set(np.nonzero(top61[:, 59] - top61[:, 60] < LOGIT_TIE)[0].tolist())
+        tied4 = set(np.nonzero(top61[:, 3] - top61[:, 4] < LOGIT_TIE)[0].tolist())
+        words, _, keys = _tokenize(" ".join(code_tokens), tok)
+        bad = set()
+        for word, poss in get_identifier_posistions_from_code(words, names).items():
+            for p in poss:
+                k0, k1 = keys[p]
+                rows = set(range(k0, k1))
+                if rows & tied or (k1 - k0 > 1 and rows & tied4):
+                    bad.add(word)
+        for word in set(got) | set(exp):
+            if word in bad:
+                excused += 1
+                continue
+            compared += 1
+            assert set(got.get(word, [])) == set(exp.get(word, [])), word
+    assert compared >= 10 and excused <= compared // 4, (compared, excused)
+    eng.close()

@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--index", nargs="+", default=["0", "1000000000"])
     ap.add_argument("--precision", default="fp32", choices=["fp32", "f32x3", "bf16"])
     ap.add_argument("--lang", default="c")
+    ap.add_argument("--no_cosine", action="store_true",
+                    help="GraphCodeBERT preprocessing: keep every top-60 candidate "
+                         "(GraphCodeBERT/Defect-detection/preprocess/get_substitutes.py:72-134)")
     args = ap.parse_args()
 
     import torch
@@ -47,7 +50,8 @@ def main():
         sd = load_checkpoint(base)
         tok = Tokenizer(base / "vocab.json", base / "merges.txt")
     eng = Engine(sd, head="none", with_mlm=True, precision=args.precision, device=local)
-    gen = SubstituteGenerator(eng, tok, block_size=args.block_size, lang=args.lang)
+    gen = SubstituteGenerator(eng, tok, block_size=args.block_size, lang=args.lang,
+                              cosine=not args.no_cosine)
     t0 = time.time()
     tot = run_sharded_substitutes(gen, args.eval_data_file, args.store_path,
                                   int(args.index[0]), int(args.index[1]),
