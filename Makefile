@@ -11,10 +11,10 @@ HDRS := $(CSRC)/common.h include/alert_engine.h
 HIPFLAGS := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -Wall -Wno-unused-result
 
 HOSTLIB := $(PKG)/lib/libalert_host.so
-HOSTSRCS := $(CSRC)/host/bpe.cpp $(CSRC)/host/lexer.cpp $(CSRC)/host/mutate.cpp $(CSRC)/host/dfg.cpp $(CSRC)/host/dfg_java.cpp $(CSRC)/host/dfg_python.cpp $(CSRC)/host/capi.cpp
+HOSTSRCS := $(CSRC)/host/bpe.cpp $(CSRC)/host/lexer.cpp $(CSRC)/host/mutate.cpp $(CSRC)/host/dfg.cpp $(CSRC)/host/dfg_java.cpp $(CSRC)/host/dfg_python.cpp $(CSRC)/host/gcb.cpp $(CSRC)/host/capi.cpp
 HOSTHDRS := $(CSRC)/host/host.h $(CSRC)/host/dfg_util.h $(CSRC)/host/unicode_tables.h include/alert_host.h
 CXX ?= g++
-HOSTFLAGS := -O2 -std=c++17 -fPIC -shared -Wall -Wextra -Wno-unused-parameter -Iinclude
+HOSTFLAGS := -O2 -std=c++17 -fPIC -shared -pthread -Wall -Wextra -Wno-unused-parameter -Iinclude
 
 all: $(LIB) $(HOSTLIB)
 

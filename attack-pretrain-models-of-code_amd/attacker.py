@@ -817,29 +817,34 @@ class GraphCloneAttacker(CloneAttacker):
         self.ga_batch = None
 
     def _pair_state(self, code):
-        from .graph import task_features
+        from .graph import compact_features, task_features
 
         tok, args = self.tokenizer_tgt, self.args
         _, toks2 = get_identifiers(code[3], self.lang)
         f2 = task_features(code[3], tok, 0, args, "clone")
         f2w = task_features(" ".join(toks2), tok, 0, args, "clone")
+        if hasattr(tok, "gcb_features"):  # code2 compact once per example
+            return compact_features(f2), compact_features(f2w)
         return f2, f2w
 
-    def _population(self, ex, pops, mode):
-        from .graph import task_features
+    def _feats(self, texts):
+        """code1 query features of many texts (run_parser data flow, Java text as is)."""
+        from .graph import gcb_dataset_from_texts, task_features
 
         tok, args = self.tokenizer_tgt, self.args
-        feats = [task_features(ex.mutant_text(p, mode), tok, 0, args, "clone") for p in pops]
+        if hasattr(tok, "gcb_features"):
+            return gcb_dataset_from_texts(texts, tok, args, "clone").c
+        return [task_features(t, tok, 0, args, "clone") for t in texts]
+
+    def _population(self, ex, pops, mode):
+        feats = self._feats([ex.mutant_text(p, mode) for p in pops])
         return self.model_tgt.prepare_pair_population(feats, self._code2[0])
 
     def _importance_payload(self):
-        from .graph import task_features
-
         f2w = self._code2[1]
-        tok, args = self.tokenizer_tgt, self.args
 
         def build(word_lists):
-            feats = [task_features(" ".join(w), tok, 0, args, "clone") for w in word_lists]
+            feats = self._feats([" ".join(w) for w in word_lists])
             return self.model_tgt.prepare_pair_population(feats, f2w)
 
         return build

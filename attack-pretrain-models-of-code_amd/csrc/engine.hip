@@ -51,6 +51,8 @@ hipError_t ae_launch_cosine_rank(const float*, const float*, int, int, int, floa
 hipError_t ae_launch_scatter_rows(const float*, const int*, const int*, int, int, int, int,
                                   float*, const int*, hipStream_t);
 hipError_t ae_launch_nll_rows(const float*, const int*, int, int, float*, hipStream_t);
+hipError_t ae_launch_graph_mask(const int*, const int*, const int*, const int*, int, int, int,
+                                uint32_t*, hipStream_t);
 }
 
 namespace {
@@ -729,6 +731,16 @@ int ae_topk(const float* x, int32_t rows, int32_t cols, int32_t k, float* vals_o
   if (!x || !vals_out || !idx_out) return fail(AE_EINVAL, "null argument");
   if (rows < 0 || cols < 1 || k < 1 || k > 256 || k > cols) return fail(AE_EINVAL, "bad shape");
   HIPC(ae_launch_topk(x, rows, cols, k, vals_out, idx_out, (hipStream_t)stream));
+  return AE_OK;
+}
+
+int ae_graph_mask(const int32_t* ids, const int32_t* meta, const int32_t* spans,
+                  const int32_t* edges, int32_t n, int32_t L, int32_t e_cap, uint32_t* mask_bits,
+                  void* stream) {
+  if (n > 0 && (!ids || !meta || !spans || !edges || !mask_bits))
+    return fail(AE_EINVAL, "null argument");
+  if (n < 0 || L < 32 || L % 32 || L > 1024 || e_cap < 1) return fail(AE_EINVAL, "bad shape");
+  HIPC(ae_launch_graph_mask(ids, meta, spans, edges, n, L, e_cap, mask_bits, (hipStream_t)stream));
   return AE_OK;
 }
 

@@ -10,8 +10,9 @@
 //     a·w ≈ a_hi·w_hi + a_hi·w_lo + a_lo·w_hi          (3 bf16 MFMAs, f32 accumulate)
 // from ONE load of the four planes.
 //
-// Two kernels: gemm_pp_kernel (below; production for N % 256 == 0, i.e. every encoder GEMM) and
-// gemm_pk_kernel (other widths; its gfx950 mapping:)
+// Three kernels: gemm_pp_kernel and gemm_pp192_kernel (below; the production path, chosen per
+// shape by ae_launch_gemm_packed) and gemm_pk_kernel (the round-1 kernel, now reachable only
+// through ae_bench_gemm_packed for A/B runs; its gfx950 mapping:)
 //   * tile 256 x BN (BN = 256: 8 waves as 2 x 4, wave tile 128 x 64; BN = 128: 4 x 2, 64 x 64),
 //     one 512-thread workgroup per CU, LDS NST x (256 + BN) x 128 B (NST = 3 stages for BN = 128,
 //     2 for BN = 256)
@@ -713,6 +714,215 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Ping-pong 256 x 192 packed GEMM (gemm_pp192_kernel): the N = 768 GEMMs (O-projection, FFN2)
+// tile as 128 x 4 = 512 tiles = 2 full rounds on 256 CUs instead of 384 256^2 tiles (1.5 rounds,
+// the second half idle).  gemm_pp_kernel's structure with a 64 x 96 block per wave: group g
+// (rows 128 g ..) holds 4 waves as 2 (m) x 2 (n); a K-tile is consumed in three phases, one
+// 64 x 32 column block (tn) each — phase 0 reads A (both 32-row blocks) and W(tn 0), phases 1
+// and 2 read W(tn 1), W(tn 2).  Two 56-KiB stages; K-tile kt+2's A + W(tn 0) go into kt's stage
+// at phase 2 of kt (their last read was phase 0), W(tn 1) and W(tn 2) of kt+1 at phases 0 and 1
+// of kt (>= 2 phases after their last read); each waited one phase before it is read.  f32
+// epilogues only (bias / +residual / tanh), staged through LDS in 32-row passes with 400-B
+// padded rows (conflict-free), stored as whole 384-B row segments.
+template <int NP, int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
+    const __bf16* __restrict__ A, const __bf16* __restrict__ W, const float* __restrict__ bias,
+    const float* __restrict__ R, float* __restrict__ C, int M, int N, int K, int group_m) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char pk_smem[];
+  constexpr int BM = 256, BN = 192, ROWB = PK_ROWB;
+  constexpr int A_BYTES = BM * ROWB, STAGE = (BM + BN) * ROWB;  // 56 KiB per K-tile
+  constexpr int KB = 64 / NP, NS = KB / 16, T = NP == 2 ? 3 : 1;
+
+  const int tiles_n = (N + BN - 1) / BN;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int per_group = group_m * tiles_n;
+  const int g = t / per_group, first_m = g * group_m;
+  const int gsize = min(tiles_m - first_m, group_m);
+  const int tm0 = first_m + (t - g * per_group) % gsize, tn0 = (t - g * per_group) / gsize;
+  const int m0 = tm0 * BM, n0 = tn0 * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, sm = (wave >> 1) & 1, sn = wave & 1;  // group, sub-row, sub-column
+  const int li = lane & 31, lh = lane >> 5;
+  const size_t lda = (size_t)NP * K;
+
+  // ---- DMA pieces (8 rows x 128 B) per wave per K-tile: [0..3] A rows 32 wave + 8 u, [4..6]
+  // W(tn) rows 96 (wave >> 2) + 32 tn + 8 (wave & 3) (the 64 W rows of column block tn)
+  const char* src[7];
+  uint32_t dst[7];
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    const bool is_a = j < 4;
+    const int r0 = is_a ? 32 * wave + 8 * j : 96 * (wave >> 2) + 32 * (j - 4) + 8 * (wave & 3);
+    const int r = r0 + (lane >> 3);
+    const int cs = (lane & 7) ^ ((r >> 1) & 7);
+    if (is_a) {
+      const int gr = m0 + r < M ? m0 + r : M - 1;
+      src[j] = reinterpret_cast<const char*>(A + gr * lda) + 16 * cs;
+      dst[j] = r0 * ROWB;
+    } else {
+      const int gr = n0 + r < N ? n0 + r : N - 1;
+      src[j] = reinterpret_cast<const char*>(W + gr * lda) + 16 * cs;
+      dst[j] = A_BYTES + r0 * ROWB;
+    }
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)pk_smem;
+  const int nk = K / KB;
+  auto issue = [&](int j, int kt) {
+    dma16(src[j] + (size_t)kt * ROWB, lds0 + (kt & 1) * STAGE + dst[j]);
+  };
+
+  floatx16 acc[2][3];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  const int sw = (li >> 1) & 7;
+  const int a_row = (wm * 128 + sm * 64 + li) * ROWB;
+  const int w_row = A_BYTES + (sn * 96 + li) * ROWB;
+  bf16x8 fa[2][NS][NP], fw[3][NS][NP];
+  auto read_a = [&](const unsigned char* st) {
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+          fa[tt][s][p] = *reinterpret_cast<const bf16x8*>(
+              st + a_row + tt * 32 * ROWB + 16 * ((4 * p + 2 * s + lh) ^ sw));
+  };
+  auto read_w = [&](const unsigned char* st, int tn) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+        fw[tn][s][p] = *reinterpret_cast<const bf16x8*>(
+            st + w_row + tn * 32 * ROWB + 16 * ((4 * p + 2 * s + lh) ^ sw));
+  };
+  // column block tn's MFMAs; DMA pieces j0 .. j0 + nj - 1 of K-tile kd ride in the issue gaps
+  auto mfma_col = [&](int tn, auto j0c, auto njc, bool dma, int kd) {
+    constexpr int J0 = decltype(j0c)::value, NJ = decltype(njc)::value;
+    constexpr int NM = NS * 2 * T;
+    constexpr int EVERY = NJ > 0 ? NM / (NJ + 1) : NM + 1;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+      const int s = i / (2 * T), tt = (i / T) % 2, term = i % T;
+      floatx16& c = acc[tt][tn];
+      const bf16x8& x = (T == 3 && term == 1) ? fw[tn][s][NP - 1] : fw[tn][s][0];
+      const bf16x8& y = (T == 3 && term == 0) ? fa[tt][s][NP - 1] : fa[tt][s][0];
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, c, 0, 0, 0);
+      if (dma && i % EVERY == EVERY - 1 && i / EVERY < NJ) {
+        const int j = J0 + i / EVERY;
+        __builtin_amdgcn_sched_barrier(0);
+        dma16(src[j] + (size_t)kd * ROWB, lds0 + (kd & 1) * STAGE + dst[j]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto sync_compute = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto sync_load = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue: K-tile 0 whole, K-tile 1's A + W(tn 0) (its W(tn 1), W(tn 2): phases 0, 1 of kt 0)
+  if (nk > 0) {
+#pragma unroll
+    for (int j = 0; j < 7; ++j) issue(j, 0);
+  }
+  if (nk > 1) {
+#pragma unroll
+    for (int j = 0; j < 5; ++j) issue(j, 1);
+    asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // K-tile 0's A + W(tn 0)
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) sync_load();  // group 1 runs one phase behind
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const unsigned char* st = pk_smem + (kt & 1) * STAGE;
+    const bool next1 = kt + 1 < nk, next2 = kt + 2 < nk;
+    // phase 0: reads A, W(tn 0); waits for W(tn 1) of kt; W(tn 1) of kt+1 into its stage
+    if (next1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    read_a(st);
+    read_w(st, 0);
+    sync_compute();
+    mfma_col(0, std::integral_constant<int, 5>(), std::integral_constant<int, 1>(), next1,
+             kt + 1);
+    sync_load();
+    // phase 1: reads W(tn 1); waits for W(tn 2) of kt; W(tn 2) of kt+1 into its stage
+    if (next1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    read_w(st, 1);
+    sync_compute();
+    mfma_col(1, std::integral_constant<int, 6>(), std::integral_constant<int, 1>(), next1,
+             kt + 1);
+    sync_load();
+    // phase 2: reads W(tn 2); waits for A + W(tn 0) of kt+1; A + W(tn 0) of kt+2 into kt's stage
+    if (next1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    read_w(st, 2);
+    sync_compute();
+    mfma_col(2, std::integral_constant<int, 0>(), std::integral_constant<int, 5>(), next2,
+             kt + 2);
+    sync_load();
+  }
+  if (wm == 0) sync_load();  // same barrier count in both groups; every LDS read and DMA done
+
+  // ---- epilogue: per 32-row pass (tm), the wave's 32 x 96 f32 block goes to its LDS region
+  // (rows of 400 B: 384 + 16 pad, so 16 lanes of different rows hit 16 different bank slots),
+  // then whole 384-B row segments go out with 16-B lanes (+ bias, tanh / residual)
+  constexpr int RS = 400;
+  unsigned char* reg = pk_smem + wave * 32 * RS;
+  const int cb0 = n0 + sn * 96;
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm) {
+#pragma unroll
+    for (int tn = 0; tn < 3; ++tn)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        floatx4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = acc[tm][tn][4 * j + i];
+        *reinterpret_cast<floatx4*>(reg + li * RS + (tn * 8 + 2 * j + lh) * 16) = v;
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+      const int idx = k * 64 + lane, lr = idx / 24, c = idx % 24;
+      const int row = m0 + wm * 128 + sm * 64 + tm * 32 + lr;
+      const int col = cb0 + 4 * c;
+      floatx4 f = *reinterpret_cast<const floatx4*>(reg + lr * RS + c * 16);
+      if (row < M && col < N) {
+        const size_t o = (size_t)row * N + col;
+        f += *reinterpret_cast<const floatx4*>(bias + col);
+        if (EPI == PK_EPI_TANH)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) f[i] = tanhf(f[i]);
+        if (EPI == PK_EPI_RES) f += *reinterpret_cast<const floatx4*>(R + o);
+        *reinterpret_cast<floatx4*>(C + o) = f;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
 namespace {
 template <int NP, int EPI, int DIAG>
 hipError_t pp_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R, float* C,
@@ -749,6 +959,40 @@ hipError_t pp_epi(int epi, const __bf16* A, const __bf16* W, const float* bias, 
       return pp_launch<NP, PK_EPI_RES, 0>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
     default: return pp_launch<NP, PK_EPI_TANH, 0>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
   }
+}
+
+template <int NP, int EPI>
+hipError_t pp192_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R,
+                        float* C, int M, int N, int K, int group_m, hipStream_t st) {
+  constexpr int lds = 2 * (256 + 192) * PK_ROWB;  // 112 KiB
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_pp192_kernel<NP, EPI>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int tiles = ((M + 255) / 256) * ((N + 191) / 192);
+  hipLaunchKernelGGL((gemm_pp192_kernel<NP, EPI>), dim3(tiles), dim3(512), lds, st, A, W, bias, R,
+                     C, M, N, K, group_m);
+  return hipGetLastError();
+}
+
+// f32 epilogues only (bias, +residual, tanh); N % 32 == 0
+hipError_t pp192_dispatch(const unsigned short* A, const unsigned short* W, const float* bias,
+                          const float* R, float* C, int M, int N, int K, int epi, int np,
+                          int group_m, hipStream_t st) {
+  auto a = reinterpret_cast<const __bf16*>(A);
+  auto w = reinterpret_cast<const __bf16*>(W);
+  if (epi == PK_EPI_GELU_PACKED) return hipErrorInvalidValue;
+  if (np == 2) {
+    if (epi == PK_EPI_BIAS) return pp192_launch<2, PK_EPI_BIAS>(a, w, bias, R, C, M, N, K, group_m, st);
+    if (epi == PK_EPI_RES) return pp192_launch<2, PK_EPI_RES>(a, w, bias, R, C, M, N, K, group_m, st);
+    return pp192_launch<2, PK_EPI_TANH>(a, w, bias, R, C, M, N, K, group_m, st);
+  }
+  if (epi == PK_EPI_BIAS) return pp192_launch<1, PK_EPI_BIAS>(a, w, bias, R, C, M, N, K, group_m, st);
+  if (epi == PK_EPI_RES) return pp192_launch<1, PK_EPI_RES>(a, w, bias, R, C, M, N, K, group_m, st);
+  return pp192_launch<1, PK_EPI_TANH>(a, w, bias, R, C, M, N, K, group_m, st);
 }
 
 template <int DIAG>
@@ -827,6 +1071,30 @@ bool pk_shape_ok(int M, int N, int K, int np) {
 }
 }  // namespace
 
+namespace {
+int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      n = v;
+    else
+      n = 256;
+  }
+  return n;
+}
+
+// tile width of the ping-pong GEMM for an M x N output (see ae_launch_gemm_packed)
+int pp_choose(int M, int N, int epi) {
+  if (epi == PK_EPI_GELU_PACKED) return 256;
+  const long tm = (M + 255) / 256, cus = cu_count();
+  const long r256 = (tm * ((N + 255) / 256) + cus - 1) / cus;
+  const long r192 = (tm * ((N + 191) / 192) + cus - 1) / cus;
+  return 0.89 * (double)r192 < (double)r256 ? 192 : 256;
+}
+}  // namespace
+
 // C = A·W^T (+epilogue) over packed bf16 planes.  A: [M][np*K], W: [N][np*K] packed (see top);
 // f32 output C [M][N] or packed output planes Cp [M][np*N] (GELU epilogue).  np: 2 = split-bf16
 // (f32-class), 1 = plain bf16.  Requires K % 64 == 0 and N % 32 == 0.
@@ -836,11 +1104,14 @@ extern "C" hipError_t ae_launch_gemm_packed(const unsigned short* A, const unsig
                                             int np, hipStream_t st) {
   if (M <= 0) return hipSuccess;
   if (!pk_shape_ok(M, N, K, np)) return hipErrorInvalidValue;
-  // the ping-pong 256 x 256 kernel for every width it tiles exactly (all encoder GEMMs: 768,
-  // 2304, 3072 — for N = 768 its 1.5 rounds of 256^2 tiles still beat 3 rounds of 256 x 128)
-  if (N % 256 == 0) return pp_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
-  return pk_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, pick_bn(M, N), st);
+  // the ping-pong kernels for every encoder GEMM: 256 x 192 or 256 x 256 tiles, whichever
+  // finishes first by rounds of CU-count tiles x per-tile time (tools/gemm_bench.py: a 256 x 192
+  // round takes 0.89 of a 256 x 256 round; the 192 kernel has f32 epilogues only)
+  return pp_choose(M, N, epi) == 192
+             ? pp192_dispatch(A, W, bias, R, C, M, N, K, epi, np, PK_GROUP_M, st)
+             : pp_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
 }
+
 
 // Kernel experiments (tools/gemm_bench.py, tests): explicit tile width (0 = the production choice)
 // and a diagnostic variant (0 = the production kernel; see DIAG above — other values give WRONG
@@ -850,8 +1121,10 @@ extern "C" hipError_t ae_bench_gemm_packed(const unsigned short* A, const unsign
                                            unsigned short* Cp, int M, int N, int K, int epi,
                                            int np, int bn, int diag, hipStream_t st) {
   if (M <= 0) return hipSuccess;
-  if (!pk_shape_ok(M, N, K, np) || (bn != 0 && bn != 128 && bn != 256 && bn != 512))
+  if (!pk_shape_ok(M, N, K, np) ||
+      (bn != 0 && bn != 128 && bn != 192 && bn != 256 && bn != 512))
     return hipErrorInvalidValue;
+  if (bn == 192) return pp192_dispatch(A, W, bias, R, C, M, N, K, epi, np, PK_GROUP_M, st);
   if (bn == 512) {  // the ping-pong 256 x 256 kernel
     switch (diag) {
       case 0: return pp_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);

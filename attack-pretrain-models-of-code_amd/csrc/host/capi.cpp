@@ -1,7 +1,9 @@
 // capi.cpp — extern "C" surface of libalert_host.so (include/alert_host.h).
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 
 #include "../../../include/alert_host.h"
@@ -9,7 +11,23 @@
 
 struct ah_tokenizer {
   ah::Tokenizer t;
+  // worker clones for the multi-threaded featurisers (the BPE caches are per object)
+  std::mutex mu;
+  std::vector<std::unique_ptr<ah::Tokenizer>> clones;
+  std::vector<std::unique_ptr<std::unordered_map<std::string, std::vector<int32_t>>[]>> leaf_caches;
 };
+
+namespace ah {
+struct GcbArgs {
+  Lang lang;
+  DfgVariant variant;
+  bool normalize, run_trunc;
+  int code_length, dfl, e_cap;
+};
+bool gcb_features_one(Tokenizer& t, std::unordered_map<std::string, std::vector<int32_t>>* cache,
+                      const std::string& code_in, const GcbArgs& a, int32_t* ids, int32_t* pos,
+                      int32_t* meta, int32_t* spans, int32_t* edges, std::string* err);
+}  // namespace ah
 
 struct ah_example {
   ah::Example ex;
@@ -86,6 +104,55 @@ bool build_mutant(ah_example* e, int32_t mode, int32_t b, int32_t end, const cha
 extern "C" {
 
 const char* ah_last_error(void) { return g_err.c_str(); }
+
+int32_t ah_gcb_features_batch(ah_tokenizer* tok, int32_t n, const char* const* codes, int32_t lang,
+                              int32_t variant, int32_t flags, int32_t code_length,
+                              int32_t data_flow_length, int32_t e_cap, int32_t threads,
+                              int32_t* ids_out, int32_t* pos_out, int32_t* meta_out,
+                              int32_t* spans_out, int32_t* edges_out) {
+  if (!tok || (n > 0 && (!codes || !ids_out || !pos_out || !meta_out || !spans_out || !edges_out)))
+    return fail("null argument");
+  if (lang < 0 || lang > 2) return fail("unknown language");
+  if (variant != AH_DFG_RUN_PARSER && variant != AH_DFG_GCB_RUN) return fail("unknown DFG variant");
+  if (variant == AH_DFG_GCB_RUN && lang == AH_LANG_C)
+    return fail("the GraphCodeBERT run.py data flow has no C walk (parser/DFG.py)");
+  const int32_t L = code_length + data_flow_length;
+  if (code_length < 4 || data_flow_length < 0 || L > 65535 || e_cap < 1) return fail("bad lengths");
+  ah::GcbArgs a{(ah::Lang)lang, (ah::DfgVariant)variant, (flags & AH_GCB_NORMALIZE) != 0,
+                (flags & AH_GCB_RUN_TRUNC) != 0, code_length, data_flow_length, e_cap};
+  const int nthr = std::max(1, std::min(std::min(threads, n), 64));
+  {
+    std::lock_guard<std::mutex> g(tok->mu);
+    while ((int)tok->clones.size() < nthr) {
+      tok->clones.emplace_back(new ah::Tokenizer(tok->t));
+      tok->leaf_caches.emplace_back(new std::unordered_map<std::string, std::vector<int32_t>>[2]);
+    }
+  }
+  std::vector<std::string> errs(nthr);
+  std::vector<char> ok(nthr, 1);
+  auto work = [&](int w) {
+    for (int32_t i = w; i < n; i += nthr) {
+      if (!ah::gcb_features_one(*tok->clones[w], tok->leaf_caches[w].get(), codes[i], a,
+                                ids_out + (size_t)i * L, pos_out + (size_t)i * L,
+                                meta_out + (size_t)i * 4, spans_out + (size_t)i * L,
+                                edges_out + (size_t)i * e_cap, &errs[w])) {
+        ok[w] = 0;
+        return;
+      }
+    }
+  };
+  if (nthr == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> pool;
+    for (int w = 1; w < nthr; ++w) pool.emplace_back(work, w);
+    work(0);
+    for (auto& th : pool) th.join();
+  }
+  for (int w = 0; w < nthr; ++w)
+    if (!ok[w]) return fail(errs[w]);
+  return n;
+}
 
 ah_tokenizer* ah_tokenizer_load(const char* vocab_json, const char* merges_txt) {
   auto* t = new ah_tokenizer();

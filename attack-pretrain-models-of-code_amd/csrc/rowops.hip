@@ -360,7 +360,76 @@ __global__ __launch_bounds__(256) void nll_rows_kernel(const float* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------------
+// GraphCodeDataset.__getitem__'s graph-guided attention mask (GraphCodeBERT/*/code/run.py
+// TextDataset / utils.py:547-570) built from the compact features of ah_gcb_features_batch, one
+// workgroup per query, the [L, L/32] bit image assembled in LDS:
+//   rows < node_index: keys [0, node_index)                (code tokens see code tokens)
+//   rows with id 0 / 2 (CLS / SEP): keys [0, max_length)
+//   node k (row node_index + k), span (a, b): keys [a, b), and rows a..b-1 see key node_index + k
+//   edge (k, t): row node_index + k sees key node_index + t (t + node_index < L)
+__device__ __forceinline__ uint32_t range_bits(int w, int a, int b) {
+  const int lo = max(a, 32 * w), hi = min(b, 32 * w + 32);
+  if (lo >= hi) return 0u;
+  const int n = hi - lo;
+  return (n == 32 ? 0xffffffffu : ((1u << n) - 1u)) << (lo - 32 * w);
+}
+
+__global__ __launch_bounds__(256) void graph_mask_kernel(const int* __restrict__ ids,
+                                                         const int* __restrict__ meta,
+                                                         const int* __restrict__ spans,
+                                                         const int* __restrict__ edges, int L,
+                                                         int e_cap, uint32_t* __restrict__ bits) {
+  extern __shared__ uint32_t gm_words[];
+  const int q = blockIdx.x, W = L >> 5;
+  const int ni = meta[4 * q], ml = meta[4 * q + 1], nn = meta[4 * q + 2], ne = meta[4 * q + 3];
+  const int* qid = ids + (size_t)q * L;
+  const int* qsp = spans + (size_t)q * L;
+  for (int x = threadIdx.x; x < L * W; x += blockDim.x) {
+    const int r = x / W, w = x - r * W;
+    uint32_t v = 0;
+    if (r < ni) v |= range_bits(w, 0, ni);
+    const int id = qid[r];
+    if (id == 0 || id == 2) v |= range_bits(w, 0, ml);
+    if (r >= ni && r - ni < nn) {
+      const int sp = qsp[r - ni];
+      if (sp >= 0) v |= range_bits(w, sp & 0xffff, sp >> 16);
+    }
+    gm_words[x] = v;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < nn; k += blockDim.x) {
+    const int sp = qsp[k];
+    if (sp < 0) continue;
+    const int col = ni + k;
+    for (int r = sp & 0xffff; r < (sp >> 16); ++r) atomicOr(&gm_words[r * W + (col >> 5)], 1u << (col & 31));
+  }
+  for (int j = threadIdx.x; j < ne; j += blockDim.x) {
+    const int e = edges[(size_t)q * e_cap + j];
+    const int row = ni + (e & 0xffff), col = ni + (e >> 16);
+    if (col < L) atomicOr(&gm_words[row * W + (col >> 5)], 1u << (col & 31));
+  }
+  __syncthreads();
+  uint32_t* out = bits + (size_t)q * L * W;
+  for (int x = threadIdx.x; x < L * W; x += blockDim.x) out[x] = gm_words[x];
+}
+
 extern "C" {
+hipError_t ae_launch_graph_mask(const int* ids, const int* meta, const int* spans,
+                                const int* edges, int n, int L, int e_cap, uint32_t* bits,
+                                hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const size_t lds = (size_t)L * (L / 32) * 4;
+  static size_t attr = 0;
+  if (lds > 65536 && attr < lds) {
+    hipError_t e = hipFuncSetAttribute((const void*)graph_mask_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    attr = lds;
+  }
+  hipLaunchKernelGGL(graph_mask_kernel, dim3(n), dim3(256), lds, st, ids, meta, spans, edges, L,
+                     e_cap, bits);
+  return hipGetLastError();
+}
 hipError_t ae_launch_scatter_rows(const float* x, const int* cu, const int* src_col, int n,
                                   int row0, int nrows, int T, float* out, const int* err,
                                   hipStream_t st) {

@@ -33,7 +33,8 @@ class AeWeightView(ctypes.Structure):
 
 
 # every symbol include/alert_engine.h declares (checked by tests/test_abi.py)
-EXPORTS = ("ae_create", "ae_destroy", "ae_score", "ae_score_graph", "ae_encode", "ae_encode_ex", "ae_mlm_topk",
+EXPORTS = ("ae_create", "ae_destroy", "ae_score", "ae_score_graph", "ae_graph_mask", "ae_encode",
+           "ae_encode_ex", "ae_mlm_topk",
            "ae_mlm_nll", "ae_splice",
            "ae_topk", "ae_cosine_rank", "ae_set_profiling", "ae_kernel_time", "ae_last_error",
            "ae_version")
@@ -60,6 +61,7 @@ def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     lib.ae_destroy.argtypes = [vp]
     lib.ae_score.argtypes = [vp, vp, vp, vp, vp, i32, i32, vp, vp]
     lib.ae_score_graph.argtypes = [vp, vp, vp, vp, vp, i32, i32, vp, vp]
+    lib.ae_graph_mask.argtypes = [vp, vp, vp, vp, i32, i32, i32, vp, vp]
     lib.ae_encode.argtypes = [vp, vp, vp, i32, i32, vp, vp]
     lib.ae_encode_ex.argtypes = [vp, vp, vp, i32, i32, i32, i32, i32, vp, vp]
     lib.ae_mlm_topk.argtypes = [vp, vp, i32, i32, vp, vp, vp]
@@ -177,6 +179,23 @@ class Engine:
         _check(self.lib.ae_score_graph(self.handle, _ptr(ids), ctypes.c_void_p(lens.ctypes.data),
                                        _ptr(pos), _ptr(mask_bits), n, L, _ptr(out),
                                        _stream(stream)), "ae_score_graph")
+        return out
+
+    def graph_mask(self, ids, meta, spans, edges, out=None, stream=None):
+        """Device-built bit mask [n, L, L/32] (ae_graph_mask) from the compact features of
+        Tokenizer.gcb_features (all device int32: ids / spans [n, L], meta [n, 4], edges
+        [n, e_cap])."""
+        import torch
+
+        n, L = ids.shape
+        for t in (ids, meta, spans, edges):
+            assert t.dtype == torch.int32 and t.is_cuda and t.is_contiguous()
+        assert meta.shape == (n, 4) and spans.shape == (n, L) and edges.shape[0] == n
+        if out is None:
+            out = torch.empty((n, L, L // 32), dtype=torch.int32, device=ids.device)
+        _check(self.lib.ae_graph_mask(_ptr(ids), _ptr(meta), _ptr(spans), _ptr(edges), n, L,
+                                      edges.shape[1], _ptr(out), _stream(stream)),
+               "ae_graph_mask")
         return out
 
     def encode(self, ids, lens: np.ndarray, attend_pad: bool = False, row0: int = 0,

@@ -22,9 +22,12 @@ Which builder, language and whitespace handling each GraphCodeBERT victim uses (
                                               run.extract_dataflow)
 
 The reference builds a bool [L, L] mask per query in Python loops and ships it to the GPU as
-L*L bytes; here the mask is built with numpy slices and shipped bit-packed (uint32 [L, L/32],
-bit j of word w = key 32*w + j), 8x less host->device traffic, which is what the attention kernel
-reads directly.
+L*L bytes.  The attack-time queries here go through the C++ batch featuriser
+(Tokenizer.gcb_features: worker threads, one tokenizer clone each) which leaves the mask compact
+(per query: node_index, max_length, node code spans, node->node edges, ~4 KB instead of 400 KB),
+and the device builds the bit-packed mask (uint32 [L, L/32], bit j of word w = key 32*w + j) that
+the attention kernel reads (ae_graph_mask).  The numpy builder below (graph_mask / pack_mask)
+remains for the dataset example and as the reference the device path is tested against.
 """
 from __future__ import annotations
 
@@ -201,6 +204,129 @@ class GraphCodeDataset:
         return ids, pos, bits
 
 
+def compact_features(f, e_cap: int | None = None) -> dict:
+    """One GraphInputFeatures -> the compact arrays of Tokenizer.gcb_features ([1, ...] each)."""
+    ids = np.asarray(f.input_ids, dtype=np.int32)
+    pos = np.asarray(f.position_idx, dtype=np.int32)
+    L = len(ids)
+    e_cap = e_cap or 4 * L
+    ni, nn = int((pos > 1).sum()), len(f.dfg_to_code)
+    spans = np.full((L,), -1, np.int32)
+    for k, (a, b) in enumerate(f.dfg_to_code):
+        if a < ni and b < ni:
+            spans[k] = a | (b << 16)
+    edges = [k | (t << 16) for k, ts in enumerate(f.dfg_to_dfg) for t in ts if ni + t < L]
+    if len(edges) > e_cap:
+        raise ValueError("more data-flow edges than e_cap")
+    e = np.zeros((e_cap,), np.int32)
+    e[:len(edges)] = edges
+    meta = np.asarray([ni, int((pos != 1).sum()), nn, len(edges)], np.int32)
+    return {"ids": ids[None], "pos": pos[None], "meta": meta[None], "spans": spans[None],
+            "edges": e[None]}
+
+
+def graph_mask_from_compact(ids, meta, spans, edges) -> np.ndarray:
+    """bool [L, L] from one query's compact arrays (what ae_graph_mask builds on the device)."""
+    L = len(ids)
+    ni, ml, nn, ne = (int(x) for x in meta)
+    m = np.zeros((L, L), dtype=bool)
+    m[:ni, :ni] = True
+    m[np.nonzero((ids == 0) | (ids == 2))[0], :ml] = True
+    for k in range(nn):
+        sp = int(spans[k])
+        if sp >= 0:
+            a, b = sp & 0xFFFF, sp >> 16
+            m[ni + k, a:b] = True
+            m[a:b, ni + k] = True
+    for e in edges[:ne]:
+        k, t = int(e) & 0xFFFF, int(e) >> 16
+        if ni + t < L:
+            m[ni + k, ni + t] = True
+    return m
+
+
+def _cat_compact(parts):
+    return {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
+
+
+class CompactGraphDataset:
+    """Queries featurised by Tokenizer.gcb_features: the arrays stay compact until the device
+    builds the mask.  pairs=True: rows interleaved code1, code2 (len = rows / 2).  Indexing and
+    packed() rebuild the reference's tuples / bits on the host (compatibility, tests)."""
+
+    def __init__(self, arrays: dict, labels=None, pairs: bool = False):
+        self.c = arrays
+        self.pairs = pairs
+        rows = len(arrays["ids"])
+        self.n = rows // 2 if pairs else rows
+        self.labels = list(labels) if labels is not None else [0] * self.n
+
+    def __len__(self):
+        return self.n
+
+    def _row(self, r):
+        c = self.c
+        m = graph_mask_from_compact(c["ids"][r], c["meta"][r], c["spans"][r], c["edges"][r])
+        return c["ids"][r], c["pos"][r], m
+
+    def __getitem__(self, item):
+        import torch
+
+        if self.pairs:
+            out = []
+            for r in (2 * item, 2 * item + 1):
+                ids, pos, m = self._row(r)
+                out += [torch.tensor(ids), torch.tensor(pos), torch.tensor(m)]
+            return tuple(out) + (torch.tensor(self.labels[item]),)
+        ids, pos, m = self._row(item)
+        return (torch.tensor(ids), torch.tensor(m), torch.tensor(pos),
+                torch.tensor(self.labels[item]))
+
+    def packed(self):
+        rows = len(self.c["ids"])
+        bits = np.stack([pack_mask(self._row(r)[2]) for r in range(rows)])
+        return self.c["ids"], self.c["pos"], bits
+
+
+def payload_rows_host(live):
+    """(ids, pos, mask bits) numpy arrays of every row of GraphModel payloads, the compact ones'
+    masks built on the host (graph_mask_from_compact) — for victims without an engine."""
+    ids, pos, bits = [], [], []
+    for p in live:
+        ids.append(p.ids)
+        if p.extra[0] == "bits":
+            pos.append(p.extra[1])
+            bits.append(p.extra[2])
+        else:
+            c = p.extra[1]
+            pos.append(c["pos"])
+            bits.append(np.stack([pack_mask(graph_mask_from_compact(c["ids"][r], c["meta"][r],
+                                                                    c["spans"][r], c["edges"][r]))
+                                  for r in range(len(c["ids"]))]))
+    return np.concatenate(ids), np.concatenate(pos), np.concatenate(bits)
+
+
+def gcb_dataset_from_texts(texts, tokenizer, args, task: str, label=0):
+    """The task's convert_code_to_features of many query texts through the batch featuriser."""
+    lang, normalize, variant = TASK_FEATURES[task]
+    c = tokenizer.gcb_features(list(texts), lang, variant, normalize, args.code_length,
+                               args.data_flow_length)
+    return CompactGraphDataset(c, [label] * len(texts))
+
+
+def compact_pairs(c1: dict, c2_one: dict) -> CompactGraphDataset:
+    """Clone queries: rows of c1 (mutated code1) each paired with the single code2 query c2_one,
+    rows interleaved code1, code2 (clonedetection/code/model.py:42-45)."""
+    n = len(c1["ids"])
+    out = {}
+    for k in c1:
+        a, b = c1[k], np.repeat(c2_one[k], n, axis=0)
+        if a.shape[1:] != b.shape[1:]:
+            raise ValueError(f"pair feature widths differ for {k}")
+        out[k] = np.stack([a, b], 1).reshape((2 * n,) + a.shape[1:])
+    return CompactGraphDataset(out, pairs=True)
+
+
 class GraphPairFeatures:
     """GraphCodeBERT/clonedetection/code/run.py InputFeatures of a pair (field suffixes _1/_2)."""
 
@@ -301,15 +427,52 @@ class GraphModel(Model):
 
     def prepare(self, dataset) -> Payload:
         """(probs, pred_labels) request of GraphCodeBERT/*/code/model.py get_results: packed
-        ids / positions / mask bits (rows interleaved code1, code2 for clone pairs)."""
+        ids / positions / mask bits (rows interleaved code1, code2 for clone pairs), or the compact
+        arrays of a CompactGraphDataset (mask built on the device)."""
         n = len(dataset)
         if n == 0:
             return Payload(None, None, 0)
+        if isinstance(dataset, CompactGraphDataset):
+            return Payload(dataset.c["ids"], None, n, ("compact", dataset.c))
         if hasattr(dataset, "packed"):
             ids, pos, bits = dataset.packed()
         else:
             ids, pos, bits = _pack_items(dataset, self.task == "clone")
-        return Payload(ids, None, n, (pos, bits))
+        return Payload(ids, None, n, ("bits", pos, bits))
+
+    def _bits_rows(self, p, dev):
+        """Device mask bits of one payload's rows."""
+        import torch
+
+        kind = p.extra[0]
+        if kind == "bits":
+            return torch.from_numpy(np.ascontiguousarray(p.extra[2])).to(dev)
+        c = p.extra[1]
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+        return self.engine.graph_mask(t(c["ids"]), t(c["meta"]), t(c["spans"]), t(c["edges"]))
+
+    def score_payload_rows(self, live):
+        """Logits of every row of the live payloads (device mask build for compact ones)."""
+        import torch
+
+        dev = f"cuda:{self.engine.device}"
+        ids = np.concatenate([p.ids for p in live])
+        pos = np.concatenate([p.extra[1]["pos"] if p.extra[0] == "compact" else p.extra[1]
+                              for p in live])
+        n, L = ids.shape
+        step = self.max_rows_per_launch
+        outs, off, pi = [], 0, 0
+        bits_parts = []
+        for p in live:
+            bits_parts.append(self._bits_rows(p, dev))
+        bits = torch.cat(bits_parts, 0) if len(bits_parts) > 1 else bits_parts[0]
+        ids_d = torch.from_numpy(np.ascontiguousarray(ids)).to(dev)
+        pos_d = torch.from_numpy(np.ascontiguousarray(pos)).to(dev)
+        for s0 in range(0, n, step):
+            e = min(n, s0 + step)
+            lens = np.full((e - s0,), L, dtype=np.int32)
+            outs.append(self.engine.score_graph(ids_d[s0:e], lens, pos_d[s0:e], bits[s0:e]))
+        return torch.cat(outs, 0).cpu().numpy() if len(outs) > 1 else outs[0].cpu().numpy()
 
     def prepare_population(self, example, tokenizer, population, mode: int, block_size: int):
         """A population of chromosomes of one program: mutant texts (host get_example(_batch))
@@ -322,10 +485,7 @@ class GraphModel(Model):
         live = [p for p in payloads if p.n]
         if not live:
             return [([], []) for _ in payloads]
-        ids = np.concatenate([p.ids for p in live])
-        pos = np.concatenate([p.extra[0] for p in live])
-        bits = np.concatenate([p.extra[1] for p in live])
-        logits = self.score_packed(ids, pos, bits)
+        logits = self.score_payload_rows(live)
         out, off = [], 0
         for p in payloads:
             out.append(self._format(logits[off:off + p.n], threshold) if p.n else ([], []))
@@ -333,14 +493,21 @@ class GraphModel(Model):
         return out
 
     def dataset_from_texts(self, texts, tokenizer, args, label=0):
-        """Mutant texts -> GraphCodeDataset (the GCB attacker featurises every mutant text with
-        convert_code_to_features, GraphCodeBERT/Defect-detection/code/attacker.py:30-63, with the
-        task's language and builder).  Clone pairs are built by GraphCloneAttacker."""
+        """Mutant texts -> the GCB attacker's convert_code_to_features of each
+        (GraphCodeBERT/Defect-detection/code/attacker.py:30-63) with the task's language and
+        builder, through the batch featuriser (compact mask).  Clone pairs are built by
+        GraphCloneAttacker."""
         if self.task == "clone":
             raise ValueError("clone queries are pairs: build them with pair_features")
-        return GraphCodeDataset([task_features(t, tokenizer, label, args, self.task)
-                                 for t in texts], args)
+        if not hasattr(tokenizer, "gcb_features"):
+            return GraphCodeDataset([task_features(t, tokenizer, label, args, self.task)
+                                     for t in texts], args)
+        return gcb_dataset_from_texts(texts, tokenizer, args, self.task, label)
 
     def prepare_pair_population(self, feats1, f2) -> Payload:
-        """Clone queries of mutated code1 features against one fixed code2 (rows interleaved)."""
+        """Clone queries of mutated code1 features against one fixed code2 (rows interleaved).
+        feats1: a list of GraphInputFeatures, or the compact arrays of Tokenizer.gcb_features."""
+        if isinstance(feats1, dict):
+            c2 = f2 if isinstance(f2, dict) else compact_features(f2, feats1["edges"].shape[1])
+            return self.prepare(compact_pairs(feats1, c2))
         return self.prepare(CodePairDataset([GraphPairFeatures(f, f2, 0) for f in feats1]))

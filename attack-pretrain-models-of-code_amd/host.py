@@ -50,9 +50,10 @@ def load_host_library(path=None) -> ctypes.CDLL:
     lib.ah_example_dfg.argtypes = [vp, vp, i32, vp, i32]
     lib.ah_example_dfg_variant.argtypes = [vp, i32, vp, i32, vp, i32]
     lib.ah_remove_comments.argtypes = [cp, vp, i32]
+    lib.ah_gcb_features_batch.argtypes = [vp, i32, pp] + [i32] * 7 + [vp] * 5
     lib.ah_last_error.restype = ctypes.c_char_p
     for f in ("ah_example_identifiers", "ah_example_dfg", "ah_example_dfg_variant",
-              "ah_remove_comments",
+              "ah_remove_comments", "ah_gcb_features_batch",
               "ah_tokenizer_special", "ah_tokenize", "ah_decode", "ah_featurize_batch",
               "ah_featurize_batch_raw", "ah_tokens_to_ids",
               "ah_example_num_leaves", "ah_example_leaves", "ah_example_mutant_text",
@@ -60,6 +61,20 @@ def load_host_library(path=None) -> ctypes.CDLL:
         getattr(lib, f).restype = i32
     _LIB = lib
     return lib
+
+
+def gcb_threads() -> int:
+    """Worker threads of the batch featurisers: this process's CPU share (sched affinity), at
+    most 16 (the GPU box's share per GPU), overridable with APMC_HOST_THREADS."""
+    import os
+    env = os.environ.get("APMC_HOST_THREADS")
+    if env:
+        return max(1, int(env))
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
 
 
 def _err(what):
@@ -135,6 +150,26 @@ class Tokenizer:
         if n and fn(self.h, n, _cstrs(codes), L, _i32p(ids), _i32p(lens)) < 0:
             _err("ah_featurize_batch")
         return ids, lens
+
+    def gcb_features(self, codes: list[str], lang: str, variant: int, normalize: bool,
+                     code_length: int, data_flow_length: int, run_trunc: bool = False,
+                     threads: int | None = None, e_cap: int | None = None):
+        """GraphCodeBERT convert_code_to_features of each text on host worker threads, the graph
+        mask left compact (ah_gcb_features_batch): -> dict of ids, pos [n, L], meta [n, 4]
+        (node_index, max_length, nodes, edges), spans [n, L], edges [n, e_cap] int32."""
+        n, L = len(codes), code_length + data_flow_length
+        e_cap = e_cap or 4 * L
+        threads = threads or gcb_threads()
+        out = {"ids": np.empty((n, L), np.int32), "pos": np.empty((n, L), np.int32),
+               "meta": np.empty((n, 4), np.int32), "spans": np.empty((n, L), np.int32),
+               "edges": np.zeros((n, e_cap), np.int32)}
+        flags = (1 if normalize else 0) | (2 if run_trunc else 0)
+        if n and self.lib.ah_gcb_features_batch(
+                self.h, n, _cstrs(codes), LANG[lang], variant, flags, code_length,
+                data_flow_length, e_cap, threads, *(_i32p(out[k]) for k in
+                                                    ("ids", "pos", "meta", "spans", "edges"))) < 0:
+            _err("ah_gcb_features_batch")
+        return out
 
     def convert_tokens_to_ids(self, tokens):
         """tokenizer.convert_tokens_to_ids (a token string not in the vocabulary -> unk id)."""

@@ -77,6 +77,11 @@ def parse_args():
     return ap.parse_args()
 
 
+def log(msg):
+    """Progress on stderr (the JSON line alone goes to stdout): a long default run keeps writing."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def relaunch_as_ranks(args):
     """--gpus N outside torchrun: run N ranks via torch.distributed.run as a child process
     (started before this process touches the GPU) and exit with its status."""
@@ -447,6 +452,7 @@ def aa_leg(dev, n_examples, n_gcb, rank, world, precision):
     res["ga"] = summary(_gather_sum_max([out["examples"], out["total_cnt"], out["success"],
                                          out["queries"], out["wall_s"]], dev, world, 4))
     res["ga"]["mode"] = "greedy -> GA (attack.py), cross-example batched"
+    log("authorship leg: MHM-NS")
     margs = AttackArgs(block_size=512, eval_batch_size=64, seed=123456, task="authorship")
     mine = list(range(rank, len(codes), world))
     out = run_mhm_attack(model, codes, subs, labels, margs, indices=mine, max_iter=100,
@@ -456,6 +462,7 @@ def aa_leg(dev, n_examples, n_gcb, rank, world, precision):
     res["mhm"]["mode"] = "MHM-NS (mhm.py), cross-example batched chains"
     model.engine.close()
     if n_gcb > 0:
+        log("authorship leg: GraphCodeBERT GA")
         gargs = AttackArgs(block_size=512, eval_batch_size=32, seed=123456, rng="per_example",
                            task="gcb_authorship", code_length=512, data_flow_length=128)
         gmodel = GraphModel(sd, task="authorship", args=gargs, precision=precision,
@@ -655,21 +662,28 @@ def main():
         res["fp32_mode"] = fp32_mode
     eng.close()
     threads, phys = host_cores()
+    log(f"scoring step: {value:.1f} q/s")
     if args.attack_examples > 0:
+        log("config-2 attack leg")
         res["attack"] = attack_leg(dev, args.attack_examples, args.attack_deadline,
                                    args.attack_inflight, rank, world, args.precision)
     if rank == 0 and world == 1:
+        log("config-1 leg")
         res["config1"] = config1_leg(dev, args.precision, threads,
                                      0 if args.no_cpu_baseline else args.cpu_e2e_seconds)
     if args.subs_seconds > 0:
+        log("substitutes leg")
         res["substitutes"] = subs_leg(dev, args.subs_seconds, rank, world, args.precision)
     if args.aa_examples > 0:
+        log("authorship leg")
         res["authorship"] = aa_leg(dev, args.aa_examples, args.aa_gcb_examples, rank, world,
                                    args.precision)
     if args.mhm_examples > 0:
+        log("MHM-NS leg")
         res["mhm"] = mhm_leg(dev, args.mhm_examples, args.mhm_seq_examples, rank, world,
                              args.precision)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("CPU baseline")
         v, sample = cpu_baseline(L, args.cpu_seconds, threads)
         res["cpu_baseline"] = {"value": v, "unit": "victim queries/s", "cores": threads,
                                "kind": "port",

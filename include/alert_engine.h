@@ -33,6 +33,9 @@
  *                    (utils.py:237-239 get_bpe_substitues)
  *   ae_cosine_rank<- CosineSimilarity(dim=1) summed over the sub-word span / L_sub
  *                    (get_substitutes.py:75,108)
+ *   ae_graph_mask <- GraphCodeDataset.__getitem__'s bool [L, L] graph-guided attention mask
+ *                    (GraphCodeBERT/Defect-detection/code/utils.py:547-570 and the run.py
+ *                    TextDataset of each GraphCodeBERT task), built on the device
  *
  * Conventions
  *   - Every function returns 0 on success or a negative AE_E* code; the
@@ -176,6 +179,14 @@ int ae_topk(const float *x, int32_t rows, int32_t cols, int32_t k, float *vals_o
  *   ref  device float [span_len, hidden], cand device float [n, span_len, hidden]. */
 int ae_cosine_rank(const float *ref, const float *cand, int32_t n, int32_t span_len, int32_t hidden,
                    float eps, float *sims_out, void *stream);
+
+/* The bit-packed mask ae_score_graph reads (mask_bits device uint32 [n, L, L/32], bit j of word
+ * w = key 32 w + j) from the compact per-query features ah_gcb_features_batch emits (all device
+ * int32): ids [n, L]; meta [n, 4] = node_index, max_length, nodes, edges; spans [n, L] = node k's
+ * code span a | b << 16 or -1; edges [n, e_cap] = node | target << 16.  L % 32 == 0, L <= 1024. */
+int ae_graph_mask(const int32_t *ids, const int32_t *meta, const int32_t *spans,
+                  const int32_t *edges, int32_t n, int32_t L, int32_t e_cap, uint32_t *mask_bits,
+                  void *stream);
 
 /* Profiling of the dominant kernel: when enabled, the engine brackets every launch of kernel
  * class `kind` with HIP events on the launch stream.  ae_kernel_time synchronises and returns the

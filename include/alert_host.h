@@ -21,6 +21,12 @@
  *   ah_example_dfg_variant    <- the same, or GraphCodeBERT/{clonedetection,Authorship-Attribution}/code/run.py extract_dataflow
  *                                (parser/DFG.py + edge filter)
  *   ah_remove_comments        <- remove_comments_and_docstrings (parser_folder/utils.py:30-87)
+ *   ah_gcb_features_batch     <- GraphCodeBERT convert_code_to_features of many query texts
+ *                                (GraphCodeBERT/Defect-detection/code/attacker.py:30-63,
+ *                                 Authorship-Attribution/code/attacker.py:52-88,
+ *                                 clonedetection/code/attacker.py:33-72, run.py:148-192) with
+ *                                GraphCodeDataset's mask (utils.py:547-570) left compact for the
+ *                                device (ae_graph_mask)
  * All strings are UTF-8, NUL-terminated.  Functions return >= 0 on success (a count) or a
  * negative code; ah_last_error() describes the last failure of the calling thread.
  */
@@ -118,6 +124,24 @@ int32_t ah_example_dfg_variant(ah_example *ex, int32_t variant, int32_t *rows, i
 /* remove_comments_and_docstrings(code, 'c'|'java') (parser_folder/utils.py:30-87); returns
  * bytes needed incl. NUL. */
 int32_t ah_remove_comments(const char *code, char *out, int32_t cap);
+
+/* GraphCodeBERT query features of n texts, split over `threads` worker threads.
+ * flags: AH_GCB_NORMALIZE = ' '.join(code.split()) first (Devign); AH_GCB_RUN_TRUNC =
+ * clonedetection run.py's truncation (one token fewer, at most 509 code tokens).  With
+ * L = code_length + data_flow_length, per query i:
+ *   ids_out [n, L], pos_out [n, L]   input_ids, position_idx
+ *   meta_out [n, 4]                  node_index, max_length, nodes, edges
+ *   spans_out [n, L]                 node k's dfg_to_code span a | b << 16 if both < node_index,
+ *                                    else -1 (entries past the node count are -1)
+ *   edges_out [n, e_cap]             node | target << 16 of dfg_to_dfg (column inside L)
+ * Returns n, or -1 (ah_last_error) e.g. when a query has more than e_cap edges. */
+#define AH_GCB_NORMALIZE 1
+#define AH_GCB_RUN_TRUNC 2
+int32_t ah_gcb_features_batch(ah_tokenizer *tok, int32_t n, const char *const *codes, int32_t lang,
+                              int32_t variant, int32_t flags, int32_t code_length,
+                              int32_t data_flow_length, int32_t e_cap, int32_t threads,
+                              int32_t *ids_out, int32_t *pos_out, int32_t *meta_out,
+                              int32_t *spans_out, int32_t *edges_out);
 
 const char *ah_last_error(void);
 

@@ -196,3 +196,74 @@ def test_engine_graph_forward_matches_transformers_golden(precision):
                        precision=precision)
         got = m.score_packed(g["gcb_ids"], g["gcb_pos"], g["gcb_bits"])
         np.testing.assert_allclose(got, g[f"gcb_{name}_probs"], atol=PROB_TOL, rtol=0)
+
+
+def _task_texts(task, n):
+    from apmc_amd.drivers import load_fixture
+    path = {"devign": ROOT / "data" / "devign" / "test_subs_0_400.jsonl",
+            "clone": ROOT / "data" / "clone" / "test_subs_0_500.jsonl",
+            "authorship": ROOT / "data" / "authorship" / "valid_subs.jsonl"}[task]
+    codes, _, _ = load_fixture(path, 0, n)
+    if task == "clone":
+        return [c[2] for c in codes] + [c[3] for c in codes]
+    return codes
+
+
+@pytest.mark.parametrize("task,run_trunc", [("devign", False), ("clone", False), ("clone", True),
+                                            ("authorship", False)])
+def test_batch_featuriser_matches_python_features(task, run_trunc):
+    """ah_gcb_features_batch (C++, worker threads) against graph.py convert_code_to_features on
+    fixture texts of every GraphCodeBERT task (language, whitespace rule, data-flow builder, the
+    clone run.py truncation): identical ids / positions / node count, and the mask rebuilt from
+    the compact spans + edges equals GraphCodeDataset's bool mask."""
+    import _apmc  # noqa: F401
+    from apmc_amd.drivers import AttackArgs
+    from apmc_amd.graph import DFG_GCB_RUN, TASK_FEATURES, convert_code_to_features, \
+        graph_mask, graph_mask_from_compact
+    from apmc_amd.host import Tokenizer
+
+    tok = Tokenizer()
+    args = AttackArgs(code_length=512, data_flow_length=128)
+    texts = _task_texts(task, 30)
+    lang, normalize, variant = TASK_FEATURES[task]
+    if run_trunc:
+        variant = DFG_GCB_RUN
+    c = tok.gcb_features(texts, lang, variant, normalize, 512, 128, run_trunc=run_trunc, threads=3)
+    for i, t in enumerate(texts):
+        f = convert_code_to_features(t, tok, 0, args, lang, normalize, variant=variant,
+                                     run_trunc=run_trunc)
+        assert c["ids"][i].tolist() == f.input_ids, i
+        assert c["pos"][i].tolist() == f.position_idx, i
+        assert c["meta"][i][2] == len(f.dfg_to_code), i
+        m = graph_mask(f.input_ids, f.position_idx, f.dfg_to_code, f.dfg_to_dfg)
+        m2 = graph_mask_from_compact(c["ids"][i], c["meta"][i], c["spans"][i], c["edges"][i])
+        assert (m == m2).all(), i
+
+
+@pytest.mark.gpu
+def test_device_graph_mask_matches_host(gpu):
+    """ae_graph_mask (rowops.hip) builds exactly pack_mask(graph_mask) of every query, for the
+    three tasks' fixture texts (L = 640) and a short L = 96 case."""
+    import torch
+
+    import _apmc  # noqa: F401
+    from apmc_amd.engine import Engine
+    from apmc_amd.graph import TASK_FEATURES, graph_mask_from_compact, pack_mask
+    from apmc_amd.host import Tokenizer
+    from apmc_amd.weights import RobertaShape, synthetic_state_dict
+
+    tok = Tokenizer()
+    shape = RobertaShape(layers=1)
+    eng = Engine(synthetic_state_dict(seed=1, shape=shape, head="sigmoid1"), head="sigmoid1",
+                 num_labels=1, shape=shape, precision="fp32")
+    for task in ("devign", "clone", "authorship"):
+        lang, normalize, variant = TASK_FEATURES[task]
+        for cl, dfl in ((512, 128), (64, 32)):
+            c = tok.gcb_features(_task_texts(task, 12), lang, variant, normalize, cl, dfl)
+            t = {k: torch.from_numpy(v).cuda() for k, v in c.items()}
+            bits = eng.graph_mask(t["ids"], t["meta"], t["spans"], t["edges"]).cpu().numpy()
+            for i in range(len(c["ids"])):
+                ref = pack_mask(graph_mask_from_compact(c["ids"][i], c["meta"][i], c["spans"][i],
+                                                        c["edges"][i]))
+                assert (bits[i] == ref).all(), (task, cl, i)
+    eng.close()

@@ -3,7 +3,7 @@ lib/libalert_engine.so (not part of the public C-ABI; the engine tests cover the
 
 Packed-plane GEMM (gemm_planes.hip): C = A·W^T over packed bf16 planes must equal the float64 sum
 of the split products A_hi·W_hi + A_hi·W_lo + A_lo·W_hi (f32 accumulation: |Δ| ≤ 1e-5·Σ|a||w|), for
-ragged M, both tile widths, the ping-pong 256 x 256 kernel, both plane counts and every
+ragged M, both tile widths, the ping-pong 256 x 256 and 256 x 192 kernels, both plane counts and every
 epilogue."""
 import ctypes
 
@@ -67,6 +67,13 @@ def _p(t):
     (700, 256, 256, 1, 1, "512"),
     (64, 2304, 768, 2, 3, "512"),
     (600, 3072, 768, 2, 1, "512"),
+    # ping-pong 256 x 192 kernel (f32 epilogues): ragged M / N, short and long K
+    (300, 768, 128, 2, 0, "192"),
+    (512, 768, 768, 2, 2, "192"),
+    (1000, 384, 64, 1, 3, "192"),
+    (64, 768, 3072, 2, 2, "192"),
+    (257, 192, 192, 1, 0, "192"),
+    (700, 576, 256, 2, 2, "192"),
 ])
 def test_gemm_packed_matches_split_products(gpu, M, N, K, np_, epi, bn):
     lib = _lib()

@@ -146,6 +146,10 @@ def host_graph_victim(score, base):
         def score_packed(self, ids, pos, bits):
             return np.asarray(score(ids, pos, bits))
 
+        def score_payload_rows(self, live):  # compact masks rebuilt on the host
+            from apmc_amd.graph import payload_rows_host
+            return self.score_packed(*payload_rows_host(live))
+
     return HostGraphVictim()
 
 
