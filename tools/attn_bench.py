@@ -1,0 +1,112 @@
+"""Microbenchmark + parity check of the split-bf16 fused attention kernels (GPU).
+
+Random qkv [T, 2304] (f32, the QKV GEMM's output layout) over n sequences of length L (ragged
+with --ragged), every variant of ae_bench_attention_x3 timed with HIP events in interleaved rounds
+in one process, and checked against a float64 torch reference of the same attention (softmax of
+Q·K^T/8 over each sequence's keys, times V).  One JSON line per variant: median / min µs per
+launch, the algorithmic TFLOP/s (4·len²·64 per (sequence, head)) and max |out - ref|.
+
+  python tools/attn_bench.py [--n 64] [--L 512] [--variants 0,1] [--terms 3] [--ragged]
+"""
+import argparse
+import ctypes
+import json
+import pathlib
+import statistics
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+import torch  # noqa: E402
+
+import _apmc  # noqa: E402,F401
+
+H, HEADS, D = 768, 12, 64
+
+
+def reference(qkv, cu, n):
+    outs = []
+    for s in range(n):
+        a, b = int(cu[s]), int(cu[s + 1])
+        x = qkv[a:b].double()
+        q = x[:, :H].view(-1, HEADS, D).transpose(0, 1)
+        k = x[:, H:2 * H].view(-1, HEADS, D).transpose(0, 1)
+        v = x[:, 2 * H:].view(-1, HEADS, D).transpose(0, 1)
+        p = torch.softmax(q @ k.transpose(1, 2) / 8.0, dim=-1)
+        outs.append((p @ v).transpose(0, 1).reshape(b - a, H))
+    return torch.cat(outs)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=64)
+    ap.add_argument("--L", type=int, default=512)
+    ap.add_argument("--variants", default="0")
+    ap.add_argument("--terms", type=int, default=3)
+    ap.add_argument("--ragged", action="store_true")
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--check-seqs", type=int, default=8)
+    args = ap.parse_args()
+
+    from apmc_amd.engine import load_library
+    lib = load_library()
+    vp, i32 = ctypes.c_void_p, ctypes.c_int32
+    fn = lib.ae_bench_attention_x3
+    fn.argtypes = [vp] * 5 + [i32] * 3 + [vp, i32, i32, i32, vp]
+    fn.restype = ctypes.c_int
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream(dev)
+    sp = ctypes.c_void_p(st.cuda_stream)
+    g = torch.Generator().manual_seed(0)
+    n, L = args.n, args.L
+    if args.ragged:
+        lens = torch.randint(L // 4, L + 1, (n,), generator=g)
+    else:
+        lens = torch.full((n,), L)
+    cu = torch.zeros(n + 1, dtype=torch.int32)
+    cu[1:] = torch.cumsum(lens, 0)
+    T = int(cu[-1])
+    qkv = (torch.randn((T, 3 * H), generator=g) * 1.5).to(dev)
+    cu_d = cu.to(dev)
+    flop = float(sum(4.0 * int(x) ** 2 * D * HEADS for x in lens))
+    cs = min(args.check_seqs, n)
+    ref = reference(qkv[:int(cu[cs])], cu, cs)
+
+    def p(t):
+        return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(None)
+
+    cases = []
+    for v in args.variants.split(","):
+        var = int(v)
+        out = torch.zeros((T, H), device=dev)
+        call = (lambda out=out, var=var: fn(p(qkv), p(out), p(None), p(cu_d), p(None), int(lens.max()),
+                                            n, HEADS, p(None), 0, args.terms, var, sp))
+        rc = call()
+        torch.cuda.synchronize()
+        if rc != 0:
+            print(json.dumps({"variant": var, "error": rc}))
+            continue
+        err = float((out[:int(cu[cs])].double() - ref).abs().max())
+        cases.append(dict(variant=var, call=call, t=[], err=err))
+    for _ in range(args.rounds):
+        for c in cases:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            c["call"]()
+            e0.record(st)
+            for _ in range(args.iters):
+                c["call"]()
+            e1.record(st)
+            e1.synchronize()
+            c["t"].append(e0.elapsed_time(e1) * 1e3 / args.iters)
+    for c in cases:
+        med, mn = statistics.median(c["t"]), min(c["t"])
+        print(json.dumps({"variant": c["variant"], "n": n, "L": L, "ragged": args.ragged,
+                          "terms": args.terms, "us_median": round(med, 2), "us_min": round(mn, 2),
+                          "tflops_median": round(flop / med / 1e6, 1),
+                          "max_abs_err_vs_f64": c["err"]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
