@@ -18,6 +18,7 @@
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
 namespace {
 constexpr int QPB = 128, KT = 32;
@@ -25,16 +26,28 @@ constexpr int K_ROWB = 128;          // 64 d bf16 per key row
 constexpr int K_PLANE = KT * K_ROWB; // 4 KiB
 constexpr int VT_ROWB = 72;          // 32 keys bf16 + 8 B pad
 constexpr int VT_PLANE = 64 * VT_ROWB;
-constexpr int STAGE = 2 * K_PLANE + 2 * VT_PLANE;  // hi/lo planes of K and V^T
+constexpr int V_PLANE = KT * K_ROWB;  // row-major V (VAR_VTR): 64 d bf16 per key row
 constexpr int OSTRIDE = 65;
-constexpr int LDS_BYTES = (2 * STAGE > 4 * 32 * OSTRIDE * 4) ? 2 * STAGE : 4 * 32 * OSTRIDE * 4;
+template <int VAR>
+constexpr int stage_bytes() { return 2 * K_PLANE + 2 * ((VAR & 1) ? V_PLANE : VT_PLANE); }
+template <int VAR>
+constexpr int lds_bytes() {
+  return (2 * stage_bytes<VAR>() > 4 * 32 * OSTRIDE * 4) ? 2 * stage_bytes<VAR>() : 4 * 32 * OSTRIDE * 4;
+}
 
 __device__ __forceinline__ int kswz(int key, int chunk) { return chunk ^ (key & 7); }
+// row-major V image: 16-B chunk c of key row r at c ^ 4 ((r >> 1) & 1), so the 4 rows of a
+// ds_read_b64_tr_b16 block (keys 4m .. 4m+3) land on 4 distinct 16-bank ranges of a 32-lane half
+__device__ __forceinline__ int vswz(int key, int chunk) { return chunk ^ (((key >> 1) & 1) << 2); }
 }  // namespace
 
+// Variant bits (VAR): 1 = V stored row-major and fed to the PV MFMA through the hardware
+// transposed read ds_read_b64_tr_b16 (4-key x 16-d blocks; replaces the transposing 2-byte LDS
+// scatter), 2 = exp2 domain (log2 e folded into the Q scale) and the O rescale skipped when no
+// lane's running max moved (alpha == 1 exactly: the skip changes no bit).
 // PLANES: write the context as packed bf16 planes (hi = bf16(o), lo = bf16(o - hi); layout of
 // gemm_planes.hip) for the O-projection instead of f32 rows in out.
-template <int TERMS, bool HAS_MASK, bool PLANES>
+template <int TERMS, bool HAS_MASK, bool PLANES, int VAR>
 __global__ __launch_bounds__(256, 2) void attn_x3_kernel(const float* __restrict__ qkv,
                                                          float* __restrict__ out,
                                                          unsigned short* __restrict__ op,
@@ -42,7 +55,9 @@ __global__ __launch_bounds__(256, 2) void attn_x3_kernel(const float* __restrict
                                                          const int* __restrict__ q_rows,
                                                          const uint32_t* __restrict__ mask,
                                                          int mask_L) {
-  __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
+  constexpr bool VTR = VAR & 1, EXP2 = VAR & 2;
+  constexpr int STAGE = stage_bytes<VAR>();
+  __shared__ __attribute__((aligned(16))) unsigned char lds[lds_bytes<VAR>()];
   const int seq = blockIdx.z, head = blockIdx.y, qb = blockIdx.x;
   const int start = cu[seq];
   const int len = cu[seq + 1] - start;
@@ -65,7 +80,8 @@ __global__ __launch_bounds__(256, 2) void attn_x3_kernel(const float* __restrict
       const floatx4 b = *reinterpret_cast<const floatx4*>(qp + 16 * s + 8 * lh + 4);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float v = (e < 4 ? a[e] : b[e - 4]) * 0.125f;
+        // 1/sqrt(64) (and log2 e in the exp2 domain)
+        const float v = (e < 4 ? a[e] : b[e - 4]) * (EXP2 ? 0.18033688011112042f : 0.125f);
         const __bf16 h = (__bf16)v;
         qh[s][e] = h;
         ql[s][e] = (__bf16)(v - (float)h);
@@ -102,6 +118,19 @@ __global__ __launch_bounds__(256, 2) void attn_x3_kernel(const float* __restrict
       const int off = key * K_ROWB + kswz(key, st_c4 >> 1) * 16 + (st_c4 & 1) * 8;
       *reinterpret_cast<bf16x4*>(st + off) = kh;
       if (TERMS == 3) *reinterpret_cast<bf16x4*>(st + K_PLANE + off) = kl;
+      if (VTR) {  // V row-major: the same 8 B per plane as K
+        bf16x4 vh, vl;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const __bf16 h = (__bf16)rv[i][e];
+          vh[e] = h;
+          vl[e] = (__bf16)(rv[i][e] - (float)h);
+        }
+        const int voff = key * K_ROWB + vswz(key, st_c4 >> 1) * 16 + (st_c4 & 1) * 8;
+        *reinterpret_cast<bf16x4*>(st + 2 * K_PLANE + voff) = vh;
+        if (TERMS == 3) *reinterpret_cast<bf16x4*>(st + 2 * K_PLANE + V_PLANE + voff) = vl;
+        continue;
+      }
       // V^T: element (key, d) -> row d, column key
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -152,30 +181,43 @@ __global__ __launch_bounds__(256, 2) void attn_x3_kernel(const float* __restrict
     uint32_t mbits = 0xffffffffu;
     if (HAS_MASK) mbits = mrow[kt];
     float mt = -INFINITY;
+    // (EXP2 variants: a full tile without a mask needs no per-key select; the branch is
+    // wave-uniform)
+    if (EXP2 && !HAS_MASK && (kt + 1) * KT <= len) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int kk = mfma32_row(r, lh);
-      // absent keys (beyond the sequence) are -inf; keys the mask excludes score the most
-      // negative finite float, as HF's additive finfo(f32).min mask does: a query row that
-      // excludes every key then attends all of them uniformly (GraphCodeBERT truncated nodes)
-      const bool in = kt * KT + kk < len;
-      s[r] = !in ? -INFINITY : (((mbits >> kk) & 1u) ? s[r] : -FLT_MAX);
-      mt = fmaxf(mt, s[r]);
+      for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[r]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kk = mfma32_row(r, lh);
+        // absent keys (beyond the sequence) are -inf; keys the mask excludes score the most
+        // negative finite float, as HF's additive finfo(f32).min mask does: a query row that
+        // excludes every key then attends all of them uniformly (GraphCodeBERT truncated nodes)
+        const bool in = kt * KT + kk < len;
+        s[r] = !in ? -INFINITY : (((mbits >> kk) & 1u) ? s[r] : -FLT_MAX);
+        mt = fmaxf(mt, s[r]);
+      }
     }
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
     const float m_new = fmaxf(m_run, mt);
-    const float alpha = (m_run == -INFINITY) ? 0.f : __expf(m_run - m_new);
+    const float alpha = (m_run == -INFINITY) ? 0.f
+                        : EXP2                ? __builtin_amdgcn_exp2f(m_run - m_new)
+                                              : __expf(m_run - m_new);
     float psum = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float p = (s[r] == -INFINITY) ? 0.f : __expf(s[r] - m_new);
+      // exp2(-inf - m) = 0 for finite m; m_new is finite once any key of the row is present
+      const float p = EXP2 ? __builtin_amdgcn_exp2f(s[r] - m_new)
+                           : ((s[r] == -INFINITY) ? 0.f : __expf(s[r] - m_new));
       s[r] = p;
       psum += p;
     }
     l_run = l_run * alpha + psum;
     m_run = m_new;
+    if (!EXP2 || __any(alpha != 1.f)) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+    }
 
     // ---- O^T += V^T P^T (2 k-steps of 16 keys, 2 d-tiles)
 #pragma unroll
@@ -192,20 +234,40 @@ __global__ __launch_bounds__(256, 2) void attn_x3_kernel(const float* __restrict
       const int k0 = 16 * t + 4 * lh;
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
-        const int d = dt * 32 + li;
-        const unsigned char* vrow = st + 2 * K_PLANE + d * VT_ROWB;
         bf16x8 vh, vl;
-        {
-          const bf16x4 a = *reinterpret_cast<const bf16x4*>(vrow + 2 * k0);
-          const bf16x4 b = *reinterpret_cast<const bf16x4*>(vrow + 2 * (k0 + 8));
+        if (VTR) {
+          // lane 16g + 4q + p addresses key row k0 + q (and k0 + 8 + q), d columns
+          // 32 dt + 16 (g & 1) + 4p; it receives d = 32 dt + (lane & 31) of those 4 keys
+          const int kq = k0 + ((lane >> 2) & 3);
+          const int col = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+          const unsigned char* vb = st + 2 * K_PLANE + (col & 7) * 2;
+          const int o_a = kq * K_ROWB + vswz(kq, col >> 3) * 16;
+          const int o_b = (kq + 8) * K_ROWB + vswz(kq + 8, col >> 3) * 16;
+          const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(vb + o_a));
+          const bf16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(vb + o_b));
 #pragma unroll
           for (int e = 0; e < 4; ++e) { vh[e] = a[e]; vh[4 + e] = b[e]; }
-        }
-        if (TERMS == 3) {
-          const bf16x4 a = *reinterpret_cast<const bf16x4*>(vrow + VT_PLANE + 2 * k0);
-          const bf16x4 b = *reinterpret_cast<const bf16x4*>(vrow + VT_PLANE + 2 * (k0 + 8));
+          if (TERMS == 3) {
+            const bf16x4 c = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(vb + V_PLANE + o_a));
+            const bf16x4 d = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(vb + V_PLANE + o_b));
 #pragma unroll
-          for (int e = 0; e < 4; ++e) { vl[e] = a[e]; vl[4 + e] = b[e]; }
+            for (int e = 0; e < 4; ++e) { vl[e] = c[e]; vl[4 + e] = d[e]; }
+          }
+        } else {
+          const int d = dt * 32 + li;
+          const unsigned char* vrow = st + 2 * K_PLANE + d * VT_ROWB;
+          {
+            const bf16x4 a = *reinterpret_cast<const bf16x4*>(vrow + 2 * k0);
+            const bf16x4 b = *reinterpret_cast<const bf16x4*>(vrow + 2 * (k0 + 8));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { vh[e] = a[e]; vh[4 + e] = b[e]; }
+          }
+          if (TERMS == 3) {
+            const bf16x4 a = *reinterpret_cast<const bf16x4*>(vrow + VT_PLANE + 2 * k0);
+            const bf16x4 b = *reinterpret_cast<const bf16x4*>(vrow + VT_PLANE + 2 * (k0 + 8));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { vl[e] = a[e]; vl[4 + e] = b[e]; }
+          }
         }
         floatx16& o = dt == 0 ? o0 : o1;
         if (TERMS == 3) {
@@ -249,15 +311,15 @@ __global__ __launch_bounds__(256, 2) void attn_x3_kernel(const float* __restrict
   }
 }
 
-extern "C" hipError_t ae_launch_attention_x3(const float* qkv, float* out, unsigned short* op,
-                                             const int* cu,
-                                             const int* q_rows, int max_q, int n, int heads,
-                                             const uint32_t* mask, int mask_L, int terms,
-                                             hipStream_t stream) {
+namespace {
+template <int VAR>
+hipError_t attn_launch(const float* qkv, float* out, unsigned short* op, const int* cu,
+                       const int* q_rows, int max_q, int n, int heads, const uint32_t* mask,
+                       int mask_L, int terms, hipStream_t stream) {
   if (n <= 0 || max_q <= 0) return hipSuccess;
   dim3 grid((max_q + QPB - 1) / QPB, heads, n), block(256);
 #define ATT_LAUNCH(T, M, P)                                                                  \
-  hipLaunchKernelGGL((attn_x3_kernel<T, M, P>), grid, block, 0, stream, qkv, out, op, cu,     \
+  hipLaunchKernelGGL((attn_x3_kernel<T, M, P, VAR>), grid, block, 0, stream, qkv, out, op, cu, \
                      q_rows, mask, mask_L)
 #define ATT_MP(T)                                              \
   if (op) {                                                    \
@@ -273,4 +335,30 @@ extern "C" hipError_t ae_launch_attention_x3(const float* qkv, float* out, unsig
 #undef ATT_MP
 #undef ATT_LAUNCH
   return hipGetLastError();
+}
+constexpr int ATT_VAR = 3;  // production variant (tools/attn_bench.py A/B: 227 -> 192 us at B=64, L=512)
+}  // namespace
+
+extern "C" hipError_t ae_launch_attention_x3(const float* qkv, float* out, unsigned short* op,
+                                             const int* cu,
+                                             const int* q_rows, int max_q, int n, int heads,
+                                             const uint32_t* mask, int mask_L, int terms,
+                                             hipStream_t stream) {
+  return attn_launch<ATT_VAR>(qkv, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, terms,
+                              stream);
+}
+
+// Kernel experiments (tools/attn_bench.py): the variant bits of attn_x3_kernel (0..3).  Every
+// variant computes the same attention; not part of include/alert_engine.h.
+extern "C" hipError_t ae_bench_attention_x3(const float* qkv, float* out, unsigned short* op,
+                                            const int* cu, const int* q_rows, int max_q, int n,
+                                            int heads, const uint32_t* mask, int mask_L, int terms,
+                                            int variant, hipStream_t stream) {
+  switch (variant) {
+    case 0: return attn_launch<0>(qkv, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, terms, stream);
+    case 1: return attn_launch<1>(qkv, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, terms, stream);
+    case 2: return attn_launch<2>(qkv, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, terms, stream);
+    case 3: return attn_launch<3>(qkv, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, terms, stream);
+    default: return hipErrorInvalidValue;
+  }
 }

@@ -31,27 +31,21 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
 }
 
-// exact-erf GELU through a rational erfc: erfc(z) = t·exp(-z² + P(t)), t = 1/(1 + z/2), the
-// 10-term Chebyshev fit of Numerical Recipes (fractional error < 1.2e-7).  Over [-12, 12] it is
-// within 3.9e-7 absolute / 2.4e-6 relative of the float64 GELU (torch's f32 GELU: 1.2e-6
-// absolute), branch-free, ~20 VALU instead of erff's piecewise series — the split-precision
-// FFN1 epilogue is VALU-bound on this (tools/gemm_bench.py diag 6).
+// exact-erf GELU through a rational erfc (Abramowitz & Stegun 7.1.26, |erf error| <= 1.5e-7):
+// erfc(z) = t·P5(t)·exp(-z²), t = 1/(1 + 0.3275911 z), z = |x|/√2, so GELU(x) = x - h (x >= 0) or
+// h (x < 0) with h = x·erfc(z)/2.  Over [-12, 12] it is within 3.3e-7 absolute of the float64
+// GELU (torch's f32 GELU: 1.2e-6 absolute), branch-free, 5 Horner FMAs + rcp + exp2 — the
+// split-precision FFN1 epilogue is VALU-bound on this (tools/gemm_bench.py diag 4 vs 0).
 __device__ __forceinline__ float gelu_erfc_fast(float x) {
-  const float z = fabsf(x) * 0.70710678118654752440f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.0f));
-  float p = 0.17087277f;
-  p = fmaf(p, t, -0.82215223f);
-  p = fmaf(p, t, 1.48851587f);
-  p = fmaf(p, t, -1.13520398f);
-  p = fmaf(p, t, 0.27886807f);
-  p = fmaf(p, t, -0.18628806f);
-  p = fmaf(p, t, 0.09678418f);
-  p = fmaf(p, t, 0.37409196f);
-  p = fmaf(p, t, 1.00002368f);
-  p = fmaf(p, t, -1.26551223f);
-  const float ec = t * __expf(fmaf(-z, z, p));  // erfc(|x| / sqrt 2)
-  const float phi = x >= 0.f ? fmaf(-0.5f, ec, 1.0f) : 0.5f * ec;
-  return x * phi;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.23164190207799160f, fabsf(x), 1.0f));
+  float p = 1.061405429f;
+  p = fmaf(p, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float e = __builtin_amdgcn_exp2f((x * -0.72134752044448170f) * x);  // exp(-x²/2)
+  const float h = (0.5f * x) * ((p * t) * e);
+  return x >= 0.f ? x - h : h;
 }
 
 // bf16 round-to-nearest-even of an f32 (NaN-preserving cast lowered to v_cvt_pk_bf16_f32).

@@ -120,3 +120,77 @@ def test_gemm_packed_matches_split_products(gpu, M, N, K, np_, epi, bn):
     assert torch.isfinite(got).all()
     err = (got - ref).abs()
     assert (err <= tol).all(), float((err - tol).max())
+
+
+def _attn_ref(qkv, cu, n, mask=None, L=0, q_rows=None):
+    """float64 attention per (sequence, head): softmax(Q·K^T/8 (+ finfo.min where the bit-packed
+    mask excludes a key)) · V over each sequence's keys; [T, 768]."""
+    H, heads, D = 768, 12, 64
+    outs = []
+    for s in range(n):
+        a, b = int(cu[s]), int(cu[s + 1])
+        x = qkv[a:b].double()
+        q = x[:, :H].view(-1, heads, D).transpose(0, 1)
+        k = x[:, H:2 * H].view(-1, heads, D).transpose(0, 1)
+        v = x[:, 2 * H:].view(-1, heads, D).transpose(0, 1)
+        sc = q @ k.transpose(1, 2) / 8.0
+        if mask is not None:
+            words = mask[s].view(L, L // 32)[: b - a]
+            bits = ((words.unsqueeze(-1) >> torch.arange(32)) & 1).reshape(b - a, L)[:, : b - a]
+            sc = sc + (bits == 0).double() * torch.finfo(torch.float32).min
+        o = (torch.softmax(sc, dim=-1) @ v).transpose(0, 1).reshape(b - a, H)
+        outs.append(o)
+    return torch.cat(outs)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("case", ["ragged", "mask", "cls", "planes"])
+def test_attention_x3_variants_match_f64(gpu, variant, case):
+    """attn_x3_kernel (every variant bit: transposed-read V, exp2 + rescale skip) against a float64
+    reference: ragged lengths (1..300, one tile boundary each side), the GraphCodeBERT bit mask
+    (incl. a fully-masked query row -> uniform over the keys, HF's finfo.min semantics), the
+    CLS-only query launch of the last layer and the packed-plane context output."""
+    lib = _lib()
+    vp, i32 = ctypes.c_void_p, ctypes.c_int32
+    lib.ae_bench_attention_x3.argtypes = [vp] * 5 + [i32] * 3 + [vp, i32, i32, i32, vp]
+    lib.ae_bench_attention_x3.restype = ctypes.c_int
+    g = torch.Generator().manual_seed(7 + variant)
+    lens = [1, 31, 32, 33, 129, 300, 64] if case != "mask" else [40, 97, 128]
+    n = len(lens)
+    cu = torch.zeros(n + 1, dtype=torch.int32)
+    cu[1:] = torch.cumsum(torch.tensor(lens), 0)
+    T = int(cu[-1])
+    qkv = torch.randn(T, 3 * 768, generator=g)
+    L, mask, dmask = 0, None, None
+    if case == "mask":
+        L = 128
+        dense = (torch.rand(n, L, L, generator=g) < 0.6)
+        dense[:, :, 0] = True
+        dense[1, 5, :] = False  # a query row that excludes every key
+        words = (dense.view(n, L, L // 32, 32).long() << torch.arange(32)).sum(-1)
+        mask = words
+        dmask = (words - (words >= 2 ** 31).long() * 2 ** 32).to(torch.int32).cuda()
+    ref = _attn_ref(qkv, cu, n, mask, L)
+    dq, dcu = qkv.cuda(), cu.cuda()
+    out = torch.full((T, 768), float("nan"), device="cuda")
+    op = torch.zeros((T, 2 * 768), dtype=torch.bfloat16, device="cuda") if case == "planes" else None
+    one = torch.ones(1, dtype=torch.int32, device="cuda") if case == "cls" else None
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    rc = lib.ae_bench_attention_x3(_p(dq), _p(out), _p(op), _p(dcu), _p(one),
+                                   1 if case == "cls" else max(lens), n, 12, _p(dmask), L, 3,
+                                   variant, st)
+    assert rc == 0
+    torch.cuda.synchronize()
+    # split-bf16 products carry ~2^-16 relative error: ~1e-4 on these scores; layout errors are O(1)
+    if case == "planes":
+        got = _unpack(op.cpu(), 2, 768)
+        tol = 2e-4 + 2e-5 * ref.abs()
+    else:
+        got = out.double().cpu()
+        tol = 2e-4
+    if case == "cls":
+        rows = cu[:-1].long()
+        got, ref = got[rows], ref[rows]
+    assert torch.isfinite(got).all()
+    err = (got - ref).abs()
+    assert (err <= tol).all(), float(err.max())
