@@ -427,6 +427,17 @@ class CTree {
 
   // declaration body after the specifiers: declarators (with initialisers) up to ';'
   void init_declarators(int decl, size_t limit) {
+    // `uint32_t av_unused auxtag;`, `struct {...} QEMU_PACKED name;`: two identifiers then ';' as
+    // the first declarator — tree-sitter keeps the first as the declarator and puts the second in
+    // an ERROR node (fixture keys: av_unused / QEMU_PACKED defined, auxtag / name not; after a
+    // ',' or with '=' / '*' following, the second identifier is the declarator: declarator())
+    if (p_ + 2 < limit && is_ident(t(p_)) && is_ident(t(p_ + 1)) && t(p_ + 2) == ";") {
+      attach(decl, leaf_node(p_++));
+      const int err = make(N_GENERIC);
+      attach(decl, err);
+      add_leaf(err, p_++);
+      return;
+    }
     while (p_ < limit && !at(";")) {
       const size_t before = p_;
       const int d = declarator(false);
@@ -773,6 +784,19 @@ class CTree {
     // declaration of its own (an identifier directly under a declaration) and the function
     // definition starts at the type keyword that follows
     if (p_ + 1 < n_ && is_ident(t(p_)) && type_start(p_ + 1)) {
+      add_leaf(d, p_++);
+      attach(parent, d);
+      return;
+    }
+    // `uint32_t av_unused auxtag;`, `struct {...} QEMU_PACKED name;`: two identifiers then ';'
+    // as the first declarator — tree-sitter keeps the first as the declarator and puts the
+    // second in an ERROR node (fixture keys: av_unused / QEMU_PACKED defined, auxtag / name not;
+    // with '=' or '*' after the second identifier it is the declarator instead, below)
+    if (p_ + 2 < n_ && is_ident(t(p_)) && is_ident(t(p_ + 1)) && t(p_ + 2) == ";") {
+      attach(d, leaf_node(p_++));
+      const int err = make(N_GENERIC);
+      attach(d, err);
+      add_leaf(err, p_++);
       add_leaf(d, p_++);
       attach(parent, d);
       return;
