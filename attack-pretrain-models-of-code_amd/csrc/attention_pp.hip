@@ -1,0 +1,310 @@
+// attention_pp.hip — the fused attention of the split-precision modes over packed bf16 planes.
+//
+// attn_x3_kernel's algorithm (128 queries of one (sequence, head) per workgroup, the query on the
+// lane, online softmax in the exp2 domain, optional bit-packed data-flow mask), fed by the QKV
+// GEMM's packed-plane output (gemm_planes.hip PK_EPI_BIAS_PACKED: per 32 columns a block
+// [hi 32 | lo 32] for NP = 2, plain bf16 for NP = 1) instead of f32:
+//   * Q is read once as planes; its softmax scale log2(e)/8 is folded into Wq and bq at engine
+//     creation, so the kernel converts and scales nothing;
+//   * a key's 64 d of K (or V) are one contiguous 128·NP-byte run of its token row, so a 32-key
+//     tile moves global -> LDS by LDS-DMA (global_load_lds_dwordx4, 4 key rows of 256 B per wave
+//     instruction for NP = 2) into a double-buffered stage, with no register staging and no
+//     hi/lo split in the loop;
+//   * the DMA picks each lane's source chunk so that LDS position c of key row r holds logical
+//     chunk c ^ swizzle(r): K rows (read by ds_read_b128, one key row per lane) XOR by the row's
+//     low bits, V rows (read by ds_read_b64_tr_b16 in 4-key blocks) by (r & 3) << 2, both
+//     conflict-free for their reads;
+//   * S^T = K·Q^T and O^T += V^T·P^T on v_mfma_f32_32x32x16_bf16, 3 products per term pair for
+//     NP = 2 (x_hi·y_hi + x_hi·y_lo + x_lo·y_hi), P split into hi/lo from the S accumulator.
+#include <cfloat>
+
+#include "common.h"
+
+// m0 is written only by dma16 below; nothing else in this kernel reads it
+#pragma clang diagnostic ignored "-Winline-asm"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+namespace {
+constexpr int QPB = 128, KT = 32, OSTRIDE = 65;
+constexpr int QKV_COLS = 3 * AE_HIDDEN;
+
+// One LDS-DMA wave instruction: 64 lanes x 16 B from per-lane global addresses into
+// lds_base + 16 * lane (SALU write of m0 -> LDS-DMA needs one wait state).
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_base) {
+  asm volatile(
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %0, off"
+      :
+      : "v"(gsrc), "s"(lds_base)
+      : "memory", "m0");
+}
+
+template <int NP>
+struct PPL {
+  static constexpr int RB = 128 * NP;             // bytes of one key's 64 d (NP planes)
+  static constexpr int CR = RB / 16;              // 16-B chunks per key row
+  static constexpr int TILE = KT * RB;            // K (or V) tile
+  static constexpr int STAGE = 2 * TILE;          // K then V
+  static constexpr int ROWS_PER_DMA = 1024 / RB;  // key rows per wave DMA instruction
+  static constexpr int DMA_PER_WAVE = KT / ROWS_PER_DMA / 4;  // per matrix, 4 waves
+  static constexpr int LDS =
+      (2 * STAGE > 4 * 32 * OSTRIDE * 4) ? 2 * STAGE : 4 * 32 * OSTRIDE * 4;
+};
+
+// logical 16-B chunk of (plane p, d) in a key row: block d / 32 holds [hi 32 | lo 32] (NP = 2)
+template <int NP>
+__device__ __forceinline__ int chunk_of(int p, int d) {
+  return (d >> 5) * 4 * NP + 4 * p + ((d & 31) >> 3);
+}
+template <int NP>
+__device__ __forceinline__ int kpos(int r, int x) {
+  return x ^ (r & (PPL<NP>::CR - 1));
+}
+template <int NP>
+__device__ __forceinline__ int vpos(int r, int x) {
+  return NP == 2 ? x ^ ((r & 3) << 2) : x ^ (((r >> 1) & 1) << 2);
+}
+}  // namespace
+
+template <int NP, bool HAS_MASK, bool PLANES>
+__global__ __launch_bounds__(256, 2) void attn_pp_kernel(const unsigned short* __restrict__ qkvp,
+                                                         float* __restrict__ out,
+                                                         unsigned short* __restrict__ op,
+                                                         const int* __restrict__ cu,
+                                                         const int* __restrict__ q_rows,
+                                                         const uint32_t* __restrict__ mask,
+                                                         int mask_L) {
+  using P = PPL<NP>;
+  constexpr int TERMS = NP == 2 ? 3 : 1;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[P::LDS];
+  const int seq = blockIdx.z, head = blockIdx.y, qb = blockIdx.x;
+  const int start = cu[seq];
+  const int len = cu[seq + 1] - start;
+  const int nq = q_rows ? min(len, q_rows[0]) : len;
+  if (qb * QPB >= nq) return;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 31, lh = lane >> 5;
+  constexpr size_t LDR = (size_t)NP * QKV_COLS;  // elements of one packed token row
+
+  // Q fragments (pre-scaled): step s covers d = 16s + 8 lh .. +8 (B operand: B[k=d][j=q])
+  const int q = qb * QPB + wave * 32 + li;
+  const int qr = q < nq ? q : nq - 1;
+  bf16x8 qh[4], ql[4];
+  {
+    const unsigned short* qp = qkvp + (size_t)(start + qr) * LDR + (size_t)head * 64 * NP;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int d = 16 * s + 8 * lh;
+      const int off = (d >> 5) * 32 * NP + (d & 31);
+      qh[s] = *reinterpret_cast<const bf16x8*>(qp + off);
+      if (TERMS == 3) ql[s] = *reinterpret_cast<const bf16x8*>(qp + off + 32);
+    }
+  }
+
+  // K and V of key tile kt into stage buf: wave instruction i moves key rows
+  // i·ROWS_PER_DMA .. +ROWS_PER_DMA (lane -> row lane / CR, LDS position lane % CR)
+  const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
+  const int dr = lane / P::CR, dc = lane % P::CR;
+  auto issue = [&](int kt, int buf) {
+#pragma unroll
+    for (int j = 0; j < P::DMA_PER_WAVE; ++j) {
+      const int i = wave * P::DMA_PER_WAVE + j;
+      const int r = i * P::ROWS_PER_DMA + dr;
+      int key = kt * KT + r;
+      key = key < len ? key : len - 1;
+      const unsigned short* row = qkvp + (size_t)(start + key) * LDR;
+      dma16(row + (size_t)(AE_HIDDEN + head * 64) * NP + kpos<NP>(r, dc) * 8,
+            lds0 + buf * P::STAGE + i * 1024);
+      dma16(row + (size_t)(2 * AE_HIDDEN + head * 64) * NP + vpos<NP>(r, dc) * 8,
+            lds0 + buf * P::STAGE + P::TILE + i * 1024);
+    }
+  };
+
+  floatx16 o0, o1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; }
+  float m_run = -INFINITY, l_run = 0.f;
+  const uint32_t* mrow = nullptr;
+  if (HAS_MASK) mrow = mask + ((size_t)seq * mask_L + qr) * (mask_L / 32);
+
+  const int nkt = (len + KT - 1) / KT;
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    // the other stage was last read in iteration kt - 1, before its closing barrier
+    if (kt + 1 < nkt) issue(kt + 1, cur ^ 1);
+    const unsigned char* stk = lds + cur * P::STAGE;
+    const unsigned char* stv = stk + P::TILE;
+
+    // ---- S^T = K Q^T (4 k-steps of 16 d); lane li reads key row li
+    floatx16 s;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int d0 = 16 * ks + 8 * lh;
+      const unsigned char* kr = stk + li * P::RB;
+      const bf16x8 kh =
+          *reinterpret_cast<const bf16x8*>(kr + kpos<NP>(li, chunk_of<NP>(0, d0)) * 16);
+      if (TERMS == 3) {
+        const bf16x8 kl =
+            *reinterpret_cast<const bf16x8*>(kr + kpos<NP>(li, chunk_of<NP>(1, d0)) * 16);
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl, qh[ks], s, 0, 0, 0);
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, ql[ks], s, 0, 0, 0);
+      }
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, qh[ks], s, 0, 0, 0);
+    }
+
+    // ---- mask + online softmax (lane = query), exp2 domain
+    uint32_t mbits = 0xffffffffu;
+    if (HAS_MASK) mbits = mrow[kt];
+    float mt = -INFINITY;
+    if (!HAS_MASK && (kt + 1) * KT <= len) {  // full tile, no mask: no per-key select
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[r]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kk = mfma32_row(r, lh);
+        // absent keys (beyond the sequence) are -inf; keys the mask excludes score the most
+        // negative finite float, as HF's additive finfo(f32).min mask does: a query row that
+        // excludes every key then attends all of them uniformly (GraphCodeBERT truncated nodes)
+        const bool in = kt * KT + kk < len;
+        s[r] = !in ? -INFINITY : (((mbits >> kk) & 1u) ? s[r] : -FLT_MAX);
+        mt = fmaxf(mt, s[r]);
+      }
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float m_new = fmaxf(m_run, mt);  // finite: key kt·KT is present in every tile
+    const float alpha = (m_run == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m_run - m_new);
+    float psum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = __builtin_amdgcn_exp2f(s[r] - m_new);  // exp2(-inf) = 0
+      s[r] = p;
+      psum += p;
+    }
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+    if (__any(alpha != 1.f)) {  // alpha == 1 exactly when no row max moved: skipping is exact
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+    }
+
+    // ---- O^T += V^T P^T (2 k-steps of 16 keys, 2 d-tiles).  P^T straight from the S
+    // accumulator: registers 8t..8t+7 of lane half h hold keys 16t + 4h + {0..3} and
+    // 16t + 8 + 4h + {0..3}; the V^T operand takes the same keys through the transposed read
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      bf16x8 ph, pl;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float p = s[8 * t + j];
+        const __bf16 h = (__bf16)p;
+        ph[j] = h;
+        pl[j] = (__bf16)(p - (float)h);
+      }
+      const int k0 = 16 * t + 4 * lh;
+      // lane 16g + 4q + p addresses key row k0 + q (and k0 + 8 + q), d columns
+      // 32 dt + 16 (g & 1) + 4p; it receives d = 32 dt + (lane & 31) of those 4 keys
+      const int kq = k0 + ((lane >> 2) & 3);
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int col = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+        const int cb = (col & 7) * 2;
+        const unsigned char* va = stv + kq * P::RB + cb;
+        const unsigned char* vb = stv + (kq + 8) * P::RB + cb;
+        bf16x8 vh, vl;
+        {
+          const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)(va + vpos<NP>(kq, chunk_of<NP>(0, col)) * 16));
+          const bf16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)(vb + vpos<NP>(kq + 8, chunk_of<NP>(0, col)) * 16));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { vh[e] = a[e]; vh[4 + e] = b[e]; }
+        }
+        if (TERMS == 3) {
+          const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)(va + vpos<NP>(kq, chunk_of<NP>(1, col)) * 16));
+          const bf16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)(vb + vpos<NP>(kq + 8, chunk_of<NP>(1, col)) * 16));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { vl[e] = a[e]; vl[4 + e] = b[e]; }
+        }
+        floatx16& o = dt == 0 ? o0 : o1;
+        if (TERMS == 3) {
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl, ph, o, 0, 0, 0);
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, pl, o, 0, 0, 0);
+        }
+        o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, ph, o, 0, 0, 0);
+      }
+    }
+
+    // tile kt + 1 landed (this wave's DMA), and every wave is done reading stage cur
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  float* os = reinterpret_cast<float*>(lds) + wave * 32 * OSTRIDE;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int d = mfma32_row(r, lh);
+    os[li * OSTRIDE + d] = o0[r] * inv;
+    os[li * OSTRIDE + 32 + d] = o1[r] * inv;
+  }
+  __syncthreads();
+  for (int rr = 0; rr < 32; ++rr) {
+    const int qq = qb * QPB + wave * 32 + rr;
+    if (qq < nq) {
+      const float v = os[rr * OSTRIDE + lane];
+      if (PLANES) {  // packed planes of the O-projection operand (gemm_planes.hip layout)
+        const int c = head * AE_HEAD_DIM + lane;
+        unsigned short* dst = op + (size_t)(start + qq) * NP * AE_HIDDEN + (c >> 5) * 32 * NP + (c & 31);
+        const unsigned short h = f2bf(v);
+        dst[0] = h;
+        if (NP == 2) dst[32] = f2bf(v - __builtin_bit_cast(float, (uint32_t)h << 16));
+      } else {
+        out[(size_t)(start + qq) * AE_HIDDEN + head * AE_HEAD_DIM + lane] = v;
+      }
+    }
+  }
+}
+
+// qkvp: packed planes [T][np·2304] with Q pre-scaled by log2(e)/8; context to op (packed planes)
+// or out (f32 [T, 768]).  q_rows / max_q: the CLS-only launch of the last layer.
+extern "C" hipError_t ae_launch_attention_pp(const unsigned short* qkvp, float* out,
+                                             unsigned short* op, const int* cu, const int* q_rows,
+                                             int max_q, int n, int heads, const uint32_t* mask,
+                                             int mask_L, int np, hipStream_t stream) {
+  if (n <= 0 || max_q <= 0) return hipSuccess;
+  if (np != 1 && np != 2) return hipErrorInvalidValue;
+  dim3 grid((max_q + QPB - 1) / QPB, heads, n), block(256);
+#define APP_LAUNCH(N, M, PL)                                                                 \
+  hipLaunchKernelGGL((attn_pp_kernel<N, M, PL>), grid, block, 0, stream, qkvp, out, op, cu, \
+                     q_rows, mask, mask_L)
+#define APP_MP(N)                                                      \
+  if (op) {                                                            \
+    if (mask) APP_LAUNCH(N, true, true); else APP_LAUNCH(N, false, true);   \
+  } else {                                                             \
+    if (mask) APP_LAUNCH(N, true, false); else APP_LAUNCH(N, false, false); \
+  }
+  if (np == 2) {
+    APP_MP(2)
+  } else {
+    APP_MP(1)
+  }
+#undef APP_MP
+#undef APP_LAUNCH
+  return hipGetLastError();
+}

@@ -27,6 +27,8 @@ hipError_t ae_launch_gemm_x3(const float*, const unsigned short*, const unsigned
                              int, int, hipStream_t);
 hipError_t ae_launch_attention_f32(const float*, float*, const int*, const int*, int, int, int,
                                    const uint32_t*, int, hipStream_t);
+hipError_t ae_launch_attention_pp(const unsigned short*, float*, unsigned short*, const int*,
+                                  const int*, int, int, int, const uint32_t*, int, int, hipStream_t);
 hipError_t ae_launch_attention_x3(const float*, float*, unsigned short*, const int*, const int*,
                                   int, int, int, const uint32_t*, int, int, hipStream_t);
 hipError_t ae_launch_gemm_packed(const unsigned short*, const unsigned short*, const float*,
@@ -69,7 +71,7 @@ int fail(int code, const std::string& msg) {
       return fail(AE_EDEVICE, std::string(#x) + ": " + hipGetErrorString(_e));          \
   } while (0)
 
-enum { EPI_BIAS = 0, EPI_BIAS_GELU = 1, EPI_BIAS_RESIDUAL = 2, EPI_BIAS_TANH = 3 };
+enum { EPI_BIAS = 0, EPI_BIAS_GELU = 1, EPI_BIAS_RESIDUAL = 2, EPI_BIAS_TANH = 3, EPI_BIAS_PACKED = 4 };
 
 struct LayerW {
   float *wqkv, *bqkv, *wo, *bo, *ln1g, *ln1b, *w1, *b1, *w2, *b2, *ln2g, *ln2b;
@@ -334,13 +336,15 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
   HIPC(ae_launch_embed_ln(e->tok_ids, e->tok_pos, e->wemb, e->pemb, e->temb, e->eg, e->eb, eps,
                           (int)T, e->cfg.max_pos, e->x, pl ? e->xp : nullptr, e->np,
                           node_avg ? mask_bits : nullptr, L, e->cu, n, st));
+  unsigned short* qkvp = reinterpret_cast<unsigned short*>(e->qkv);  // planes mode: [T][np·3H]
   for (int li = 0; li < NL; ++li) {
     const LayerW& w = e->layers[li];
     const bool last_cls = cls_only && li == NL - 1;
     int rc;
     if (pl) {
-      if ((rc = gemm_pk(e, e->xp, w.wqkv_p, w.bqkv, nullptr, e->qkv, nullptr, (int)T, 3 * H, H,
-                        EPI_BIAS, st, false)))
+      // Q | K | V as packed planes (Q pre-scaled) straight into the attention's LDS-DMA
+      if ((rc = gemm_pk(e, e->xp, w.wqkv_p, w.bqkv, nullptr, nullptr, qkvp, (int)T, 3 * H, H,
+                        EPI_BIAS_PACKED, st, false)))
         return rc;
     } else if ((rc = gemm(e, e->x, w.wqkv, w.wqkv_h, w.wqkv_l, w.bqkv, nullptr, e->qkv, (int)T,
                           3 * H, H, EPI_BIAS, st, false))) {
@@ -353,10 +357,9 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
         HIPC(ae_launch_attention_f32(e->qkv, e->ctx, e->cu, last_cls ? e->one : nullptr,
                                      last_cls ? 1 : max_len, n, heads, mask_bits, L, st));
       else
-        HIPC(ae_launch_attention_x3(e->qkv, e->ctx, (pl && !last_cls) ? e->cp : nullptr, e->cu,
-                                    last_cls ? e->one : nullptr,
-                                    last_cls ? 1 : max_len, n, heads, mask_bits, L,
-                                    e->cfg.precision == AE_PREC_F32X3 ? 3 : 1, st));
+        HIPC(ae_launch_attention_pp(qkvp, e->ctx, last_cls ? nullptr : e->cp, e->cu,
+                                    last_cls ? e->one : nullptr, last_cls ? 1 : max_len, n, heads,
+                                    mask_bits, L, e->np, st));
     }
     if (!last_cls && pl) {
       if ((rc = gemm_pk(e, e->cp, w.wo_p, w.bo, e->x, e->tmp, nullptr, (int)T, H, H,
@@ -476,6 +479,14 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
     std::memcpy(hb.data(), qb->data, H * 4);
     std::memcpy(hb.data() + H, kb->data, H * 4);
     std::memcpy(hb.data() + 2 * H, vb->data, H * 4);
+    if (cfg->precision != AE_PREC_FP32) {
+      // split-precision modes: the packed QKV output feeds attention_pp.hip, which runs its
+      // softmax in the exp2 domain over Q·K^T·log2(e)/8 — fold that scale into Wq and bq (these
+      // copies serve only the split path; the fp32 mode keeps the HF weights unchanged)
+      constexpr float kQScale = 0.18033688011112042f;  // log2(e) / sqrt(64)
+      for (int64_t i = 0; i < (int64_t)H * H; ++i) hw[i] *= kQScale;
+      for (int i = 0; i < H; ++i) hb[i] *= kQScale;
+    }
     if ((rc = dev_alloc(e, (void**)&w.wqkv, hw.size() * 4)) ||
         (rc = dev_alloc(e, (void**)&w.bqkv, hb.size() * 4))) {
       std::string m = g_err;

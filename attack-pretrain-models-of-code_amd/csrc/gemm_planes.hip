@@ -40,7 +40,9 @@
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-enum { PK_EPI_BIAS = 0, PK_EPI_GELU_PACKED = 1, PK_EPI_RES = 2, PK_EPI_TANH = 3 };
+// PK_EPI_BIAS_PACKED: +bias -> packed planes (the QKV output feeding attention_pp.hip); only the
+// ping-pong 256 x 256 kernel has it
+enum { PK_EPI_BIAS = 0, PK_EPI_GELU_PACKED = 1, PK_EPI_RES = 2, PK_EPI_TANH = 3, PK_EPI_BIAS_PACKED = 4 };
 
 namespace {
 constexpr int PK_BM = 256, PK_ROWB = 128;
@@ -636,7 +638,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
   // or packed rows (NP 2: two 128-B [hi 32 | lo 32] blocks; NP 1: 128 B of hi) — with the 16-B
   // chunk index XOR-ed by (row & 15) (conflict-free 16-row groups), then stores it with 16-B
   // lanes, whole row segments per instruction.
-  constexpr int RB = EPI == PK_EPI_GELU_PACKED ? 64 * 2 * NP : 256;  // bytes of a row segment
+  constexpr bool PACKED = EPI == PK_EPI_GELU_PACKED || EPI == PK_EPI_BIAS_PACKED;
+  constexpr int RB = PACKED ? 64 * 2 * NP : 256;  // bytes of a row segment
   constexpr int CPR = RB / 16;                                       // 16-B chunks per row
   unsigned char* reg = pk_smem + wave * 16384;
   const int cb0 = n0 + wn * 64;
@@ -651,13 +654,14 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
         for (int j = 0; j < 4; ++j) {
           const floatx16& c = acc[2 * half + tt][tn];
           const int cc = tn * 32 + 8 * j + 4 * lh;  // column within the wave's 64
-          if (EPI == PK_EPI_GELU_PACKED) {
+          if (PACKED) {
             const int col = cb0 + cc < N ? cb0 + cc : N - 4;
             const floatx4 bv = *reinterpret_cast<const floatx4*>(bias + col);
             ushortx4 h, l;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              const float y = gelu_erfc_fast(c[4 * j + i] + bv[i]);
+              const float y = EPI == PK_EPI_GELU_PACKED ? gelu_erfc_fast(c[4 * j + i] + bv[i])
+                                                        : c[4 * j + i] + bv[i];
               const __bf16 hv = (__bf16)y;
               h[i] = __builtin_bit_cast(unsigned short, hv);
               l[i] = f2bf(y - (float)hv);
@@ -689,7 +693,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
       const int row = m0 + wm * 128 + half * 64 + lr;
       const bool ok = row < M;
       const uint4 v = *reinterpret_cast<const uint4*>(reg + lr * RB + ((c ^ (lr & 15)) & (CPR - 1)) * 16);
-      if (EPI == PK_EPI_GELU_PACKED) {
+      if (PACKED) {
         // 16 B of the packed row: column block (c*16 / (64 NP)), all within the wave's 64 columns
         const int col = cb0 + (c * 16) / (2 * NP);  // first column this chunk belongs to (>= block start)
         if (ok && col < N) {
@@ -955,6 +959,8 @@ hipError_t pp_epi(int epi, const __bf16* A, const __bf16* W, const float* bias, 
       return pp_launch<NP, PK_EPI_BIAS, 0>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
     case PK_EPI_GELU_PACKED:
       return pp_launch<NP, PK_EPI_GELU_PACKED, 0>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
+    case PK_EPI_BIAS_PACKED:
+      return pp_launch<NP, PK_EPI_BIAS_PACKED, 0>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
     case PK_EPI_RES:
       return pp_launch<NP, PK_EPI_RES, 0>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
     default: return pp_launch<NP, PK_EPI_TANH, 0>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
@@ -984,7 +990,7 @@ hipError_t pp192_dispatch(const unsigned short* A, const unsigned short* W, cons
                           int group_m, hipStream_t st) {
   auto a = reinterpret_cast<const __bf16*>(A);
   auto w = reinterpret_cast<const __bf16*>(W);
-  if (epi == PK_EPI_GELU_PACKED) return hipErrorInvalidValue;
+  if (epi == PK_EPI_GELU_PACKED || epi == PK_EPI_BIAS_PACKED) return hipErrorInvalidValue;
   if (np == 2) {
     if (epi == PK_EPI_BIAS) return pp192_launch<2, PK_EPI_BIAS>(a, w, bias, R, C, M, N, K, group_m, st);
     if (epi == PK_EPI_RES) return pp192_launch<2, PK_EPI_RES>(a, w, bias, R, C, M, N, K, group_m, st);
@@ -1035,6 +1041,7 @@ hipError_t pk_epi(int epi, const __bf16* A, const __bf16* W, const float* bias, 
       return pk_launch<BN, 2, PK_EPI_BIAS, DIAG>(A, W, bias, R, C, Cp, M, N, K, st);
     return pk_launch<BN, 2, PK_EPI_GELU_PACKED, DIAG>(A, W, bias, R, C, Cp, M, N, K, st);
   }
+  if (epi == PK_EPI_BIAS_PACKED) return hipErrorInvalidValue;  // ping-pong kernel only
   switch (epi) {
     case PK_EPI_BIAS: return pk_launch<BN, NP, PK_EPI_BIAS, DIAG>(A, W, bias, R, C, Cp, M, N, K, st);
     case PK_EPI_GELU_PACKED:
@@ -1087,7 +1094,7 @@ int cu_count() {
 
 // tile width of the ping-pong GEMM for an M x N output (see ae_launch_gemm_packed)
 int pp_choose(int M, int N, int epi) {
-  if (epi == PK_EPI_GELU_PACKED) return 256;
+  if (epi == PK_EPI_GELU_PACKED || epi == PK_EPI_BIAS_PACKED) return 256;
   const long tm = (M + 255) / 256, cus = cu_count();
   const long r256 = (tm * ((N + 255) / 256) + cus - 1) / cus;
   const long r192 = (tm * ((N + 191) / 192) + cus - 1) / cus;

@@ -39,6 +39,7 @@ BF16_MFMA_PEAK_TFLOPS = 2516.6  # dense bf16 (spec, no sparsity)
 METRIC = "victim queries/sec + attacked examples/min (node), CodeBERT Devign GA attack"
 FIXTURE = ROOT / "data" / "devign" / "test_subs_0_400.jsonl"
 AA_FIXTURE = ROOT / "data" / "authorship" / "valid_subs.jsonl"
+CLONE_FIXTURE = ROOT / "data" / "clone" / "test_subs_0_500.jsonl"
 # attack-sensitive synthetic victim (the attack parity tests' weights): a larger classifier
 # out_proj spreads probabilities so that substitutions can flip predictions
 VICTIM_SEED, VICTIM_OUT_STD = 5, 8.0
@@ -73,6 +74,8 @@ def parse_args():
                     help="authorship programs of the config-5 leg (GA vs MHM-NS; 0 disables)")
     ap.add_argument("--aa-gcb-examples", type=int, default=32,
                     help="of them, attacked by GA on the GraphCodeBERT victim too (0 disables)")
+    ap.add_argument("--clone-examples", type=int, default=48,
+                    help="config-4 leg: GraphCodeBERT BigCloneBench pairs attacked (0 = skip)")
     ap.add_argument("--no-fp32-mode", action="store_true")
     return ap.parse_args()
 
@@ -482,6 +485,46 @@ def aa_leg(dev, n_examples, n_gcb, rank, world, precision):
     return res
 
 
+def clone_leg(dev, n_examples, rank, world, precision):
+    """Config 4: the GraphCodeBERT BigCloneBench pair attack (GraphCodeBERT/clonedetection/code/
+    attack.py with README's --code_length 512 --data_flow_length 128 --eval_batch_size 32):
+    greedy -> GA on code1 of each pair, both codes through the graph forward at L = 640 with the
+    data-flow mask, the pair head over [code1 | code2] CLS rows.  Synthetic victim (seed 5,
+    out_proj std 8); labels are its own predictions, so every pair is attacked."""
+    from apmc_amd.dist import DynamicQueue, call_key
+    from apmc_amd.drivers import AttackArgs, _example, load_fixture, run_gi_attack_batched
+    from apmc_amd.graph import GraphModel
+    from apmc_amd.host import Tokenizer
+    from apmc_amd.weights import synthetic_state_dict
+
+    codes, subs, _ = load_fixture(CLONE_FIXTURE, 0, n_examples)
+    tok = Tokenizer()
+    sd = synthetic_state_dict(seed=VICTIM_SEED, head="pair2", num_labels=2, out_std=VICTIM_OUT_STD)
+    gargs = AttackArgs(block_size=512, eval_batch_size=32, seed=123456, rng="per_example",
+                       task="gcb_clone", code_length=512, data_flow_length=128)
+    gmodel = GraphModel(sd, task="clone", args=gargs, precision=precision, device=dev.index)
+    labels = [int(gmodel.get_results([_example(tok, c, 0, 512, "gcb_clone", gargs)])[1][0])
+              for c in codes]
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    queue = DynamicQueue(len(codes), key=call_key("bench_clone_gcb_queue"))
+    out = run_gi_attack_batched(gmodel, codes, subs, labels, gargs, queue=queue, max_inflight=64)
+    ex, cnt, suc, q, wall = _gather_sum_max([out["examples"], out["total_cnt"], out["success"],
+                                             out["queries"], out["wall_s"]], dev, world, 4)
+    gmodel.engine.close()
+    return {"workload": f"GraphCodeBERT BigCloneBench pairs test_subs_0_500.jsonl [0, {len(codes)}),"
+                        " greedy -> GA on code1, code_length 512 + data_flow_length 128 per code, "
+                        "pair head (synthetic victim, labels = its own predictions)",
+            "precision": precision, "examples": int(ex), "attacked": int(cnt),
+            "successes": int(suc), "success_rate": round(suc / cnt, 4) if cnt else None,
+            "victim_queries": int(q), "wall_s": round(wall, 2),
+            "victim_queries_per_s": round(q / wall, 1) if wall else None,
+            "sequences_per_s": round(2 * q / wall, 1) if wall else None,
+            "attacked_examples_per_min": round(60 * ex / wall, 2) if wall else None,
+            "batching": "cross-example: up to 64 pairs' requests per device batch"}
+
+
 def subs_leg(dev, seconds, rank, world, precision):
     """Config-3 workload: masked-LM substitute generation (get_substitutes.py) over the Devign
     fixture functions in order (12-layer codebert-shaped MLM, synthetic weights), items pulled
@@ -678,6 +721,9 @@ def main():
         log("authorship leg")
         res["authorship"] = aa_leg(dev, args.aa_examples, args.aa_gcb_examples, rank, world,
                                    args.precision)
+    if args.clone_examples > 0:
+        log("config-4 leg (GraphCodeBERT clone)")
+        res["clone_gcb"] = clone_leg(dev, args.clone_examples, rank, world, args.precision)
     if args.mhm_examples > 0:
         log("MHM-NS leg")
         res["mhm"] = mhm_leg(dev, args.mhm_examples, args.mhm_seq_examples, rank, world,

@@ -194,3 +194,61 @@ def test_attention_x3_variants_match_f64(gpu, variant, case):
     assert torch.isfinite(got).all()
     err = (got - ref).abs()
     assert (err <= tol).all(), float(err.max())
+
+
+def _qkv_planes(qkv, np_):
+    """f32 qkv [T, 2304] -> the QKV GEMM's packed-plane output with Q pre-scaled by log2(e)/8
+    (what the engine feeds attention_pp: gemm_planes PK_EPI_BIAS_PACKED over scaled Wq, bq)."""
+    x = qkv.clone()
+    x[:, :768] *= 0.18033688011112042
+    hi, lo = _split(x)
+    return _pack(hi, lo, np_)
+
+
+@pytest.mark.parametrize("np_", [2, 1])
+@pytest.mark.parametrize("case", ["ragged", "mask", "cls", "planes"])
+def test_attention_pp_matches_f64(gpu, np_, case):
+    """attn_pp_kernel (packed-plane Q/K/V moved by LDS-DMA, swizzled K/V images, transposed V
+    reads) against the float64 reference, for both plane counts (np 1 = bf16 mode: stated
+    tolerance 2e-2) and the ragged / mask / CLS-only / packed-output launches."""
+    lib = _lib()
+    vp, i32 = ctypes.c_void_p, ctypes.c_int32
+    lib.ae_launch_attention_pp.argtypes = [vp] * 5 + [i32] * 3 + [vp, i32, i32, vp]
+    lib.ae_launch_attention_pp.restype = ctypes.c_int
+    g = torch.Generator().manual_seed(11 + np_)
+    lens = [1, 31, 32, 33, 129, 300, 64] if case != "mask" else [40, 97, 128]
+    n = len(lens)
+    cu = torch.zeros(n + 1, dtype=torch.int32)
+    cu[1:] = torch.cumsum(torch.tensor(lens), 0)
+    T = int(cu[-1])
+    qkv = torch.randn(T, 3 * 768, generator=g)
+    L, mask, dmask = 0, None, None
+    if case == "mask":
+        L = 128
+        dense = (torch.rand(n, L, L, generator=g) < 0.6)
+        dense[:, :, 0] = True
+        dense[1, 5, :] = False  # a query row that excludes every key
+        words = (dense.view(n, L, L // 32, 32).long() << torch.arange(32)).sum(-1)
+        mask = words
+        dmask = (words - (words >= 2 ** 31).long() * 2 ** 32).to(torch.int32).cuda()
+    ref = _attn_ref(qkv, cu, n, mask, L)
+    dq, dcu = _qkv_planes(qkv, np_).cuda(), cu.cuda()
+    out = torch.full((T, 768), float("nan"), device="cuda")
+    op = torch.zeros((T, np_ * 768), dtype=torch.bfloat16, device="cuda") if case == "planes" else None
+    one = torch.ones(1, dtype=torch.int32, device="cuda") if case == "cls" else None
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    rc = lib.ae_launch_attention_pp(_p(dq), _p(out), _p(op), _p(dcu), _p(one),
+                                    1 if case == "cls" else max(lens), n, 12, _p(dmask), L, np_, st)
+    assert rc == 0
+    torch.cuda.synchronize()
+    if case == "planes":
+        got = _unpack(op.cpu(), np_, 768)
+    else:
+        got = out.double().cpu()
+    tol = (2e-4 + 2e-5 * ref.abs()) if np_ == 2 else (2e-2 + 2e-2 * ref.abs())
+    if case == "cls":
+        rows = cu[:-1].long()
+        got, ref = got[rows], ref[rows]
+    assert torch.isfinite(got).all()
+    err = (got - ref).abs()
+    assert (err <= tol).all(), float(err.max())

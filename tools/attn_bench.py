@@ -56,6 +56,9 @@ def main():
     fn = lib.ae_bench_attention_x3
     fn.argtypes = [vp] * 5 + [i32] * 3 + [vp, i32, i32, i32, vp]
     fn.restype = ctypes.c_int
+    fpp = lib.ae_launch_attention_pp  # variant "pp": packed-plane input (Q pre-scaled), LDS-DMA
+    fpp.argtypes = [vp] * 5 + [i32] * 3 + [vp, i32, i32, vp]
+    fpp.restype = ctypes.c_int
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream(dev)
     sp = ctypes.c_void_p(st.cuda_stream)
@@ -77,12 +80,24 @@ def main():
     def p(t):
         return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(None)
 
+    np_ = 2 if args.terms == 3 else 1
+    x = qkv.clone()
+    x[:, :H] *= 0.18033688011112042
+    hi = x.to(torch.bfloat16)
+    lo = (x - hi.float()).to(torch.bfloat16)
+    planes = hi if np_ == 1 else torch.stack(
+        [hi.view(T, -1, 32), lo.view(T, -1, 32)], 2).reshape(T, 2 * 3 * H).contiguous()
     cases = []
     for v in args.variants.split(","):
-        var = int(v)
+        var = v if v == "pp" else int(v)
         out = torch.zeros((T, H), device=dev)
-        call = (lambda out=out, var=var: fn(p(qkv), p(out), p(None), p(cu_d), p(None), int(lens.max()),
-                                            n, HEADS, p(None), 0, args.terms, var, sp))
+        if var == "pp":
+            call = (lambda out=out: fpp(p(planes), p(out), p(None), p(cu_d), p(None),
+                                        int(lens.max()), n, HEADS, p(None), 0, np_, sp))
+        else:
+            call = (lambda out=out, var=var: fn(p(qkv), p(out), p(None), p(cu_d), p(None),
+                                                int(lens.max()), n, HEADS, p(None), 0, args.terms,
+                                                var, sp))
         rc = call()
         torch.cuda.synchronize()
         if rc != 0:
