@@ -245,10 +245,10 @@ def test_attention_pp_matches_f64(gpu, np_, case):
         got = _unpack(op.cpu(), np_, 768)
     else:
         got = out.double().cpu()
-    tol = (2e-4 + 2e-5 * ref.abs()) if np_ == 2 else (2e-2 + 2e-2 * ref.abs())
     if case == "cls":
         rows = cu[:-1].long()
         got, ref = got[rows], ref[rows]
+    tol = (2e-4 + 2e-5 * ref.abs()) if np_ == 2 else (2e-2 + 2e-2 * ref.abs())
     assert torch.isfinite(got).all()
     err = (got - ref).abs()
     assert (err <= tol).all(), float(err.max())
