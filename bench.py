@@ -74,7 +74,7 @@ def parse_args():
                     help="authorship programs of the config-5 leg (GA vs MHM-NS; 0 disables)")
     ap.add_argument("--aa-gcb-examples", type=int, default=32,
                     help="of them, attacked by GA on the GraphCodeBERT victim too (0 disables)")
-    ap.add_argument("--clone-examples", type=int, default=48,
+    ap.add_argument("--clone-examples", type=int, default=32,
                     help="config-4 leg: GraphCodeBERT BigCloneBench pairs attacked (0 = skip)")
     ap.add_argument("--no-fp32-mode", action="store_true")
     return ap.parse_args()
