@@ -70,7 +70,10 @@ __device__ __forceinline__ int vpos(int r, int x) {
 }
 }  // namespace
 
-template <int NP, bool HAS_MASK, bool PLANES>
+// PIPE: software-pipelined loop — the S MFMAs of key tile kt + 1 issue in the same scheduling
+// region as the exp / P-split VALU of tile kt (independent streams the SIMD co-issues), K and V in
+// separate 2-slot rings (K two tiles ahead, V one).
+template <int NP, bool HAS_MASK, bool PLANES, bool PIPE>
 __global__ __launch_bounds__(256, 2) void attn_pp_kernel(const unsigned short* __restrict__ qkvp,
                                                          float* __restrict__ out,
                                                          unsigned short* __restrict__ op,
@@ -107,11 +110,10 @@ __global__ __launch_bounds__(256, 2) void attn_pp_kernel(const unsigned short* _
     }
   }
 
-  // K and V of key tile kt into stage buf: wave instruction i moves key rows
-  // i·ROWS_PER_DMA .. +ROWS_PER_DMA (lane -> row lane / CR, LDS position lane % CR)
   const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
   const int dr = lane / P::CR, dc = lane % P::CR;
-  auto issue = [&](int kt, int buf) {
+  // DMA of one matrix (K: moff 0 into slot kslot, V: moff 2·AE_HIDDEN) of key tile kt
+  auto issue1 = [&](int kt, int moff, uint32_t dst, bool vimg) {
 #pragma unroll
     for (int j = 0; j < P::DMA_PER_WAVE; ++j) {
       const int i = wave * P::DMA_PER_WAVE + j;
@@ -119,10 +121,8 @@ __global__ __launch_bounds__(256, 2) void attn_pp_kernel(const unsigned short* _
       int key = kt * KT + r;
       key = key < len ? key : len - 1;
       const unsigned short* row = qkvp + (size_t)(start + key) * LDR;
-      dma16(row + (size_t)(AE_HIDDEN + head * 64) * NP + kpos<NP>(r, dc) * 8,
-            lds0 + buf * P::STAGE + i * 1024);
-      dma16(row + (size_t)(2 * AE_HIDDEN + head * 64) * NP + vpos<NP>(r, dc) * 8,
-            lds0 + buf * P::STAGE + P::TILE + i * 1024);
+      dma16(row + (size_t)(moff + head * 64) * NP + (vimg ? vpos<NP>(r, dc) : kpos<NP>(r, dc)) * 8,
+            dst + i * 1024);
     }
   };
 
@@ -133,20 +133,8 @@ __global__ __launch_bounds__(256, 2) void attn_pp_kernel(const unsigned short* _
   const uint32_t* mrow = nullptr;
   if (HAS_MASK) mrow = mask + ((size_t)seq * mask_L + qr) * (mask_L / 32);
 
-  const int nkt = (len + KT - 1) / KT;
-  issue(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int cur = kt & 1;
-    // the other stage was last read in iteration kt - 1, before its closing barrier
-    if (kt + 1 < nkt) issue(kt + 1, cur ^ 1);
-    const unsigned char* stk = lds + cur * P::STAGE;
-    const unsigned char* stv = stk + P::TILE;
-
-    // ---- S^T = K Q^T (4 k-steps of 16 d); lane li reads key row li
-    floatx16 s;
+  // S^T = K Q^T over a K image (4 k-steps of 16 d); lane li reads key row li
+  auto s_mfma = [&](const unsigned char* stk, floatx16& s) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) s[r] = 0.f;
 #pragma unroll
@@ -163,8 +151,9 @@ __global__ __launch_bounds__(256, 2) void attn_pp_kernel(const unsigned short* _
       }
       s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, qh[ks], s, 0, 0, 0);
     }
-
-    // ---- mask + online softmax (lane = query), exp2 domain
+  };
+  // mask + running max of tile kt (lane = query); returns the new max
+  auto tile_max = [&](int kt, floatx16& s) {
     uint32_t mbits = 0xffffffffu;
     if (HAS_MASK) mbits = mrow[kt];
     float mt = -INFINITY;
@@ -184,35 +173,27 @@ __global__ __launch_bounds__(256, 2) void attn_pp_kernel(const unsigned short* _
       }
     }
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    const float m_new = fmaxf(m_run, mt);  // finite: key kt·KT is present in every tile
-    const float alpha = (m_run == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m_run - m_new);
+    return fmaxf(m_run, mt);  // finite: key kt·KT is present in every tile
+  };
+  // P = exp2(S - m) (in place), its row sum, and the bf16 hi / lo split of P^T for the PV MFMAs
+  auto exp_split = [&](floatx16& s, float m_new, bf16x8 (&ph)[2], bf16x8 (&pl)[2]) {
     float psum = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float p = __builtin_amdgcn_exp2f(s[r] - m_new);  // exp2(-inf) = 0
-      s[r] = p;
       psum += p;
+      const __bf16 h = (__bf16)p;
+      ph[r >> 3][r & 7] = h;
+      pl[r >> 3][r & 7] = (__bf16)(p - (float)h);
     }
-    l_run = l_run * alpha + psum;
-    m_run = m_new;
-    if (__any(alpha != 1.f)) {  // alpha == 1 exactly when no row max moved: skipping is exact
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
-    }
-
-    // ---- O^T += V^T P^T (2 k-steps of 16 keys, 2 d-tiles).  P^T straight from the S
-    // accumulator: registers 8t..8t+7 of lane half h hold keys 16t + 4h + {0..3} and
-    // 16t + 8 + 4h + {0..3}; the V^T operand takes the same keys through the transposed read
+    return psum;
+  };
+  // O^T += V^T P^T (2 k-steps of 16 keys, 2 d-tiles).  P^T straight from the S accumulator:
+  // registers 8t..8t+7 of lane half h hold keys 16t + 4h + {0..3} and 16t + 8 + 4h + {0..3};
+  // the V^T operand takes the same keys through the transposed read
+  auto pv_mfma = [&](const unsigned char* stv, const bf16x8 (&ph)[2], const bf16x8 (&pl)[2]) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      bf16x8 ph, pl;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float p = s[8 * t + j];
-        const __bf16 h = (__bf16)p;
-        ph[j] = h;
-        pl[j] = (__bf16)(p - (float)h);
-      }
       const int k0 = 16 * t + 4 * lh;
       // lane 16g + 4q + p addresses key row k0 + q (and k0 + 8 + q), d columns
       // 32 dt + 16 (g & 1) + 4p; it receives d = 32 dt + (lane & 31) of those 4 keys
@@ -242,16 +223,83 @@ __global__ __launch_bounds__(256, 2) void attn_pp_kernel(const unsigned short* _
         }
         floatx16& o = dt == 0 ? o0 : o1;
         if (TERMS == 3) {
-          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl, ph, o, 0, 0, 0);
-          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, pl, o, 0, 0, 0);
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl, ph[t], o, 0, 0, 0);
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, pl[t], o, 0, 0, 0);
         }
-        o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, ph, o, 0, 0, 0);
+        o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, ph[t], o, 0, 0, 0);
       }
     }
+  };
+  auto rescale = [&](float alpha) {
+    if (__any(alpha != 1.f)) {  // alpha == 1 exactly when no row max moved: skipping is exact
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+    }
+  };
 
-    // tile kt + 1 landed (this wave's DMA), and every wave is done reading stage cur
+  const int nkt = (len + KT - 1) / KT;
+  if (!PIPE) {
+    // stage b = [K | V] of one tile, two stages
+    issue1(0, AE_HIDDEN, lds0, false);
+    issue1(0, 2 * AE_HIDDEN, lds0 + P::TILE, true);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int cur = kt & 1;
+      // the other stage was last read in iteration kt - 1, before its closing barrier
+      if (kt + 1 < nkt) {
+        issue1(kt + 1, AE_HIDDEN, lds0 + (cur ^ 1) * P::STAGE, false);
+        issue1(kt + 1, 2 * AE_HIDDEN, lds0 + (cur ^ 1) * P::STAGE + P::TILE, true);
+      }
+      const unsigned char* stk = lds + cur * P::STAGE;
+      floatx16 s;
+      s_mfma(stk, s);
+      const float m_new = tile_max(kt, s);
+      const float alpha = (m_run == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m_run - m_new);
+      bf16x8 ph[2], pl[2];
+      const float psum = exp_split(s, m_new, ph, pl);
+      l_run = l_run * alpha + psum;
+      m_run = m_new;
+      rescale(alpha);
+      pv_mfma(stk + P::TILE, ph, pl);
+      // tile kt + 1 landed (this wave's DMA), and every wave is done reading stage cur
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    // K ring (slots 0, 1) then V ring (slots 2, 3): K_j in slot j & 1, V_j in slot 2 + (j & 1)
+    auto kslot = [&](int j) { return (uint32_t)((j & 1) * P::TILE); };
+    auto vslot = [&](int j) { return (uint32_t)((2 + (j & 1)) * P::TILE); };
+    issue1(0, AE_HIDDEN, lds0 + kslot(0), false);
+    issue1(0, 2 * AE_HIDDEN, lds0 + vslot(0), true);
+    if (nkt > 1) issue1(1, AE_HIDDEN, lds0 + kslot(1), false);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    floatx16 s_cur;
+    s_mfma(lds + kslot(0), s_cur);
+    __syncthreads();  // every wave has read K_0 before K_2 lands in its slot
+    for (int kt = 0; kt < nkt; ++kt) {
+      // V_{kt+1} into V_{kt-1}'s slot and K_{kt+2} into K_kt's slot: both last read in
+      // iteration kt - 1 (or the prologue), before its closing barrier
+      if (kt + 1 < nkt) issue1(kt + 1, 2 * AE_HIDDEN, lds0 + vslot(kt + 1), true);
+      if (kt + 2 < nkt) issue1(kt + 2, AE_HIDDEN, lds0 + kslot(kt + 2), false);
+      const float m_new = tile_max(kt, s_cur);
+      const float alpha = (m_run == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m_run - m_new);
+      bf16x8 ph[2], pl[2];
+      floatx16 s_next;
+      // one scheduling region: tile kt's exp / split on the VALU, tile kt + 1's S on the MFMA
+      // (the last iteration's S of a tile past the end reads a stale slot and is discarded;
+      // unconditional so the region has no branch)
+      const float psum = exp_split(s_cur, m_new, ph, pl);
+      s_mfma(lds + kslot(kt + 1), s_next);
+      l_run = l_run * alpha + psum;
+      m_run = m_new;
+      rescale(alpha);
+      pv_mfma(lds + vslot(kt), ph, pl);
+      s_cur = s_next;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
 
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
@@ -283,15 +331,16 @@ __global__ __launch_bounds__(256, 2) void attn_pp_kernel(const unsigned short* _
 
 // qkvp: packed planes [T][np·2304] with Q pre-scaled by log2(e)/8; context to op (packed planes)
 // or out (f32 [T, 768]).  q_rows / max_q: the CLS-only launch of the last layer.
-extern "C" hipError_t ae_launch_attention_pp(const unsigned short* qkvp, float* out,
-                                             unsigned short* op, const int* cu, const int* q_rows,
-                                             int max_q, int n, int heads, const uint32_t* mask,
-                                             int mask_L, int np, hipStream_t stream) {
+namespace {
+template <bool PIPE>
+hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op, const int* cu,
+                      const int* q_rows, int max_q, int n, int heads, const uint32_t* mask,
+                      int mask_L, int np, hipStream_t stream) {
   if (n <= 0 || max_q <= 0) return hipSuccess;
   if (np != 1 && np != 2) return hipErrorInvalidValue;
   dim3 grid((max_q + QPB - 1) / QPB, heads, n), block(256);
 #define APP_LAUNCH(N, M, PL)                                                                 \
-  hipLaunchKernelGGL((attn_pp_kernel<N, M, PL>), grid, block, 0, stream, qkvp, out, op, cu, \
+  hipLaunchKernelGGL((attn_pp_kernel<N, M, PL, PIPE>), grid, block, 0, stream, qkvp, out, op, cu, \
                      q_rows, mask, mask_L)
 #define APP_MP(N)                                                      \
   if (op) {                                                            \
@@ -307,4 +356,26 @@ extern "C" hipError_t ae_launch_attention_pp(const unsigned short* qkvp, float* 
 #undef APP_MP
 #undef APP_LAUNCH
   return hipGetLastError();
+}
+constexpr bool APP_PIPE = true;  // production loop (tools/attn_bench.py A/B: pp1 190 us vs pp 203 us)
+}  // namespace
+
+extern "C" hipError_t ae_launch_attention_pp(const unsigned short* qkvp, float* out,
+                                             unsigned short* op, const int* cu, const int* q_rows,
+                                             int max_q, int n, int heads, const uint32_t* mask,
+                                             int mask_L, int np, hipStream_t stream) {
+  return app_launch<APP_PIPE>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np,
+                              stream);
+}
+
+// Kernel experiments (tools/attn_bench.py, tests): variant 0 = two-stage loop, 1 = pipelined.
+extern "C" hipError_t ae_bench_attention_pp(const unsigned short* qkvp, float* out,
+                                            unsigned short* op, const int* cu, const int* q_rows,
+                                            int max_q, int n, int heads, const uint32_t* mask,
+                                            int mask_L, int np, int variant, hipStream_t stream) {
+  if (variant == 1)
+    return app_launch<true>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
+  if (variant == 0)
+    return app_launch<false>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
+  return hipErrorInvalidValue;
 }

@@ -76,6 +76,7 @@ def parse_args():
                     help="of them, attacked by GA on the GraphCodeBERT victim too (0 disables)")
     ap.add_argument("--clone-examples", type=int, default=32,
                     help="config-4 leg: GraphCodeBERT BigCloneBench pairs attacked (0 = skip)")
+    ap.add_argument("--no-config1", action="store_true", help="skip the config-1 leg")
     ap.add_argument("--no-fp32-mode", action="store_true")
     return ap.parse_args()
 
@@ -710,7 +711,7 @@ def main():
         log("config-2 attack leg")
         res["attack"] = attack_leg(dev, args.attack_examples, args.attack_deadline,
                                    args.attack_inflight, rank, world, args.precision)
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and not args.no_config1:
         log("config-1 leg")
         res["config1"] = config1_leg(dev, args.precision, threads,
                                      0 if args.no_cpu_baseline else args.cpu_e2e_seconds)

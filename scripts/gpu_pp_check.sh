@@ -7,7 +7,7 @@ mkdir -p gpurun_out/pp
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -q -x --timeout 120 --timeout-method thread > gpurun_out/pp/kernels.log 2>&1
 rc=$?; tail -3 gpurun_out/pp/kernels.log; echo "kernel tests rc=$rc"; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 200 python -u tools/attn_bench.py --variants 3,pp --rounds 7 > gpurun_out/pp/attn_ab.log 2>&1
+timeout -k 10 200 python -u tools/attn_bench.py --variants pp,pp1 --rounds 7 > gpurun_out/pp/attn_ab.log 2>&1
 rc=$?; grep variant gpurun_out/pp/attn_ab.log; echo "attn_bench rc=$rc"; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pp/pytest_gpu.log 2>&1
 rc=$?; tail -3 gpurun_out/pp/pytest_gpu.log; echo "pytest rc=$rc"; [ $rc -ne 0 ] && exit $rc

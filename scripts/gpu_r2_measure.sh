@@ -16,7 +16,7 @@ if [ -z "$SKIP_BENCH" ]; then
   timeout -k 10 900 python -u bench.py ${BENCH_FULL_ARGS:-} > gpurun_out/$TAG/bench.log 2>&1
   rc=$?; tail -c 3000 gpurun_out/$TAG/bench.log; echo "bench rc=$rc"; [ $rc -ne 0 ] && exit $rc
 fi
-SHORT="$GRAFT_REPO_ROOT/bench.py --steps ${STEPS:-5} --warmup 2 --no-cpu-baseline --no-fp32-mode --attack-examples 0 --subs-seconds 0 --mhm-examples 0 ${BENCH_ARGS:-}"
+SHORT="$GRAFT_REPO_ROOT/bench.py --steps ${STEPS:-5} --warmup 2 --no-cpu-baseline --no-fp32-mode --attack-examples 0 --subs-seconds 0 --mhm-examples 0 --aa-examples 0 --clone-examples 0 --no-config1 ${BENCH_ARGS:-}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/$TAG/trace" -o run -- python3 $SHORT > gpurun_out/$TAG/trace.log 2>&1
 rc=$?; tail -2 gpurun_out/$TAG/trace.log; echo "trace rc=$rc"; [ $rc -ne 0 ] && exit $rc
 for C in FETCH_SIZE WRITE_SIZE; do

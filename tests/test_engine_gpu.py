@@ -101,7 +101,18 @@ def test_mlm_topk_matches_golden(gpu):
     sc, ix = eng.mlm_topk(torch.from_numpy(g["mlm_ids"][0]).cuda(), 60)
     torch.cuda.synchronize()
     np.testing.assert_allclose(sc.cpu().numpy(), g["mlm_top_scores"], atol=1e-3, rtol=0)
-    assert (ix.cpu().numpy() == g["mlm_top_ids"]).mean() > 0.98
+    # ids exact wherever the golden order is decided by more than twice the measured score error:
+    # a position is exempt only when its golden score is within 2·max|score - golden| of a
+    # neighbour's (a near-tie that error may reorder); the last position is exempt (the 61st
+    # golden score is unknown)
+    gs, gi, got = g["mlm_top_scores"], g["mlm_top_ids"], ix.cpu().numpy()
+    eps = 2.0 * float(np.abs(sc.cpu().numpy() - gs).max()) + 1e-7
+    prev = np.concatenate([np.full((gs.shape[0], 1), np.inf), gs[:, :-1]], 1)
+    nxt = np.concatenate([gs[:, 1:], np.full((gs.shape[0], 1), -np.inf)], 1)
+    clear = (np.abs(prev - gs) > eps) & (np.abs(gs - nxt) > eps)
+    clear[:, -1] = False
+    assert clear.mean() > 0.8, (clear.mean(), eps)
+    assert (got[clear] == gi[clear]).all(), np.argwhere((got != gi) & clear)[:5]
 
 
 def test_topk_kernel_exact_with_ties(gpu):

@@ -205,16 +205,18 @@ def _qkv_planes(qkv, np_):
     return _pack(hi, lo, np_)
 
 
+@pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("np_", [2, 1])
 @pytest.mark.parametrize("case", ["ragged", "mask", "cls", "planes"])
-def test_attention_pp_matches_f64(gpu, np_, case):
+def test_attention_pp_matches_f64(gpu, np_, case, variant):
     """attn_pp_kernel (packed-plane Q/K/V moved by LDS-DMA, swizzled K/V images, transposed V
     reads) against the float64 reference, for both plane counts (np 1 = bf16 mode: stated
-    tolerance 2e-2) and the ragged / mask / CLS-only / packed-output launches."""
+    tolerance 2e-2), both loops (variant 1: software-pipelined) and the ragged / mask /
+    CLS-only / packed-output launches."""
     lib = _lib()
     vp, i32 = ctypes.c_void_p, ctypes.c_int32
-    lib.ae_launch_attention_pp.argtypes = [vp] * 5 + [i32] * 3 + [vp, i32, i32, vp]
-    lib.ae_launch_attention_pp.restype = ctypes.c_int
+    lib.ae_bench_attention_pp.argtypes = [vp] * 5 + [i32] * 3 + [vp, i32, i32, i32, vp]
+    lib.ae_bench_attention_pp.restype = ctypes.c_int
     g = torch.Generator().manual_seed(11 + np_)
     lens = [1, 31, 32, 33, 129, 300, 64] if case != "mask" else [40, 97, 128]
     n = len(lens)
@@ -237,8 +239,9 @@ def test_attention_pp_matches_f64(gpu, np_, case):
     op = torch.zeros((T, np_ * 768), dtype=torch.bfloat16, device="cuda") if case == "planes" else None
     one = torch.ones(1, dtype=torch.int32, device="cuda") if case == "cls" else None
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    rc = lib.ae_launch_attention_pp(_p(dq), _p(out), _p(op), _p(dcu), _p(one),
-                                    1 if case == "cls" else max(lens), n, 12, _p(dmask), L, np_, st)
+    rc = lib.ae_bench_attention_pp(_p(dq), _p(out), _p(op), _p(dcu), _p(one),
+                                   1 if case == "cls" else max(lens), n, 12, _p(dmask), L, np_,
+                                   variant, st)
     assert rc == 0
     torch.cuda.synchronize()
     if case == "planes":

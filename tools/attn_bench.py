@@ -56,8 +56,8 @@ def main():
     fn = lib.ae_bench_attention_x3
     fn.argtypes = [vp] * 5 + [i32] * 3 + [vp, i32, i32, i32, vp]
     fn.restype = ctypes.c_int
-    fpp = lib.ae_launch_attention_pp  # variant "pp": packed-plane input (Q pre-scaled), LDS-DMA
-    fpp.argtypes = [vp] * 5 + [i32] * 3 + [vp, i32, i32, vp]
+    fpp = lib.ae_bench_attention_pp  # variants "pp" / "pp1": packed-plane input, LDS-DMA
+    fpp.argtypes = [vp] * 5 + [i32] * 3 + [vp, i32, i32, i32, vp]
     fpp.restype = ctypes.c_int
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream(dev)
@@ -89,11 +89,12 @@ def main():
         [hi.view(T, -1, 32), lo.view(T, -1, 32)], 2).reshape(T, 2 * 3 * H).contiguous()
     cases = []
     for v in args.variants.split(","):
-        var = v if v == "pp" else int(v)
+        var = v if v.startswith("pp") else int(v)
         out = torch.zeros((T, H), device=dev)
-        if var == "pp":
-            call = (lambda out=out: fpp(p(planes), p(out), p(None), p(cu_d), p(None),
-                                        int(lens.max()), n, HEADS, p(None), 0, np_, sp))
+        if isinstance(var, str):
+            pv = 1 if var == "pp1" else 0
+            call = (lambda out=out, pv=pv: fpp(p(planes), p(out), p(None), p(cu_d), p(None),
+                                               int(lens.max()), n, HEADS, p(None), 0, np_, pv, sp))
         else:
             call = (lambda out=out, var=var: fn(p(qkv), p(out), p(None), p(cu_d), p(None),
                                                 int(lens.max()), n, HEADS, p(None), 0, args.terms,
