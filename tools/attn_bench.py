@@ -92,7 +92,7 @@ def main():
         var = v if v.startswith("pp") else int(v)
         out = torch.zeros((T, H), device=dev)
         if isinstance(var, str):
-            pv = 1 if var == "pp1" else 0
+            pv = int(var[2:]) if len(var) > 2 else 0
             call = (lambda out=out, pv=pv: fpp(p(planes), p(out), p(None), p(cu_d), p(None),
                                                int(lens.max()), n, HEADS, p(None), 0, np_, pv, sp))
         else:
