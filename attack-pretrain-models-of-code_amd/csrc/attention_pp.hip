@@ -80,22 +80,11 @@ __global__ __launch_bounds__(256, 2) void attn_pp_kernel(const unsigned short* _
                                                          const int* __restrict__ cu,
                                                          const int* __restrict__ q_rows,
                                                          const uint32_t* __restrict__ mask,
-                                                         int mask_L, int remap) {
+                                                         int mask_L) {
   using P = PPL<NP>;
   constexpr int TERMS = NP == 2 ? 3 : 1;
   __shared__ __attribute__((aligned(16))) unsigned char lds[P::LDS];
-  // remap: XCD-aware order — workgroup ids w and w + 8 share an XCD, so consecutive logical ids
-  // (the q-blocks of one (sequence, head), then its neighbouring heads) are dealt to one XCD and
-  // its L2 serves their shared K/V tiles instead of every q-block refetching them on another XCD
-  int seq = blockIdx.z, head = blockIdx.y, qb = blockIdx.x;
-  if (remap) {
-    const int gx = gridDim.x, gy = gridDim.y;
-    const int lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-    const int t = xcd_remap(lin, gx * gy * gridDim.z);
-    qb = t % gx;
-    head = (t / gx) % gy;
-    seq = t / (gx * gy);
-  }
+  const int seq = blockIdx.z, head = blockIdx.y, qb = blockIdx.x;
   const int start = cu[seq];
   const int len = cu[seq + 1] - start;
   const int nq = q_rows ? min(len, q_rows[0]) : len;
@@ -346,13 +335,13 @@ namespace {
 template <bool PIPE>
 hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op, const int* cu,
                       const int* q_rows, int max_q, int n, int heads, const uint32_t* mask,
-                      int mask_L, int np, hipStream_t stream, int remap) {
+                      int mask_L, int np, hipStream_t stream) {
   if (n <= 0 || max_q <= 0) return hipSuccess;
   if (np != 1 && np != 2) return hipErrorInvalidValue;
   dim3 grid((max_q + QPB - 1) / QPB, heads, n), block(256);
 #define APP_LAUNCH(N, M, PL)                                                                 \
   hipLaunchKernelGGL((attn_pp_kernel<N, M, PL, PIPE>), grid, block, 0, stream, qkvp, out, op, cu, \
-                     q_rows, mask, mask_L, remap)
+                     q_rows, mask, mask_L)
 #define APP_MP(N)                                                      \
   if (op) {                                                            \
     if (mask) APP_LAUNCH(N, true, true); else APP_LAUNCH(N, false, true);   \
@@ -368,7 +357,6 @@ hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op
 #undef APP_LAUNCH
   return hipGetLastError();
 }
-constexpr int APP_REMAP = 0;  // XCD-aware workgroup order (A/B: variant 2 vs 1)
 constexpr bool APP_PIPE = true;  // production loop (tools/attn_bench.py A/B: pp1 190 us vs pp 203 us)
 }  // namespace
 
@@ -377,20 +365,19 @@ extern "C" hipError_t ae_launch_attention_pp(const unsigned short* qkvp, float* 
                                              int max_q, int n, int heads, const uint32_t* mask,
                                              int mask_L, int np, hipStream_t stream) {
   return app_launch<APP_PIPE>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np,
-                              stream, APP_REMAP);
+                              stream);
 }
 
-// Kernel experiments (tools/attn_bench.py, tests): variant 0 = two-stage loop, 1 = pipelined,
-// 2 = pipelined with the XCD-aware workgroup order.
+// Kernel experiments (tools/attn_bench.py, tests): variant 0 = two-stage loop, 1 = pipelined.
+// (An XCD-aware workgroup order — the q-blocks of one (sequence, head) on one XCD — measured 2-3 %
+// slower, profiles/r2i_attn_pp_ab.jsonl: the K/V re-reads are Infinity-Cache hits, not the bound.)
 extern "C" hipError_t ae_bench_attention_pp(const unsigned short* qkvp, float* out,
                                             unsigned short* op, const int* cu, const int* q_rows,
                                             int max_q, int n, int heads, const uint32_t* mask,
                                             int mask_L, int np, int variant, hipStream_t stream) {
-  if (variant == 1 || variant == 2)
-    return app_launch<true>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream,
-                            variant == 2);
+  if (variant == 1)
+    return app_launch<true>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
   if (variant == 0)
-    return app_launch<false>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream,
-                             0);
+    return app_launch<false>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
   return hipErrorInvalidValue;
 }

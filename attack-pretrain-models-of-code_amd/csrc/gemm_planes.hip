@@ -435,7 +435,7 @@ template <int NP, int EPI, int DIAG>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
     const __bf16* __restrict__ A, const __bf16* __restrict__ W, const float* __restrict__ bias,
     const float* __restrict__ R, float* __restrict__ C, __bf16* __restrict__ Cp, int M, int N,
-    int K, int group_m, int stagger) {
+    int K, int group_m) {
   extern __shared__ __attribute__((aligned(16))) unsigned char pk_smem[];
   constexpr int BM = 256, BN = 256, ROWB = PK_ROWB;
   constexpr int A_BYTES = BM * ROWB, STAGE = (BM + BN) * ROWB;  // 64 KiB per K-tile
@@ -451,17 +451,6 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
   const int gsize = min(tiles_m - first_m, group_m);
   const int tm0 = first_m + (t - g * per_group) % gsize, tn0 = (t - g * per_group) / gsize;
   const int m0 = tm0 * BM, n0 = tn0 * BN;
-  // experiment (ae_bench_gemm_packed diag 1xx / 2xx; 0 in production): the first round of
-  // workgroups starts in 2 (or 4) phases `stagger` ticks of the 100-MHz clock apart, so that the
-  // epilogue write bursts of later rounds do not hit HBM from every CU at once
-  if (stagger > 0 && blockIdx.x < (unsigned)(stagger >> 20)) {  // (cus << 20 | phases << 16 | ticks)
-    const int phases = (stagger >> 16) & 15, ticks = stagger & 0xffff;
-    const int ph = (blockIdx.x >> 3) & (phases - 1);
-    if (ph) {
-      const uint64_t t0 = wall_clock64();
-      while (wall_clock64() - t0 < (uint64_t)(ph * ticks)) __builtin_amdgcn_s_sleep(8);
-    }
-  }
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -941,8 +930,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
 namespace {
 template <int NP, int EPI, int DIAG>
 hipError_t pp_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R, float* C,
-                     __bf16* Cp, int M, int N, int K, int group_m, hipStream_t st,
-                     int stagger = 0) {
+                     __bf16* Cp, int M, int N, int K, int group_m, hipStream_t st) {
   constexpr int lds = 2 * (256 + 256) * PK_ROWB;  // 128 KiB
   static bool attr_set = false;
   if (!attr_set) {
@@ -953,7 +941,7 @@ hipError_t pp_launch(const __bf16* A, const __bf16* W, const float* bias, const 
   }
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
   hipLaunchKernelGGL((gemm_pp_kernel<NP, EPI, DIAG>), dim3(tiles), dim3(512), lds, st, A, W, bias,
-                     R, C, Cp, M, N, K, group_m, stagger);
+                     R, C, Cp, M, N, K, group_m);
   return hipGetLastError();
 }
 
@@ -1144,18 +1132,6 @@ extern "C" hipError_t ae_bench_gemm_packed(const unsigned short* A, const unsign
       (bn != 0 && bn != 128 && bn != 192 && bn != 256 && bn != 512))
     return hipErrorInvalidValue;
   if (bn == 192) return pp192_dispatch(A, W, bias, R, C, M, N, K, epi, np, PK_GROUP_M, st);
-  if (bn == 512 && diag >= 100) {  // staggered first round: 1tt = 2 phases, 2tt = 4, tt·100 ticks
-    if (np != 2) return hipErrorInvalidValue;
-    const int stg = (cu_count() << 20) | ((diag >= 200 ? 4 : 2) << 16) | ((diag % 100) * 100);
-    auto a = reinterpret_cast<const __bf16*>(A);
-    auto w = reinterpret_cast<const __bf16*>(W);
-    auto cp = reinterpret_cast<__bf16*>(Cp);
-    if (epi == PK_EPI_GELU_PACKED)
-      return pp_launch<2, PK_EPI_GELU_PACKED, 0>(a, w, bias, R, C, cp, M, N, K, PK_GROUP_M, st, stg);
-    if (epi == PK_EPI_BIAS)
-      return pp_launch<2, PK_EPI_BIAS, 0>(a, w, bias, R, C, cp, M, N, K, PK_GROUP_M, st, stg);
-    return hipErrorInvalidValue;
-  }
   if (bn == 512) {  // the ping-pong 256 x 256 kernel
     switch (diag) {
       case 0: return pp_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
