@@ -21,10 +21,10 @@
 
 extern "C" {
 hipError_t ae_launch_gemm_f32(const float*, const float*, const float*, const float*, float*, int,
-                              int, int, int, int, int, int, const int*, hipStream_t);
+                              int, int, int, int, int, int, const int*, hipStream_t, float*, long);
 hipError_t ae_launch_gemm_x3(const float*, const unsigned short*, const unsigned short*,
                              const float*, const float*, float*, int, int, int, int, int, int,
-                             int, int, hipStream_t);
+                             int, int, hipStream_t, float*, long);
 hipError_t ae_launch_attention_f32(const float*, float*, const int*, const int*, int, int, int,
                                    const uint32_t*, int, hipStream_t);
 hipError_t ae_launch_attention_pp(const unsigned short*, float*, unsigned short*, const int*,
@@ -109,6 +109,9 @@ struct ae_engine {
   int *tok_ids = nullptr, *tok_pos = nullptr, *src_col = nullptr, *cu = nullptr, *one = nullptr;
   int* err = nullptr;  // device flag: some row's lens disagreed with its ids (compact_kernel)
   float* logits = nullptr;
+  // split-K partials of the small GEMMs (last-layer CLS rows, classifier head): 64 MB
+  static constexpr long kSplitKFloats = 16L << 20;
+  float* skws = nullptr;
   size_t cap_logits = 0;
   int* pinned_cu = nullptr;
   size_t cap_pinned = 0;
@@ -304,9 +307,11 @@ int gemm(ae_engine* e, const float* A, const float* W, const unsigned short* Wh,
   Prof p(e, st, prof, 2.0 * M * N * K);
   if (e->cfg.precision != AE_PREC_FP32 && Wh) {
     const int terms = e->cfg.precision == AE_PREC_F32X3 ? 3 : 1;
-    HIPC(ae_launch_gemm_x3(A, Wh, Wl, bias, R, C, M, N, K, K, K, N, epi, terms, st));
+    HIPC(ae_launch_gemm_x3(A, Wh, Wl, bias, R, C, M, N, K, K, K, N, epi, terms, st, e->skws,
+                           ae_engine::kSplitKFloats));
   } else {
-    HIPC(ae_launch_gemm_f32(A, W, bias, R, C, M, N, K, K, K, N, epi, nullptr, st));
+    HIPC(ae_launch_gemm_f32(A, W, bias, R, C, M, N, K, K, K, N, epi, nullptr, st, e->skws,
+                            ae_engine::kSplitKFloats));
   }
   return AE_OK;
 }
@@ -554,7 +559,8 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
     UP("lm_head.bias", V, &e->lm_bias);  // decoder weight is tied to word_embeddings
   }
 #undef UP
-  if ((rc = dev_alloc(e, (void**)&e->one, 16)) || (rc = dev_alloc(e, (void**)&e->err, 16))) {
+  if ((rc = dev_alloc(e, (void**)&e->one, 16)) || (rc = dev_alloc(e, (void**)&e->err, 16)) ||
+      (rc = dev_alloc(e, (void**)&e->skws, (size_t)ae_engine::kSplitKFloats * 4))) {
     ae_destroy(e);
     return fail(rc, "alloc");
   }
@@ -626,7 +632,8 @@ static int score_impl(ae_engine* e, const int32_t* ids, const int32_t* lens, con
   // out_proj + sigmoid/softmax
   const int in_dim = kind == 2 ? 2 * e->cfg.hidden : e->cfg.hidden;
   HIPC(ae_launch_gemm_f32(e->xc, e->hd_w, e->hd_b, nullptr, e->tc, n_out, e->cfg.hidden, in_dim,
-                          in_dim, in_dim, e->cfg.hidden, EPI_BIAS_TANH, nullptr, st));
+                          in_dim, in_dim, e->cfg.hidden, EPI_BIAS_TANH, nullptr, st, e->skws,
+                          ae_engine::kSplitKFloats));
   HIPC(ae_launch_head_out(e->tc, e->ho_w, e->ho_b, kind, e->cfg.num_labels, n_out, probs_out,
                           e->err, st));
   return AE_OK;
@@ -675,11 +682,11 @@ int mlm_logits(ae_engine* e, int64_t T, hipStream_t st) {
     e->cap_logits = (size_t)T * V;
   }
   HIPC(ae_launch_gemm_f32(e->x, e->lm_dw, e->lm_db, nullptr, e->tmp, (int)T, H, H, H, H, H,
-                          EPI_BIAS_GELU, nullptr, st));
+                          EPI_BIAS_GELU, nullptr, st, e->skws, ae_engine::kSplitKFloats));
   HIPC(ae_launch_layernorm(e->tmp, e->lm_lg, e->lm_lb, e->cfg.ln_eps, (int)T, e->ctx, nullptr, 0,
                            st));
   HIPC(ae_launch_gemm_f32(e->ctx, e->wemb, e->lm_bias, nullptr, e->logits, (int)T, V, H, H, H, V,
-                          EPI_BIAS, nullptr, st));
+                          EPI_BIAS, nullptr, st, e->skws, ae_engine::kSplitKFloats));
   return AE_OK;
 }
 }  // namespace

@@ -21,18 +21,24 @@ constexpr int BM = 128, BN = 128, BK = 32, LDS_STRIDE = 36;
 
 enum { EPI_BIAS = 0, EPI_BIAS_GELU = 1, EPI_BIAS_RESIDUAL = 2, EPI_BIAS_TANH = 3 };
 
+// Segmented split-K as in gemm_x3.hip: the K range is cut into `segs` segments (a function of K
+// alone); unsplit, one workgroup adds each segment's accumulator into a running total; split
+// (part != nullptr), workgroup (tile, s) writes segment s to part[s][M][N] for
+// ae_launch_splitk_reduce — the same sums in the same order, so scores stay batch-invariant.
 template <int EPI>
 __global__ __launch_bounds__(256, 2) void gemm_f32_nt_kernel(
     const float* __restrict__ A, const float* __restrict__ W, const float* __restrict__ bias,
     const float* __restrict__ R, float* __restrict__ C, int M, int N, int K, int lda, int ldw,
-    int ldc, const int* __restrict__ row_map) {
+    int ldc, const int* __restrict__ row_map, int segs, float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) float As[2][BM * LDS_STRIDE];
   __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDS_STRIDE];
 
   const int tiles_n = (N + BN - 1) / BN;
   const int tiles_m = (M + BM - 1) / BM;
   const int nwg = tiles_m * tiles_n;
-  const int t = xcd_remap(blockIdx.x, nwg);
+  const int nsplit = part ? segs : 1;
+  const int t_all = xcd_remap(blockIdx.x, nwg * nsplit);
+  const int t = t_all / nsplit, sp = t_all % nsplit;
   const int tm = t / tiles_n, tn = t % tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
 
@@ -81,14 +87,24 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_nt_kernel(
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
-  const int nk = K / BK;
-  gload(0);
+  const int nk_all = K / BK;
+  const int kb = part ? sp * nk_all / segs : 0;
+  const int ke = part ? (sp + 1) * nk_all / segs : nk_all;
+  floatx16 tot[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tot[a][b][r] = 0.f;
+  int seg = 0, seg_end = part ? ke : nk_all / segs;
+  gload(kb * BK);
   lstore(0);
   __syncthreads();
 
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * BK);
+  for (int kt = kb; kt < ke; ++kt) {
+    const int cur = (kt - kb) & 1;
+    if (kt + 1 < ke) gload((kt + 1) * BK);
     const float* as = &As[cur][(wm * 64 + li) * LDS_STRIDE + 16 * lh];
     const float* bs = &Bs[cur][(wn * 64 + li) * LDS_STRIDE + 16 * lh];
 #pragma unroll
@@ -105,7 +121,19 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_nt_kernel(
         acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[e], b1[e], acc[1][1], 0, 0, 0);
       }
     }
-    if (kt + 1 < nk) lstore(cur ^ 1);
+    if (!part && kt + 1 == seg_end) {  // close a segment: total += its accumulator
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          tot[a][b] += acc[a][b];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+        }
+      ++seg;
+      seg_end = (seg + 1) * nk_all / segs;
+    }
+    if (kt + 1 < ke) lstore(cur ^ 1);
     __syncthreads();
   }
 
@@ -116,12 +144,20 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_nt_kernel(
     for (int b = 0; b < 2; ++b) {
       const int col = n0 + wn * 64 + b * 32 + li;
       if (col >= N) continue;
+      if (part) {  // raw segment accumulator; the reduce adds bias + epilogue
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm * 64 + a * 32 + mfma32_row(r, lh);
+          if (row < M) part[((size_t)sp * M + row) * N + col] = acc[a][b][r];
+        }
+        continue;
+      }
       const float bv = bias[col];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * 64 + a * 32 + mfma32_row(r, lh);
         if (row < M) {
-          float v = acc[a][b][r] + bv;
+          float v = tot[a][b][r] + bv;
           if (EPI == EPI_BIAS_GELU) v = gelu_erf(v);
           if (EPI == EPI_BIAS_TANH) v = tanhf(v);
           if (EPI == EPI_BIAS_RESIDUAL) v += R[(size_t)row * ldc + col];
@@ -132,32 +168,48 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_nt_kernel(
   }
 }
 
+extern "C" hipError_t ae_launch_splitk_reduce(const float* part, int segs, int M, int N,
+                                              const float* bias, const float* R, float* C, int ldc,
+                                              int epi, hipStream_t st);
+
+// K segments of this kernel (a function of K alone, ~3 K-tiles each, at most 8)
+extern "C" int ae_splitk_segments_f32(int K) {
+  const int s = (K / BK) / 3;
+  return s < 1 ? 1 : (s > 8 ? 8 : s);
+}
+
 // Host launcher.  row_map (device, optional) gathers A rows: A row r of the product is
-// A[row_map[r]] (used to run the last layer on CLS rows only).
+// A[row_map[r]] (used to run the last layer on CLS rows only).  A grid of fewer than 128 tiles
+// takes the split-K form when ws (ws_floats f32) holds the segment partials.
 extern "C" hipError_t ae_launch_gemm_f32(const float* A, const float* W, const float* bias,
                                          const float* R, float* C, int M, int N, int K, int lda,
                                          int ldw, int ldc, int epi, const int* row_map,
-                                         hipStream_t stream) {
+                                         hipStream_t stream, float* ws, long ws_floats) {
   if (M <= 0) return hipSuccess;
   if (K % BK != 0) return hipErrorInvalidValue;
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  dim3 grid(tiles), block(256);
+  const int segs = ae_splitk_segments_f32(K);
+  float* part = (segs > 1 && tiles < 128 && N % 4 == 0 && (long)segs * M * N <= ws_floats)
+                    ? ws : nullptr;
+  dim3 grid(tiles * (part ? segs : 1)), block(256);
   switch (epi) {
     case EPI_BIAS:
       hipLaunchKernelGGL(gemm_f32_nt_kernel<EPI_BIAS>, grid, block, 0, stream, A, W, bias, R, C, M,
-                         N, K, lda, ldw, ldc, row_map);
+                         N, K, lda, ldw, ldc, row_map, segs, part);
       break;
     case EPI_BIAS_GELU:
       hipLaunchKernelGGL(gemm_f32_nt_kernel<EPI_BIAS_GELU>, grid, block, 0, stream, A, W, bias, R,
-                         C, M, N, K, lda, ldw, ldc, row_map);
+                         C, M, N, K, lda, ldw, ldc, row_map, segs, part);
       break;
     case EPI_BIAS_TANH:
       hipLaunchKernelGGL(gemm_f32_nt_kernel<EPI_BIAS_TANH>, grid, block, 0, stream, A, W, bias, R,
-                         C, M, N, K, lda, ldw, ldc, row_map);
+                         C, M, N, K, lda, ldw, ldc, row_map, segs, part);
       break;
     default:
       hipLaunchKernelGGL(gemm_f32_nt_kernel<EPI_BIAS_RESIDUAL>, grid, block, 0, stream, A, W, bias,
-                         R, C, M, N, K, lda, ldw, ldc, row_map);
+                         R, C, M, N, K, lda, ldw, ldc, row_map, segs, part);
   }
-  return hipGetLastError();
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !part) return e;
+  return ae_launch_splitk_reduce(part, segs, M, N, bias, R, C, ldc, epi, stream);
 }

@@ -32,11 +32,19 @@ __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >>
 
 enum { X3_EPI_BIAS = 0, X3_EPI_GELU = 1, X3_EPI_RES = 2, X3_EPI_TANH = 3 };
 
+// Split-K without losing batch invariance (SEG = true, the 128 x 128 configuration): the K range
+// is cut into `segs` segments that depend on K only (splitk_segments); every output is
+// acc(seg 0) + acc(seg 1) + ... summed in segment order.  Unsplit (part == nullptr) one workgroup
+// walks all segments, adding each segment's accumulator into a running total; split, workgroup
+// (tile, s) computes segment s alone into part[s][M][N] and splitk_reduce_kernel adds them in
+// the same order — bit-identical, so a row's score does not depend on how many rows share the
+// launch (small launches such as the last layer's CLS rows take the split form to fill the chip).
 template <int BM, int BN, int WM, int WN, int TERMS, int EPI>
 __global__ __launch_bounds__(512, (BM * BN >= 256 * 256 ? 2 : 4)) void gemm_x3_kernel(
     const float* __restrict__ A, const __bf16* __restrict__ Whi, const __bf16* __restrict__ Wlo,
     const float* __restrict__ bias, const float* __restrict__ R, float* __restrict__ C, int M,
-    int N, int K, int lda, int ldw, int ldc) {
+    int N, int K, int lda, int ldw, int ldc, int segs, float* __restrict__ part) {
+  constexpr bool SEG = BM * BN < 256 * 256;
   constexpr int NA = TERMS == 3 ? 2 : 1;      // A planes (hi[, lo])
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB;
@@ -46,7 +54,9 @@ __global__ __launch_bounds__(512, (BM * BN >= 256 * 256 ? 2 : 4)) void gemm_x3_k
 
   const int tiles_n = (N + BN - 1) / BN;
   const int tiles_m = (M + BM - 1) / BM;
-  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int nsplit = part ? segs : 1;
+  const int t_all = xcd_remap(blockIdx.x, tiles_m * tiles_n * nsplit);
+  const int t = t_all / nsplit, sp = t_all % nsplit;
   const int tm = t / tiles_n, tn = t % tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
 
@@ -132,14 +142,27 @@ __global__ __launch_bounds__(512, (BM * BN >= 256 * 256 ? 2 : 4)) void gemm_x3_k
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
-  const int nk = K / BK;
-  gload(0);
+  // K-tiles [kb, ke): the whole K, or segment sp of a split launch
+  const int nk_all = K / BK;
+  const int kb = part ? sp * nk_all / segs : 0;
+  const int ke = part ? (sp + 1) * nk_all / segs : nk_all;
+  floatx16 tot[SEG ? TM : 1][SEG ? TN : 1];
+  if (SEG) {
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tot[a][b][r] = 0.f;
+  }
+  int seg = 0, seg_end = (SEG && !part) ? nk_all / segs : ke;
+  gload(kb * BK);
   lstore(0);
   __syncthreads();
 
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * BK);
+  for (int kt = kb; kt < ke; ++kt) {
+    const int cur = (kt - kb) & 1;
+    if (kt + 1 < ke) gload((kt + 1) * BK);
     const unsigned char* st = lds + cur * STAGE_B;
     const unsigned char* sb = st + NA * A_BYTES;
 #pragma unroll
@@ -171,8 +194,26 @@ __global__ __launch_bounds__(512, (BM * BN >= 256 * 256 ? 2 : 4)) void gemm_x3_k
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
         }
     }
-    if (kt + 1 < nk) lstore(cur ^ 1);
+    if (SEG && !part && kt + 1 == seg_end) {  // close a segment: total += its accumulator
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          tot[a][b] += acc[a][b];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+        }
+      ++seg;
+      seg_end = (seg + 1) * nk_all / segs;
+    }
+    if (kt + 1 < ke) lstore(cur ^ 1);
     __syncthreads();
+  }
+  if (SEG && !part) {
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) acc[a][b] = tot[a][b];
   }
 
 #pragma unroll
@@ -181,12 +222,20 @@ __global__ __launch_bounds__(512, (BM * BN >= 256 * 256 ? 2 : 4)) void gemm_x3_k
     for (int b = 0; b < TN; ++b) {
       const int col = n0 + wn * (BN / WN) + b * 32 + li;
       if (col >= N) continue;
+      if (part) {  // raw segment accumulator; splitk_reduce_kernel adds bias + epilogue
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm * (BM / WM) + a * 32 + mfma32_row(r, lh);
+          if (row < M) part[((size_t)sp * M + row) * N + col] = acc[a][b][r];
+        }
+        continue;
+      }
       const float bv = bias[col];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * (BM / WM) + a * 32 + mfma32_row(r, lh);
         if (row < M) {
-          float v = acc[a][b][r] + bv;
+          float v = (0.f + acc[a][b][r]) + bv;
           if (EPI == X3_EPI_GELU) v = gelu_erf(v);
           if (EPI == X3_EPI_TANH) v = tanhf(v);
           if (EPI == X3_EPI_RES) v += R[(size_t)row * ldc + col];
@@ -197,16 +246,65 @@ __global__ __launch_bounds__(512, (BM * BN >= 256 * 256 ? 2 : 4)) void gemm_x3_k
   }
 }
 
+// part[s][M][N] (s < segs) -> C = epilogue(Σ_s part[s] + bias), summed in segment order
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part,
+                                                            int segs, int M, int N,
+                                                            const float* __restrict__ bias,
+                                                            const float* __restrict__ R,
+                                                            float* __restrict__ C, int ldc,
+                                                            int epi) {
+  const int n4 = N >> 2;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)M * n4) return;
+  const int row = (int)(i / n4), c = (int)(i % n4) * 4;
+  floatx4 v = {0.f, 0.f, 0.f, 0.f};
+  for (int sg = 0; sg < segs; ++sg)
+    v += *reinterpret_cast<const floatx4*>(part + ((size_t)sg * M + row) * N + c);
+  v += *reinterpret_cast<const floatx4*>(bias + c);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (epi == X3_EPI_GELU) v[e] = gelu_erf(v[e]);
+    if (epi == X3_EPI_TANH) v[e] = tanhf(v[e]);
+  }
+  if (epi == X3_EPI_RES) v += *reinterpret_cast<const floatx4*>(R + (size_t)row * ldc + c);
+  *reinterpret_cast<floatx4*>(C + (size_t)row * ldc + c) = v;
+}
+
+// K segments of the split-K scheme: a function of K alone (batch invariance), ~6 K-tiles each
+extern "C" int ae_splitk_segments(int K) {
+  const int nk = K / BK;
+  const int s = nk / 6;
+  return s < 1 ? 1 : (s > 8 ? 8 : s);
+}
+
+// split when the tile grid covers less than half the CUs and the workspace holds the partials
+extern "C" int ae_splitk_use(int tiles, int M, int N, int K, long ws_floats) {
+  const int segs = ae_splitk_segments(K);
+  return segs > 1 && tiles < 128 && (N % 4) == 0 && (long)segs * M * N <= ws_floats;
+}
+
+extern "C" hipError_t ae_launch_splitk_reduce(const float* part, int segs, int M, int N,
+                                              const float* bias, const float* R, float* C, int ldc,
+                                              int epi, hipStream_t st) {
+  const long n = (long)M * (N / 4);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     part, segs, M, N, bias, R, C, ldc, epi);
+  return hipGetLastError();
+}
+
 namespace {
 template <int BM, int BN, int WM, int WN, int TERMS>
 hipError_t launch_cfg(const float* A, const __bf16* Whi, const __bf16* Wlo, const float* bias,
                       const float* R, float* C, int M, int N, int K, int lda, int ldw, int ldc,
-                      int epi, hipStream_t st) {
+                      int epi, hipStream_t st, float* ws, long ws_floats) {
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  dim3 grid(tiles), block(512);
+  constexpr bool SEG = BM * BN < 256 * 256;
+  const int segs = SEG ? ae_splitk_segments(K) : 1;
+  float* part = (SEG && ae_splitk_use(tiles, M, N, K, ws_floats)) ? ws : nullptr;
+  dim3 grid(tiles * (part ? segs : 1)), block(512);
 #define X3_LAUNCH(E)                                                                         \
   hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, TERMS, E>), grid, block, 0, st, A, Whi, \
-                     Wlo, bias, R, C, M, N, K, lda, ldw, ldc)
+                     Wlo, bias, R, C, M, N, K, lda, ldw, ldc, segs, part)
   switch (epi) {
     case X3_EPI_BIAS: X3_LAUNCH(X3_EPI_BIAS); break;
     case X3_EPI_GELU: X3_LAUNCH(X3_EPI_GELU); break;
@@ -214,16 +312,20 @@ hipError_t launch_cfg(const float* A, const __bf16* Whi, const __bf16* Wlo, cons
     default: X3_LAUNCH(X3_EPI_TANH);
   }
 #undef X3_LAUNCH
-  return hipGetLastError();
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !part) return e;
+  return ae_launch_splitk_reduce(part, segs, M, N, bias, R, C, ldc, epi, st);
 }
 }  // namespace
 
 // terms: 3 = split-bf16 (f32-class), 1 = plain bf16.  Tile shape chosen per problem so the grid
-// has >= ~1.5 waves of workgroups over 256 CUs.
+// has >= ~1.5 waves of workgroups over 256 CUs; small grids take the split-K form when the
+// caller's workspace ws (ws_floats f32) holds the partials (see gemm_x3_kernel).
 extern "C" hipError_t ae_launch_gemm_x3(const float* A, const unsigned short* Whi,
                                         const unsigned short* Wlo, const float* bias,
                                         const float* R, float* C, int M, int N, int K, int lda,
-                                        int ldw, int ldc, int epi, int terms, hipStream_t st) {
+                                        int ldw, int ldc, int epi, int terms, hipStream_t st,
+                                        float* ws, long ws_floats) {
   if (M <= 0) return hipSuccess;
   if (K % BK != 0) return hipErrorInvalidValue;
   const __bf16* wh = reinterpret_cast<const __bf16*>(Whi);
@@ -234,10 +336,14 @@ extern "C" hipError_t ae_launch_gemm_x3(const float* A, const unsigned short* Wh
   const bool big = big_tiles >= 512;
   if (terms == 3) {
     if (big)
-      return launch_cfg<256, 256, 2, 4, 3>(A, wh, wl, bias, R, C, M, N, K, lda, ldw, ldc, epi, st);
-    return launch_cfg<128, 128, 2, 4, 3>(A, wh, wl, bias, R, C, M, N, K, lda, ldw, ldc, epi, st);
+      return launch_cfg<256, 256, 2, 4, 3>(A, wh, wl, bias, R, C, M, N, K, lda, ldw, ldc, epi, st,
+                                           nullptr, 0);
+    return launch_cfg<128, 128, 2, 4, 3>(A, wh, wl, bias, R, C, M, N, K, lda, ldw, ldc, epi, st,
+                                         ws, ws_floats);
   }
   if (big)
-    return launch_cfg<256, 256, 2, 4, 1>(A, wh, wl, bias, R, C, M, N, K, lda, ldw, ldc, epi, st);
-  return launch_cfg<128, 128, 2, 4, 1>(A, wh, wl, bias, R, C, M, N, K, lda, ldw, ldc, epi, st);
+    return launch_cfg<256, 256, 2, 4, 1>(A, wh, wl, bias, R, C, M, N, K, lda, ldw, ldc, epi, st,
+                                         nullptr, 0);
+  return launch_cfg<128, 128, 2, 4, 1>(A, wh, wl, bias, R, C, M, N, K, lda, ldw, ldc, epi, st, ws,
+                                       ws_floats);
 }

@@ -239,3 +239,19 @@ def test_dataflow_mask_and_explicit_positions(gpu, precision, tol):
                     mask_bits=torch.from_numpy(_pack_mask(m)).cuda())
     torch.cuda.synchronize()
     np.testing.assert_allclose(out.cpu().numpy(), ref, atol=tol, rtol=0)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "f32x3"])
+@pytest.mark.parametrize("head,num_labels", [("sigmoid1", 1), ("pair2", 2)])
+def test_scores_batch_invariant_across_split_k(gpu, precision, head, num_labels):
+    """A row's probabilities do not depend on how many rows share the launch: 8 rows take the
+    segmented split-K form of the last layer's CLS GEMMs and the classifier head (grids of < 128
+    tiles), 3000 rows the unsplit form; both sum the same K segments in the same order, so the
+    8 rows' scores must be bit-identical (the batched attack drivers rely on this)."""
+    eng = _engine(4, head, num_labels, precision=precision)
+    rng = np.random.default_rng(21)
+    n, L = 3000, 16
+    ids = _rand_ids(rng, n, L, rng.integers(3, L + 1, n))
+    big = _score(eng, ids)
+    small = _score(eng, ids[:8])
+    assert np.array_equal(big[:8], small), np.abs(big[:8] - small).max()
