@@ -260,7 +260,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   floatx4 v = {0.f, 0.f, 0.f, 0.f};
   for (int sg = 0; sg < segs; ++sg)
     v += *reinterpret_cast<const floatx4*>(part + ((size_t)sg * M + row) * N + c);
-  v += *reinterpret_cast<const floatx4*>(bias + c);
+  if (bias) v += *reinterpret_cast<const floatx4*>(bias + c);
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     if (epi == X3_EPI_GELU) v[e] = gelu_erf(v[e]);
