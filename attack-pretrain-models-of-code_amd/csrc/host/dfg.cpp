@@ -381,6 +381,18 @@ class CTree {
         attach(fd, parameter_list());
         base = fd;
       } else if (at("__attribute__")) {
+        if (!in_param && base >= 0 && nodes[base].type == N_LEAF) {
+          // `TCGReg addrhi __attribute__((unused));`, `int x __attribute__((unused)) = 0;`:
+          // tree-sitter keeps the identifier as the declarator and puts the attribute (and an
+          // initialiser after it) in an ERROR node, so the name is defined (fixture keys)
+          while (p_ < n_ && !at(",") && !at(";")) {
+            const size_t q = p_;
+            const size_t end = (at("(") && match_[p_] > 0) ? (size_t)match_[p_] : p_;
+            for (size_t k = q; k <= end; ++k) strays_.push_back(k);
+            p_ = end + 1;
+          }
+          break;
+        }
         const int g = make(N_GENERIC);
         if (base >= 0) attach(g, base);
         attribute(g);
