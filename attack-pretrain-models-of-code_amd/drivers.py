@@ -174,7 +174,7 @@ def _totals(records, wall):
 
 
 def run_gi_attack_batched(model, codes, subs, labels, args: AttackArgs, indices=None, tok=None,
-                          queue=None, log=None, max_inflight=64):
+                          queue=None, log=None, max_inflight=64, pipeline=True):
     """greedy (+GA) over many examples at once: up to `max_inflight`
     examples' attacks are in flight, and every round answers all their pending victim requests
     with ONE device batch (Model.score_prepared), so the GPU sees thousands of rows instead of
@@ -196,23 +196,24 @@ def run_gi_attack_batched(model, codes, subs, labels, args: AttackArgs, indices=
         pos += 1
         return order[pos - 1]
 
-    done, live = {}, []  # live: [index, generator, pending payload, queries, t_start]
+    done = {}
     t0 = time.time()
     drained = False
-    while True:
-        while not drained and len(live) < max_inflight:
+
+    def refill(group, cap):
+        nonlocal drained
+        while not drained and len(group) < cap:
             index = next_index()
             if index is None:
                 drained = True
                 break
             gen = attack_one_gen(attacker, tok, codes[index], subs[index], labels[index], args,
                                  random.Random(args.seed + index))
-            live.append([index, gen, next(gen), 0, time.time()])
-        if not live:
-            break
-        answers = model.score_prepared([c[2] for c in live])
+            group.append([index, gen, next(gen), 0, time.time()])
+
+    def advance(group, answers):
         still = []
-        for c, ans in zip(live, answers):
+        for c, ans in zip(group, answers):
             c[3] += c[2].n
             try:
                 c[2] = c[1].send(ans)
@@ -222,7 +223,29 @@ def run_gi_attack_batched(model, codes, subs, labels, args: AttackArgs, indices=
                 done[c[0]] = (res, attack_type, c[3], (time.time() - c[4]) / 60)
                 if log:
                     log(_record(c[0], *done[c[0]], None))
-        live = still
+        return still
+
+    # live entries: [index, generator, pending payload, queries, t_start].  With a model that can
+    # submit asynchronously the examples run as two groups: while one group's device batch runs,
+    # the host advances the other group's attacks (mutation, featurisation) on its answers.
+    groups = 2 if (pipeline and hasattr(model, "submit")) else 1
+    cap = max(1, max_inflight // groups)
+    live = [[] for _ in range(groups)]
+    pend = [None] * groups
+    while True:
+        for g in range(groups):
+            if pend[g] is not None:
+                live[g] = advance(live[g], pend[g].result())
+                pend[g] = None
+            refill(live[g], cap)
+            if live[g]:
+                payloads = [c[2] for c in live[g]]
+                if groups == 1:
+                    live[g] = advance(live[g], model.score_prepared(payloads))
+                else:
+                    pend[g] = model.submit(payloads)
+        if drained and not any(live) and all(x is None for x in pend):
+            break
     # CSV rows in example order, as the reference's loop writes them
     records = [_record(i, *done[i], recorder) for i in sorted(done)]
     return _totals(records, time.time() - t0)

@@ -444,15 +444,20 @@ class GraphModel(Model):
         """Device mask bits of one payload's rows."""
         import torch
 
+        from .model import to_device
+
         kind = p.extra[0]
         if kind == "bits":
-            return torch.from_numpy(np.ascontiguousarray(p.extra[2])).to(dev)
+            return to_device(p.extra[2], dev)
         c = p.extra[1]
-        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+        t = lambda a: to_device(a, dev)  # noqa: E731
         return self.engine.graph_mask(t(c["ids"]), t(c["meta"]), t(c["spans"]), t(c["edges"]))
 
     def score_payload_rows(self, live):
         """Logits of every row of the live payloads (device mask build for compact ones)."""
+        return self._score_payload_rows_dev(live).cpu().numpy()
+
+    def _score_payload_rows_dev(self, live):
         import torch
 
         dev = f"cuda:{self.engine.device}"
@@ -466,13 +471,15 @@ class GraphModel(Model):
         for p in live:
             bits_parts.append(self._bits_rows(p, dev))
         bits = torch.cat(bits_parts, 0) if len(bits_parts) > 1 else bits_parts[0]
-        ids_d = torch.from_numpy(np.ascontiguousarray(ids)).to(dev)
-        pos_d = torch.from_numpy(np.ascontiguousarray(pos)).to(dev)
+        from .model import to_device
+
+        ids_d = to_device(ids, dev)
+        pos_d = to_device(pos, dev)
         for s0 in range(0, n, step):
             e = min(n, s0 + step)
             lens = np.full((e - s0,), L, dtype=np.int32)
             outs.append(self.engine.score_graph(ids_d[s0:e], lens, pos_d[s0:e], bits[s0:e]))
-        return torch.cat(outs, 0).cpu().numpy() if len(outs) > 1 else outs[0].cpu().numpy()
+        return torch.cat(outs, 0) if len(outs) > 1 else outs[0]
 
     def prepare_population(self, example, tokenizer, population, mode: int, block_size: int):
         """A population of chromosomes of one program: mutant texts (host get_example(_batch))
@@ -491,6 +498,18 @@ class GraphModel(Model):
             out.append(self._format(logits[off:off + p.n], threshold) if p.n else ([], []))
             off += p.n
         return out
+
+    def submit(self, payloads, threshold: float = 0.5):
+        """score_prepared split in two (Model.submit): the batch is queued now, .result()
+        answers it."""
+        from .model import PendingScores, ScoresReady
+
+        self.query += sum(p.n for p in payloads)
+        live = [p for p in payloads if p.n]
+        if not live:
+            return ScoresReady([([], []) for _ in payloads])
+        return PendingScores(self._score_payload_rows_dev(live), payloads, self._format,
+                             threshold)
 
     def dataset_from_texts(self, texts, tokenizer, args, label=0):
         """Mutant texts -> the GCB attacker's convert_code_to_features of each

@@ -59,6 +59,52 @@ def _checked(logits: np.ndarray) -> np.ndarray:
     return logits
 
 
+def to_device(a, dev):
+    """Host array -> device tensor through pinned memory, non-blocking on the current stream:
+    a pageable .to(dev) synchronises the stream, which would stall the host behind the batch
+    already running (run_gi_attack_batched overlaps one group's host work with the other's
+    device batch).  The caching host allocator keeps the pinned buffer until the copy ran."""
+    import torch
+
+    t = a if torch.is_tensor(a) else torch.from_numpy(np.ascontiguousarray(a))
+    return t.pin_memory().to(dev, non_blocking=True)
+
+
+class ScoresReady:
+    """A submit() whose answers are already known (no live rows)."""
+
+    def __init__(self, out):
+        self.out = out
+
+    def result(self):
+        return self.out
+
+
+class PendingScores:
+    """The device scores of one submitted batch: the device-to-host copy is queued (pinned, non-
+    blocking) behind the kernels, so the caller can do host work for other examples while the
+    GPU runs; result() waits for this batch only and formats it per payload."""
+
+    def __init__(self, dev_logits, payloads, fmt, threshold):
+        import torch
+
+        self.dev = dev_logits  # alive until the copy has run
+        self.host = torch.empty(dev_logits.shape, dtype=dev_logits.dtype, pin_memory=True)
+        self.host.copy_(dev_logits, non_blocking=True)
+        self.ev = torch.cuda.Event()
+        self.ev.record()
+        self.payloads, self.fmt, self.threshold = payloads, fmt, threshold
+
+    def result(self):
+        self.ev.synchronize()
+        logits = _checked(self.host.numpy())
+        out, off = [], 0
+        for p in self.payloads:
+            out.append(self.fmt(logits[off:off + p.n], self.threshold) if p.n else ([], []))
+            off += p.n
+        return out
+
+
 class Model:
     """Victim model.  `encoder` is an `Engine` (or a state dict, from which one is built)."""
 
@@ -117,7 +163,7 @@ class Model:
         ids = np.ascontiguousarray(ids, dtype=np.int32)
         if lens is None:
             lens = (ids != self.engine.pad_id).sum(axis=1).astype(np.int32)
-        dev = torch.from_numpy(ids).to(f"cuda:{self.engine.device}")
+        dev = to_device(ids, f"cuda:{self.engine.device}")
         return Payload(dev, lens, n)
 
     def population_rows(self, example, tokenizer, population, mode: int, block_size: int):
@@ -141,11 +187,11 @@ class Model:
                     np.zeros((0,), np.int32))
         if self.raw:
             ids, lens = example.mutant_ids(tokenizer, population, block_size, mode | MODE_RAW)
-            return torch.from_numpy(ids).to(dev), lens
+            return to_device(ids, dev), lens
         word_tok, word_off, mut_words, mut_off, lens = example.mutant_words(
             tokenizer, population, block_size, mode)
-        ids, _ = splice(torch.from_numpy(word_tok).to(dev), torch.from_numpy(word_off).to(dev),
-                        torch.from_numpy(mut_words).to(dev), torch.from_numpy(mut_off).to(dev),
+        ids, _ = splice(to_device(word_tok, dev), to_device(word_off, dev),
+                        to_device(mut_words, dev), to_device(mut_off, dev),
                         n, block_size, tokenizer.cls_token_id, tokenizer.sep_token_id,
                         tokenizer.pad_token_id)
         return ids, lens
@@ -163,9 +209,9 @@ class Model:
 
         dev = f"cuda:{self.engine.device}"
         a = ids1 if torch.is_tensor(ids1) else torch.from_numpy(np.ascontiguousarray(ids1))
-        a = a.to(dev, dtype=torch.int32)
+        a = (a if a.is_cuda else to_device(a, dev)).to(dtype=torch.int32)
         n, L = a.shape
-        b = torch.from_numpy(np.ascontiguousarray(ids2_row, dtype=np.int32)).to(dev)
+        b = to_device(np.ascontiguousarray(ids2_row, dtype=np.int32), dev)
         rows = torch.stack([a, b.expand(n, L)], 1).reshape(2 * n, L).contiguous()
         lens = np.empty((2 * n,), np.int32)
         lens[0::2], lens[1::2] = np.asarray(lens1, np.int32), int(len2)
@@ -174,34 +220,35 @@ class Model:
     def score_prepared(self, payloads, threshold: float = 0.5):
         """Score payloads as one device batch; query += their total queries.  Returns one
         (probs, pred_labels) per payload, each exactly what get_results gives for it alone."""
+        return self.submit(payloads, threshold).result()
+
+    def submit(self, payloads, threshold: float = 0.5):
+        """score_prepared split in two: queue the device batch now (query += at once), answer
+        with .result() later (PendingScores)."""
         import torch
 
         nq = [p.n for p in payloads]
         self.query += sum(nq)
         live = [p for p in payloads if p.n]
         if not live:
-            return [([], []) for _ in payloads]
+            return ScoresReady([([], []) for _ in payloads])
         ids = torch.cat([p.ids for p in live], 0) if len(live) > 1 else live[0].ids
         lens = np.concatenate([p.lens for p in live]) if len(live) > 1 else live[0].lens
-        logits = self._score_dev(ids, lens)
-        out, off = [], 0
         per_row = 2 if self.task == "clone" else 1
-        for p in payloads:
-            k = p.n
-            out.append(self._format(logits[off:off + k], threshold) if k else ([], []))
-            off += k
-        assert off * per_row == ids.shape[0]
-        return out
+        assert sum(nq) * per_row == ids.shape[0]
+        return PendingScores(self._score_dev_async(ids, lens), payloads, self._format, threshold)
 
-    def _score_dev(self, ids, lens: np.ndarray) -> np.ndarray:
+    def _score_dev_async(self, ids, lens: np.ndarray):
         import torch
 
         n = ids.shape[0]
         step = self.max_rows_per_launch
         outs = [self.engine.score(ids[s:s + step].contiguous(), lens[s:s + step])
                 for s in range(0, n, step)]
-        return _checked(torch.cat(outs, 0).cpu().numpy() if len(outs) > 1 else
-                        outs[0].cpu().numpy())
+        return torch.cat(outs, 0) if len(outs) > 1 else outs[0]
+
+    def _score_dev(self, ids, lens: np.ndarray) -> np.ndarray:
+        return _checked(self._score_dev_async(ids, lens).cpu().numpy())
 
     def get_results(self, dataset, batch_size=None, threshold: float = 0.5):
         """(probs, pred_labels) exactly as the reference's get_results of this task."""
@@ -284,6 +331,10 @@ class HostIdsVictim:
         n, L = ids1.shape
         rows = np.stack([ids1, np.broadcast_to(np.asarray(ids2_row, np.int32), (n, L))], 1)
         return Payload(np.ascontiguousarray(rows.reshape(2 * n, L)), None, n)
+
+    def submit(self, payloads, threshold: float = 0.5):
+        """The asynchronous request API of Model, answered at once (host scoring)."""
+        return ScoresReady(self.score_prepared(payloads, threshold))
 
     def score_prepared(self, payloads, threshold: float = 0.5):
         self.query += sum(p.n for p in payloads)

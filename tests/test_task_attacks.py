@@ -150,6 +150,10 @@ def host_graph_victim(score, base):
             from apmc_amd.graph import payload_rows_host
             return self.score_packed(*payload_rows_host(live))
 
+        def submit(self, payloads, threshold=0.5):  # answered at once (host scoring)
+            from apmc_amd.model import ScoresReady
+            return ScoresReady(self.score_prepared(payloads, threshold))
+
     return HostGraphVictim()
 
 
