@@ -641,7 +641,6 @@ class MHM_Attacker:
         replace = self._replace_uid_random if original else self._replace_uid
         kind = "MHM-Origin" if original else "MHM"
         out = [None] * len(jobs)
-        live = []  # [job index, generator, pending (ids, lens), queries so far]
         nxt = 0
 
         def finish(j, value, q):
@@ -649,28 +648,51 @@ class MHM_Attacker:
             if on_done is not None:
                 on_done(j, value, q)
 
-        while nxt < len(jobs) or live:
-            while nxt < len(jobs) and len(live) < max_inflight:
+        def refill(group, cap):
+            nonlocal nxt
+            while nxt < len(jobs) and len(group) < cap:
                 subs, code, label, seed = jobs[nxt]
                 gen = self._run_gen(tokenizer, subs, code, label, _n_candi, _max_iter,
                                     _prob_threshold, replace, kind, random.Random(seed))
                 try:
-                    live.append([nxt, gen, next(gen), 0])
+                    group.append([nxt, gen, next(gen), 0])
                 except StopIteration as stop:
                     finish(nxt, stop.value, 0)
                 nxt += 1
-            if not live:
-                break
-            answers = self.classifier.score_prepared([c[2] for c in live])
+
+        def advance(group, answers):
             still = []
-            for c, ans in zip(live, answers):
+            for c, ans in zip(group, answers):
                 c[3] += c[2].n
                 try:
                     c[2] = c[1].send(ans)
                     still.append(c)
                 except StopIteration as stop:
                     finish(c[0], stop.value, c[3])
-            live = still
+            return still
+
+        # live entries: [job index, generator, pending payload, queries so far].  With a victim
+        # that can submit asynchronously the chains run as two groups: one group's device batch
+        # runs while the host advances the other group's chains (as run_gi_attack_batched).
+        clf = self.classifier
+        groups = 2 if hasattr(clf, "submit") else 1
+        cap = max(1, max_inflight // groups)
+        live = [[] for _ in range(groups)]
+        pend = [None] * groups
+        while True:
+            for g in range(groups):
+                if pend[g] is not None:
+                    live[g] = advance(live[g], pend[g].result())
+                    pend[g] = None
+                refill(live[g], cap)
+                if live[g]:
+                    payloads = [c[2] for c in live[g]]
+                    if groups == 1:
+                        live[g] = advance(live[g], clf.score_prepared(payloads))
+                    else:
+                        pend[g] = clf.submit(payloads)
+            if nxt >= len(jobs) and not any(live) and all(x is None for x in pend):
+                break
         return out
 
     def _candidates_result(self, rng, _tokens, _label, selected_uid, candi_token, candi_pairs,
