@@ -100,6 +100,9 @@ class PyTree {
   explicit PyTree(const std::vector<Leaf>& lv) : lv_(lv), n_(lv.size()) {
     kw.assign(n_, 0);
     match_.assign(n_, -1);
+    // token classes of find0's scan (integer compares instead of string compares per token)
+    cls_.assign(n_, 0);
+    for (size_t i = 0; i < n_; ++i) cls_[i] = (uint8_t)tok_class(lv[i].raw);
     std::vector<int> st;
     int depth = 0;
     for (size_t i = 0; i < n_; ++i) {
@@ -145,6 +148,7 @@ class PyTree {
   const std::vector<Leaf>& lv_;
   size_t n_;
   std::vector<int> match_;
+  std::vector<uint8_t> cls_;
   std::vector<Line> lines_;
   size_t li_ = 0;
   size_t p_ = 0, lim_ = 0;
@@ -191,22 +195,39 @@ class PyTree {
   void leaves_to(int parent, size_t e) {
     while (more() && p_ < e) add_leaf(parent, p_++);
   }
+  // find0's token classes: brackets, lambda, ':' and the targets it is called with
+  enum { K_OTHER, K_OPEN, K_LAMBDA, K_COLON, K_IN, K_SEMI, K_EQ, K_ELSE, K_COMMA, K_FOR };
+  static int tok_class(const std::string& x) {
+    if (x == "(" || x == "[" || x == "{") return K_OPEN;
+    if (x == "lambda") return K_LAMBDA;
+    if (x == ":") return K_COLON;
+    if (x == "in") return K_IN;
+    if (x == ";") return K_SEMI;
+    if (x == "=") return K_EQ;
+    if (x == "else") return K_ELSE;
+    if (x == ",") return K_COMMA;
+    if (x == "for") return K_FOR;
+    return K_OTHER;
+  }
   // first depth-0 occurrence of `s` in [p_, lim_) (a lambda's own ':' skipped), or lim_
   size_t find0(const char* s) const {
+    const int want = tok_class(s);
+    if (want == K_OTHER || want == K_OPEN || want == K_LAMBDA) std::abort();  // not a target
     int lambdas = 0;
-    for (size_t q = p_; q < lim_;) {
-      const std::string& x = t(q);
-      if (x == "(" || x == "[" || x == "{") {
+    const size_t end = std::min(lim_, n_);
+    for (size_t q = p_; q < end;) {
+      const int c = cls_[q];
+      if (c == K_OPEN) {
         q = close_of(q) + 1;
         continue;
       }
-      if (x == "lambda") ++lambdas;
-      else if (x == ":" && lambdas > 0) {
+      if (c == K_LAMBDA) ++lambdas;
+      else if (c == K_COLON && lambdas > 0) {
         --lambdas;
         ++q;
         continue;
       }
-      if (x == s) return q;
+      if (c == want) return q;
       ++q;
     }
     return lim_;

@@ -7,6 +7,7 @@
 #include <set>
 #include <string>
 #include <tuple>
+#include <unordered_map>
 #include <vector>
 
 #include "host.h"
@@ -16,34 +17,49 @@ namespace ah {
 using DfgStates = std::map<std::string, std::vector<int>>;
 
 // sorted(DFG, key=lambda x: x[1]) — Python's sort is stable
+// (a stable sort of an already ordered list is the identity, and most walk results arrive in leaf
+// order, so the O(n) check skips the sort's buffer and moves)
 inline void dfg_sort(std::vector<DfgEdge>& d) {
-  std::stable_sort(d.begin(), d.end(),
-                   [](const DfgEdge& a, const DfgEdge& b) { return a.idx < b.idx; });
+  auto by_idx = [](const DfgEdge& a, const DfgEdge& b) { return a.idx < b.idx; };
+  if (std::is_sorted(d.begin(), d.end(), by_idx)) return;
+  std::stable_sort(d.begin(), d.end(), by_idx);
 }
 
 inline void dfg_append(std::vector<DfgEdge>& a, std::vector<DfgEdge>&& b) {
+  if (a.empty()) {
+    a.swap(b);
+    return;
+  }
   a.insert(a.end(), std::make_move_iterator(b.begin()), std::make_move_iterator(b.end()));
 }
 
 // for / while bodies: entries with the same (code, idx, relation) are merged — from-codes as a
 // set, from-idxs as a sorted set — then ordered by idx over first-seen order (DFG_*.py `dic`)
 inline void dfg_merge_dup(std::vector<DfgEdge>& d) {
-  std::map<std::tuple<std::string, int, int>, size_t> pos;
+  // (idx, relation) -> positions in out; the code string is compared within the bucket
+  std::unordered_map<long long, std::vector<size_t>> pos;
+  pos.reserve(d.size());
   std::vector<DfgEdge> out;
+  out.reserve(d.size());
   for (auto& e : d) {
-    auto key = std::make_tuple(e.code, e.idx, (int)e.computed);
-    auto it = pos.find(key);
-    if (it == pos.end()) {
-      pos[key] = out.size();
-      out.push_back(e);
+    auto& bucket = pos[(long long)e.idx * 2 + (e.computed ? 1 : 0)];
+    size_t hit = (size_t)-1;
+    for (size_t p : bucket)
+      if (out[p].code == e.code) {
+        hit = p;
+        break;
+      }
+    if (hit == (size_t)-1) {
+      bucket.push_back(out.size());
+      out.push_back(std::move(e));
     } else {
-      DfgEdge& m = out[it->second];
+      DfgEdge& m = out[hit];
       for (auto& c : e.from_code)
         if (std::find(m.from_code.begin(), m.from_code.end(), c) == m.from_code.end())
           m.from_code.push_back(c);
-      std::set<int> s(m.from_idx.begin(), m.from_idx.end());
-      s.insert(e.from_idx.begin(), e.from_idx.end());
-      m.from_idx.assign(s.begin(), s.end());
+      m.from_idx.insert(m.from_idx.end(), e.from_idx.begin(), e.from_idx.end());
+      std::sort(m.from_idx.begin(), m.from_idx.end());
+      m.from_idx.erase(std::unique(m.from_idx.begin(), m.from_idx.end()), m.from_idx.end());
     }
   }
   dfg_sort(out);
