@@ -32,6 +32,7 @@
 #include <set>
 #include <unordered_set>
 
+#include "dfg_util.h"
 #include "host.h"
 
 namespace ah {
@@ -1143,10 +1144,9 @@ struct Walker {
       case N_IF: {
         States current = states;
         std::vector<States> others;
-        bool flag = false, tag = false;
+        bool flag = false;
         for (int k : n.kids) {
           const bool is_else = nd[k].type == N_LEAF && lv[nd[k].leaf].raw == "else";
-          if (is_else) tag = true;
           const bool in_if_list = is_else || nd[k].type == N_IF;
           if (!in_if_list && !flag) {
             append(dfg, walk(k, current));
@@ -1157,23 +1157,10 @@ struct Walker {
             others.push_back(std::move(ns));
           }
         }
-        others.push_back(current);
-        if (!tag) others.push_back(states);
-        States merged;
-        for (auto& dic : others)
-          for (auto& kv : dic) {
-            auto& m = merged[kv.first];
-            m.insert(m.end(), kv.second.begin(), kv.second.end());
-          }
-        for (auto& kv : states) {
-          auto& m = merged[kv.first];
-          m.insert(m.end(), kv.second.begin(), kv.second.end());
-        }
-        for (auto& kv : merged) {
-          std::set<int> s(kv.second.begin(), kv.second.end());
-          kv.second.assign(s.begin(), s.end());
-        }
-        states.swap(merged);
+        others.push_back(std::move(current));
+        // DFG_c.py also folds the incoming states in, with or without an else
+        others.push_back(std::move(states));
+        states = dfg_union(std::move(others));
         sort_by_idx(dfg);
         return dfg;
       }

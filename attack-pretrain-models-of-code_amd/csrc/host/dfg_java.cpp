@@ -1263,9 +1263,9 @@ struct JWalker {
             others.push_back(std::move(ns));
           }
         }
-        others.push_back(current);
-        if (!tag) others.push_back(st);
-        st = dfg_union(others);
+        others.push_back(std::move(current));
+        if (!tag) others.push_back(std::move(st));
+        st = dfg_union(std::move(others));
         dfg_sort(dfg);
         return dfg;
       }

@@ -67,17 +67,30 @@ inline void dfg_merge_dup(std::vector<DfgEdge>& d) {
 }
 
 // if statements: the union of every branch's states (and the incoming states when there is no
-// else), each list deduplicated and sorted
-inline DfgStates dfg_union(const std::vector<DfgStates>& dicts) {
-  DfgStates merged;
-  for (auto& dic : dicts)
-    for (auto& kv : dic) {
-      auto& m = merged[kv.first];
-      m.insert(m.end(), kv.second.begin(), kv.second.end());
+// else), each list deduplicated and sorted.  The maps are key-ordered, so the union merges each
+// into the first in one linear pass; a key's lists are concatenated (a list equal to the one
+// already there adds nothing to the set) and sorted + deduplicated at the end (= sorted(set)).
+inline DfgStates dfg_union(std::vector<DfgStates>&& dicts) {
+  if (dicts.empty()) return {};
+  DfgStates merged = std::move(dicts[0]);
+  for (size_t d = 1; d < dicts.size(); ++d) {
+    auto bi = merged.begin();
+    for (auto& kv : dicts[d]) {
+      while (bi != merged.end() && bi->first < kv.first) ++bi;
+      if (bi != merged.end() && bi->first == kv.first) {
+        if (bi->second != kv.second)
+          bi->second.insert(bi->second.end(), kv.second.begin(), kv.second.end());
+      } else {
+        bi = merged.emplace_hint(bi, kv.first, std::move(kv.second));
+      }
     }
+  }
   for (auto& kv : merged) {
-    std::set<int> s(kv.second.begin(), kv.second.end());
-    kv.second.assign(s.begin(), s.end());
+    auto& v = kv.second;
+    if (std::adjacent_find(v.begin(), v.end(), [](int a, int b) { return a >= b; }) != v.end()) {
+      std::sort(v.begin(), v.end());
+      v.erase(std::unique(v.begin(), v.end()), v.end());
+    }
   }
   return merged;
 }
