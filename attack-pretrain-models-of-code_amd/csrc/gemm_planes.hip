@@ -430,7 +430,8 @@ __device__ __forceinline__ void pp_wait_vm() {
 // DIAG (timing experiments only, through ae_bench_gemm_packed; results WRONG): 1 = no DMA after
 // the prologue, 2 = no MFMAs, 3 = no fragment reads after K-tile 0, 4 = no epilogue, 5 = no
 // vmcnt waits in the loop, 6 = MFMAs + barriers only (no DMA / reads / waits after K-tile 0),
-// 7 = MFMAs only (6 without barriers).  Production instantiations have DIAG = 0.
+// 7 = MFMAs only (6 without barriers); 8 = plain (not non-temporal) epilogue stores, results
+// exact.  Production instantiations have DIAG = 0.
 template <int NP, int EPI, int DIAG>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
     const __bf16* __restrict__ A, const __bf16* __restrict__ W, const float* __restrict__ bias,
@@ -504,7 +505,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
   bf16x8 fw[2][NS][NP];   // W fragments: [n-half][step][plane]
 
   auto read_a = [&](const unsigned char* st, int mh, int kt) {
-    if ((DIAG == 3 || DIAG >= 6) && kt > 0) return;
+    if ((DIAG == 3 || DIAG == 6 || DIAG == 7) && kt > 0) return;
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
@@ -515,7 +516,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
               st + a_row + (2 * mh + tt) * 32 * ROWB + 16 * ((4 * p + 2 * s + lh) ^ sw));
   };
   auto read_w = [&](const unsigned char* st, int nh, int kt) {
-    if ((DIAG == 3 || DIAG >= 6) && kt > 0) return;
+    if ((DIAG == 3 || DIAG == 6 || DIAG == 7) && kt > 0) return;
 #pragma unroll
     for (int s = 0; s < NS; ++s)
 #pragma unroll
@@ -549,7 +550,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
       const bf16x8& x = (T == 3 && term == 1) ? fw[nh][s][NP - 1] : fw[nh][s][0];
       const bf16x8& y = (T == 3 && term == 0) ? fa[tt][s][NP - 1] : fa[tt][s][0];
       c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, c, 0, 0, 0);
-      if (DIAG != 1 && DIAG < 6 && dma && (i == NM / 3 - 1 || i == 2 * NM / 3 - 1)) {
+      if (DIAG != 1 && DIAG != 6 && DIAG != 7 && dma && (i == NM / 3 - 1 || i == 2 * NM / 3 - 1)) {
         const int j = 2 * q + (i == NM / 3 - 1 ? 0 : 1);
         __builtin_amdgcn_sched_barrier(0);
         dma16(src[j] + (size_t)kd * ROWB, lds0 + (kd & 1) * STAGE + dst[j]);
@@ -583,12 +584,12 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
   } else {
     pp_wait_vm<0>();
   }
-  if (DIAG == 1 || DIAG >= 6) pp_wait_vm<0>();
+  if (DIAG == 1 || DIAG == 6 || DIAG == 7) pp_wait_vm<0>();
   __builtin_amdgcn_s_barrier();
   if (wm == 1) sync_load();  // group 1 runs one phase behind
 
   auto wait6 = [&](bool full) {
-    if (DIAG == 5 || DIAG == 1 || DIAG >= 6) return;
+    if (DIAG == 5 || DIAG == 1 || DIAG == 6 || DIAG == 7) return;
     if (full) pp_wait_vm<6>();
     else pp_wait_vm<0>();
   };
@@ -619,7 +620,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
     mfma_quad(1, 0, std::integral_constant<int, 1>(), next2, kt + 2);
     sync_load();
   }
-  if (DIAG != 0) pp_wait_vm<0>();
+  if (DIAG != 0 && DIAG != 8) pp_wait_vm<0>();
   if (wm == 0) sync_load();
   if (DIAG == 7) __builtin_amdgcn_s_barrier();  // same barrier count in both groups; every LDS read and DMA done
   if (DIAG == 4) {
@@ -698,7 +699,10 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
         const int col = cb0 + (c * 16) / (2 * NP);  // first column this chunk belongs to (>= block start)
         if (ok && col < N) {
           __bf16* dstp = Cp + (size_t)row * NP * N + (size_t)(cb0 >> 5) * 32 * NP + c * 8;
-          *reinterpret_cast<uint4*>(dstp) = v;
+          if (DIAG != 8)
+            __builtin_nontemporal_store(__builtin_bit_cast(floatx4, v), reinterpret_cast<floatx4*>(dstp));
+          else
+            *reinterpret_cast<uint4*>(dstp) = v;
         }
       } else {
         const int col = cb0 + 4 * c;
@@ -710,7 +714,10 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
 #pragma unroll
             for (int i = 0; i < 4; ++i) f[i] = tanhf(f[i]);
           if (EPI == PK_EPI_RES) f += *reinterpret_cast<const floatx4*>(R + o);
-          *reinterpret_cast<floatx4*>(C + o) = f;
+          if (DIAG != 8)
+            __builtin_nontemporal_store(f, reinterpret_cast<floatx4*>(C + o));
+          else
+            *reinterpret_cast<floatx4*>(C + o) = f;
         }
       }
     }
@@ -729,7 +736,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
 // of kt (>= 2 phases after their last read); each waited one phase before it is read.  f32
 // epilogues only (bias / +residual / tanh), staged through LDS in 32-row passes with 400-B
 // padded rows (conflict-free), stored as whole 384-B row segments.
-template <int NP, int EPI>
+template <int NP, int EPI, bool NT = false>
 __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
     const __bf16* __restrict__ A, const __bf16* __restrict__ W, const float* __restrict__ bias,
     const float* __restrict__ R, float* __restrict__ C, int M, int N, int K, int group_m) {
@@ -920,7 +927,10 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
 #pragma unroll
           for (int i = 0; i < 4; ++i) f[i] = tanhf(f[i]);
         if (EPI == PK_EPI_RES) f += *reinterpret_cast<const floatx4*>(R + o);
-        *reinterpret_cast<floatx4*>(C + o) = f;
+        if (NT)
+          __builtin_nontemporal_store(f, reinterpret_cast<floatx4*>(C + o));
+        else
+          *reinterpret_cast<floatx4*>(C + o) = f;
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -967,19 +977,19 @@ hipError_t pp_epi(int epi, const __bf16* A, const __bf16* W, const float* bias, 
   }
 }
 
-template <int NP, int EPI>
+template <int NP, int EPI, bool NT = false>
 hipError_t pp192_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R,
                         float* C, int M, int N, int K, int group_m, hipStream_t st) {
   constexpr int lds = 2 * (256 + 192) * PK_ROWB;  // 112 KiB
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_pp192_kernel<NP, EPI>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_pp192_kernel<NP, EPI, NT>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
   const int tiles = ((M + 255) / 256) * ((N + 191) / 192);
-  hipLaunchKernelGGL((gemm_pp192_kernel<NP, EPI>), dim3(tiles), dim3(512), lds, st, A, W, bias, R,
+  hipLaunchKernelGGL((gemm_pp192_kernel<NP, EPI, NT>), dim3(tiles), dim3(512), lds, st, A, W, bias, R,
                      C, M, N, K, group_m);
   return hipGetLastError();
 }
@@ -987,10 +997,15 @@ hipError_t pp192_launch(const __bf16* A, const __bf16* W, const float* bias, con
 // f32 epilogues only (bias, +residual, tanh); N % 32 == 0
 hipError_t pp192_dispatch(const unsigned short* A, const unsigned short* W, const float* bias,
                           const float* R, float* C, int M, int N, int K, int epi, int np,
-                          int group_m, hipStream_t st) {
+                          int group_m, hipStream_t st, bool nt = false) {
   auto a = reinterpret_cast<const __bf16*>(A);
   auto w = reinterpret_cast<const __bf16*>(W);
   if (epi == PK_EPI_GELU_PACKED || epi == PK_EPI_BIAS_PACKED) return hipErrorInvalidValue;
+  if (nt) {  // timing variant (ae_bench_gemm_packed diag 8): non-temporal stores
+    if (np != 2 || (epi != PK_EPI_RES && epi != PK_EPI_BIAS)) return hipErrorInvalidValue;
+    if (epi == PK_EPI_BIAS) return pp192_launch<2, PK_EPI_BIAS, true>(a, w, bias, R, C, M, N, K, group_m, st);
+    return pp192_launch<2, PK_EPI_RES, true>(a, w, bias, R, C, M, N, K, group_m, st);
+  }
   if (np == 2) {
     if (epi == PK_EPI_BIAS) return pp192_launch<2, PK_EPI_BIAS>(a, w, bias, R, C, M, N, K, group_m, st);
     if (epi == PK_EPI_RES) return pp192_launch<2, PK_EPI_RES>(a, w, bias, R, C, M, N, K, group_m, st);
@@ -1121,8 +1136,11 @@ extern "C" hipError_t ae_launch_gemm_packed(const unsigned short* A, const unsig
 
 
 // Kernel experiments (tools/gemm_bench.py, tests): explicit tile width (0 = the production choice)
-// and a diagnostic variant (0 = the production kernel; see DIAG above — other values give WRONG
-// results and exist only to time parts of the pipeline).  Not part of include/alert_engine.h.
+// and a diagnostic variant (0 = the production kernel; see DIAG above — values 1-7 give WRONG
+// results and exist only to time parts of the pipeline).  Variant 8 is exact and flips the store
+// flavour of the epilogue: plain stores for the 256 x 256 kernel (production: non-temporal, about
+// 2 % faster on FFN1 / QKV), non-temporal for the 256 x 192 kernel (production: plain; mixed
+// +-3 % on O-proj / FFN2).  Not part of include/alert_engine.h.
 extern "C" hipError_t ae_bench_gemm_packed(const unsigned short* A, const unsigned short* W,
                                            const float* bias, const float* R, float* C,
                                            unsigned short* Cp, int M, int N, int K, int epi,
@@ -1131,7 +1149,7 @@ extern "C" hipError_t ae_bench_gemm_packed(const unsigned short* A, const unsign
   if (!pk_shape_ok(M, N, K, np) ||
       (bn != 0 && bn != 128 && bn != 192 && bn != 256 && bn != 512))
     return hipErrorInvalidValue;
-  if (bn == 192) return pp192_dispatch(A, W, bias, R, C, M, N, K, epi, np, PK_GROUP_M, st);
+  if (bn == 192) return pp192_dispatch(A, W, bias, R, C, M, N, K, epi, np, PK_GROUP_M, st, diag == 8);
   if (bn == 512) {  // the ping-pong 256 x 256 kernel
     switch (diag) {
       case 0: return pp_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
@@ -1142,6 +1160,7 @@ extern "C" hipError_t ae_bench_gemm_packed(const unsigned short* A, const unsign
       case 5: return pp_dispatch<5>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
       case 6: return pp_dispatch<6>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
       case 7: return pp_dispatch<7>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
+      case 8: return pp_dispatch<8>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
       default: return hipErrorInvalidValue;
     }
   }
