@@ -21,7 +21,7 @@ from .attack_ref import _positions, _words_of
 
 
 def _replace_uid(victim, is_uid, tokens, label, uid, substitute_dict, n_candi, prob_threshold,
-                 idx2token=None):
+                 idx2token=None, lang="c", skip_known=True):
     selected_uid = random.sample(list(substitute_dict.keys()), 1)[0]
     candi_token = [selected_uid]
     candi_tokens = [copy.deepcopy(tokens)]
@@ -29,11 +29,12 @@ def _replace_uid(victim, is_uid, tokens, label, uid, substitute_dict, n_candi, p
     pool = random.sample(idx2token, n_candi) if idx2token is not None else \
         random.sample(substitute_dict[selected_uid], min(n_candi, len(substitute_dict[selected_uid])))
     for c in pool:
-        if c in uid.keys():
+        # the Authorship-Attribution __replaceUID_random has no known-name skip (its :649-655)
+        if (idx2token is None or skip_known) and c in uid.keys():
             continue
         if is_uid(c):
             candi_token.append(c)
-            candi_tokens.append(fr.get_example(copy.deepcopy(tokens), selected_uid, c, "c"))
+            candi_tokens.append(fr.get_example(copy.deepcopy(tokens), selected_uid, c, lang))
     prob, pred = victim.texts(candi_tokens)
     for i in range(len(candi_token)):
         if pred[i] != label:
@@ -58,9 +59,12 @@ def _replace_uid(victim, is_uid, tokens, label, uid, substitute_dict, n_candi, p
 
 
 def mcmc(victim, is_uid, substituions, code, label, n_candi=30, max_iter=100, prob_threshold=0.95,
-         idx2token=None):
-    """mcmc (:466-537); with idx2token, mcmc_random (:539-608)."""
-    prog_length, words = _words_of(code)
+         idx2token=None, lang="c", skip_known=True):
+    """mcmc (:466-537); with idx2token, mcmc_random (:539-608).  lang="python", skip_known=False
+    with a Victim(task="authorship") is the Authorship-Attribution copy
+    (CodeXGLUE/Authorship-Attribution/code/attacker.py:440-666: Python leaves and get_example,
+    raw-text features, argmax predictions)."""
+    prog_length, words = _words_of(code, lang)
     raw_tokens = copy.deepcopy(words)
     uid = _positions(words, list(substituions.keys()))
     if len(uid) <= 0:
@@ -73,7 +77,7 @@ def mcmc(victim, is_uid, substituions, code, label, n_candi=30, max_iter=100, pr
     res = None
     for iteration in range(1, 1 + max_iter):
         res = _replace_uid(victim, is_uid, code, label, uid, variable_substitue_dict, n_candi,
-                           prob_threshold, idx2token)
+                           prob_threshold, idx2token, lang, skip_known)
         if res["status"].lower() in ["s", "a"]:
             if iteration == 1:
                 old_uids[res["old_uid"]] = [res["new_uid"]]

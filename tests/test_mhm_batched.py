@@ -148,3 +148,57 @@ def test_authorship_driver_batched_equals_sequential():
         assert out["queries"] == v_seq.query - q0
     assert [dict(r) for r in bat["records"]] == seq
     assert {r["is_success"] for r in seq} & {1, -1}
+
+
+@pytest.mark.parametrize("kind", ["mcmc", "mcmc_random"])
+def test_authorship_mhm_matches_text_oracle_cpu(kind):
+    """AuthorshipMHM_Attacker (CodeXGLUE/Authorship-Attribution/code/attacker.py:440-666, driven as
+    mhm.py:198-206: n_candi 30, threshold 1) against oracle/mhm_ref.py over text (Python leaves,
+    raw-text features, 66-way argmax), same Python `random` seed, on a numpy stand-in victim: same
+    outcome, adversarial code, replacement chain and query count."""
+    import _apmc  # noqa: F401
+    from apmc_amd.attacker import AuthorshipMHM_Attacker
+    from apmc_amd.drivers import AttackArgs, _example, load_fixture
+    from apmc_amd.host import Tokenizer
+    from apmc_amd.model import HostIdsVictim
+    from apmc_amd.utils import isUID
+    from oracle import attack_ref, mhm_ref
+
+    codes, subs, _ = load_fixture(ROOT / "data" / "authorship" / "valid_subs.jsonl", 0, 6,
+                                  labels_path=ROOT / "data" / "authorship" / "valid.txt")
+    w = np.random.default_rng(5).standard_normal((50265, 66))
+    bias = np.random.default_rng(3).standard_normal(66) * 2.0
+
+    def score(ids):  # sharpness chosen so the sample has successes and failures
+        z = (w[ids] * (ids != 1)[..., None]).sum(1) / 20.0 + bias
+        z = np.exp(z - z.max(1, keepdims=True))
+        return (z / z.sum(1, keepdims=True)).astype(np.float32)
+
+    tok = Tokenizer()
+    victim = HostIdsVictim(score, task="authorship", block_size=BLOCK)
+    labels = [int(victim.get_results([_example(tok, c, 0, BLOCK, "authorship")])[1][0])
+              for c in codes]
+    args = AttackArgs(block_size=BLOCK, eval_batch_size=64, task="authorship", lang="python")
+    vocab = sorted({w_ for s in subs for v in s.values() for w_ in v})
+    att = AuthorshipMHM_Attacker(args, victim, None, tok, {t: i for i, t in enumerate(vocab)},
+                                 vocab)
+    seen = []
+    for i in range(len(codes)):
+        random.seed(3100 + i)
+        q0 = victim.query
+        res = getattr(att, kind)(tok, codes[i], labels[i], _n_candi=30, _max_iter=20,
+                                 _prob_threshold=1, subs=subs[i])
+        q_prod = victim.query - q0
+        random.seed(3100 + i)
+        v = attack_ref.Victim(score, BLOCK, task="authorship")
+        ref = mhm_ref.mcmc(v, isUID, subs[i], codes[i], labels[i], n_candi=30, max_iter=20,
+                           prob_threshold=1, idx2token=vocab if kind == "mcmc_random" else None,
+                           lang="python", skip_known=False)
+        assert res["succ"] == ref["succ"], i
+        assert q_prod == v.query, (i, q_prod, v.query)
+        if res["succ"] is not None:
+            for k in ("tokens", "replace_info", "nb_changed_var", "nb_changed_pos",
+                      "prog_length", "new_pred"):
+                assert res[k] == ref[k], (i, k)
+        seen.append(res["succ"])
+    assert True in seen and False in seen, seen
