@@ -638,61 +638,24 @@ class MHM_Attacker:
         ≤31.  The victim's query counter advances by the same total as the sequential runs.
         Returns `[(result_dict, queries)]` in job order; `on_done(j, result, queries)` is called as
         each chain finishes."""
+        from .batching import list_source, run_requests
+
         replace = self._replace_uid_random if original else self._replace_uid
         kind = "MHM-Origin" if original else "MHM"
         out = [None] * len(jobs)
-        nxt = 0
 
-        def finish(j, value, q):
+        def start(j):
+            subs, code, label, seed = jobs[j]
+            return self._run_gen(tokenizer, subs, code, label, _n_candi, _max_iter,
+                                 _prob_threshold, replace, kind, random.Random(seed))
+
+        def finish(j, value, q, _t0):
             out[j] = (value, q)
             if on_done is not None:
                 on_done(j, value, q)
 
-        def refill(group, cap):
-            nonlocal nxt
-            while nxt < len(jobs) and len(group) < cap:
-                subs, code, label, seed = jobs[nxt]
-                gen = self._run_gen(tokenizer, subs, code, label, _n_candi, _max_iter,
-                                    _prob_threshold, replace, kind, random.Random(seed))
-                try:
-                    group.append([nxt, gen, next(gen), 0])
-                except StopIteration as stop:
-                    finish(nxt, stop.value, 0)
-                nxt += 1
-
-        def advance(group, answers):
-            still = []
-            for c, ans in zip(group, answers):
-                c[3] += c[2].n
-                try:
-                    c[2] = c[1].send(ans)
-                    still.append(c)
-                except StopIteration as stop:
-                    finish(c[0], stop.value, c[3])
-            return still
-
-        # live entries: [job index, generator, pending payload, queries so far].  With a victim
-        # that can submit asynchronously the chains run as two groups: one group's device batch
-        # runs while the host advances the other group's chains (as run_gi_attack_batched).
-        clf = self.classifier
-        groups = 2 if hasattr(clf, "submit") else 1
-        cap = max(1, max_inflight // groups)
-        live = [[] for _ in range(groups)]
-        pend = [None] * groups
-        while True:
-            for g in range(groups):
-                if pend[g] is not None:
-                    live[g] = advance(live[g], pend[g].result())
-                    pend[g] = None
-                refill(live[g], cap)
-                if live[g]:
-                    payloads = [c[2] for c in live[g]]
-                    if groups == 1:
-                        live[g] = advance(live[g], clf.score_prepared(payloads))
-                    else:
-                        pend[g] = clf.submit(payloads)
-            if nxt >= len(jobs) and not any(live) and all(x is None for x in pend):
-                break
+        run_requests(self.classifier, list_source(range(len(jobs))), start, finish,
+                     max_inflight=max_inflight)
         return out
 
     def _candidates_result(self, rng, _tokens, _label, selected_uid, candi_token, candi_pairs,

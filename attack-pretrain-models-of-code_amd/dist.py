@@ -132,6 +132,75 @@ def run_sharded_gi_attack(model, codes, subs, labels, args, device=None, tok=Non
     return recs, tot
 
 
+def _rank_world():
+    import torch.distributed as dist
+
+    on = dist.is_available() and dist.is_initialized()
+    return (dist, dist.get_rank(), dist.get_world_size()) if on else (None, 0, 1)
+
+
+def _job_totals(st, names, nsum):
+    """Sum the first `nsum` gathered columns over ranks, max the rest (wall clocks); keep every
+    rank's row so the tail of a skewed queue stays visible."""
+    tot = {n: (float(st[:, i].sum()) if i < nsum else float(st[:, i].max()))
+           for i, n in enumerate(names)}
+    for n in names[:nsum]:
+        tot[n] = int(round(tot[n]))
+    tot["per_rank"] = [{n: (int(round(v)) if i < nsum else round(float(v), 3))
+                        for i, (n, v) in enumerate(zip(names, row))} for row in st]
+    return tot
+
+
+GI_STATS = ["examples", "total_cnt", "success", "queries", "ga_runs", "ga_successes", "wall_s"]
+MHM_STATS = ["examples", "total_cnt", "success", "queries", "wall_s"]
+
+
+def run_sharded_gi_batched(model, codes, subs, labels, args, max_inflight=64, device=None,
+                           deadline: float | None = None, key: str = "apmc_gi_batched_queue"):
+    """run_gi_attack_batched (cross-example batched greedy -> GA) over all ranks: one dynamic
+    example queue, each rank batching the examples it pulled; statistics all-gathered, records
+    merged by index.  Per-example RNG (random.Random(seed + index)) makes every record equal the
+    1-GPU run whichever rank took the example.  Returns (merged records, job totals)."""
+    from .drivers import run_gi_attack_batched
+
+    dist, _, world = _rank_world()
+    q = DynamicQueue(len(codes), key=call_key(key), deadline=deadline)
+    if dist is not None:
+        dist.barrier()
+    out = run_gi_attack_batched(model, codes, subs, labels, args, queue=q,
+                                max_inflight=max_inflight)
+    recs = out["records"]
+    ga = [r for r in recs if r["attack_type"] == "GA"]
+    st = gather_stats([out["examples"], out["total_cnt"], out["success"], out["queries"],
+                       len(ga), sum(r["is_success"] == 1 for r in ga), out["wall_s"]],
+                      device=device)
+    tot = _job_totals(st, GI_STATS, 6)
+    tot["success_rate"] = tot["success"] / tot["total_cnt"] if tot["total_cnt"] else 0.0
+    return merge_records(recs), tot
+
+
+def run_sharded_mhm(model, codes, subs, labels, args, n_candi=30, max_iter=100, prob_threshold=1,
+                    original=False, max_inflight=64, device=None, n: int | None = None,
+                    key: str = "apmc_mhm_queue"):
+    """run_mhm_attack (cross-example batched MHM-NS chains) over all ranks with one dynamic
+    queue over examples [0, n) — per-example MCMC cost is as skewed as GA's (a success after one
+    round vs 100 rounds of 31 candidates).  Returns (merged records, job totals)."""
+    from .drivers import run_mhm_attack
+
+    dist, _, world = _rank_world()
+    q = DynamicQueue(len(codes) if n is None else n, key=call_key(key))
+    if dist is not None:
+        dist.barrier()
+    out = run_mhm_attack(model, codes, subs, labels, args, n_candi=n_candi, max_iter=max_iter,
+                         prob_threshold=prob_threshold, original=original,
+                         max_inflight=max_inflight, queue=q)
+    st = gather_stats([out["examples"], out["total_cnt"], out["success"], out["queries"],
+                       out["wall_s"]], device=device)
+    tot = _job_totals(st, MHM_STATS, 4)
+    tot["success_rate"] = tot["success"] / tot["total_cnt"] if tot["total_cnt"] else 0.0
+    return merge_records(out["records"]), tot
+
+
 def run_sharded_substitutes(gen, in_path, out_path, start=0, end=None, device=None,
                             deadline: float | None = None):
     """get_substitutes.py over all ranks (examples across ranks, jsonl merged by

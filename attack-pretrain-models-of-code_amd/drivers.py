@@ -173,82 +173,74 @@ def _totals(records, wall):
                 queries=sum(r["queries"] for r in records), wall_s=wall)
 
 
-def run_gi_attack_batched(model, codes, subs, labels, args: AttackArgs, indices=None, tok=None,
-                          queue=None, log=None, max_inflight=64, pipeline=True):
-    """greedy (+GA) over many examples at once (SURVEY §7 item 6): up to `max_inflight`
-    examples' attacks are in flight, and every round answers all their pending victim requests
-    with ONE device batch (Model.score_prepared), so the GPU sees thousands of rows instead of
-    one GA population of <= 64.  Example `index` draws from random.Random(args.seed + index),
-    so each record is exactly the sequential run with rng="per_example" (same outcome, mutants,
-    adversarial code and query count); records come back in example order."""
-    tok = tok or Tokenizer()
-    attacker = make_attacker(args, model, tok)
-    recorder = Recorder(args.csv_store_path) if args.csv_store_path else None
-    order = list(range(len(codes))) if indices is None else list(indices)
+class _InOrderWriter:
+    """Recorder rows as examples finish, in the order they were taken (example order for a list
+    or a rank's queue), so a crash or deadline mid-run keeps every finished row."""
+
+    def __init__(self, recorder):
+        self.recorder, self.taken, self.done, self.rows, self.pos = recorder, [], {}, {}, 0
+
+    def take(self, index):
+        self.taken.append(index)
+
+    def finish(self, index, make_row):
+        self.done[index] = make_row
+        while self.pos < len(self.taken) and self.taken[self.pos] in self.done:
+            i = self.taken[self.pos]
+            self.rows[i] = self.done.pop(i)(self.recorder)
+            self.pos += 1
+
+    def records(self):
+        return [self.rows[i] for i in sorted(self.rows)]
+
+
+def _source(order, queue, writer):
     pos = 0
 
     def next_index():
         nonlocal pos
         if queue is not None:
-            return queue()
-        if pos >= len(order):
-            return None
-        pos += 1
-        return order[pos - 1]
+            index = queue()
+        elif pos < len(order):
+            index, pos = order[pos], pos + 1
+        else:
+            index = None
+        if index is not None:
+            writer.take(index)
+        return index
+    return next_index
 
-    done = {}
+
+def run_gi_attack_batched(model, codes, subs, labels, args: AttackArgs, indices=None, tok=None,
+                          queue=None, log=None, max_inflight=64, pipeline=True):
+    """greedy (+GA) over many examples at once (SURVEY §7 item 6): up to `max_inflight`
+    examples' attacks are in flight, and every round answers all their pending victim requests
+    with ONE device batch (batching.run_requests), so the GPU sees thousands of rows instead of
+    one GA population of <= 64.  Example `index` draws from random.Random(args.seed + index),
+    so each record is exactly the sequential run with rng="per_example" (same outcome, mutants,
+    adversarial code and query count); records come back in example order, and the CSV rows are
+    written as the examples finish (in the order they were taken)."""
+    from .batching import run_requests
+
+    tok = tok or Tokenizer()
+    attacker = make_attacker(args, model, tok)
+    writer = _InOrderWriter(Recorder(args.csv_store_path) if args.csv_store_path else None)
+    order = list(range(len(codes))) if indices is None else list(indices)
     t0 = time.time()
-    drained = False
 
-    def refill(group, cap):
-        nonlocal drained
-        while not drained and len(group) < cap:
-            index = next_index()
-            if index is None:
-                drained = True
-                break
-            gen = attack_one_gen(attacker, tok, codes[index], subs[index], labels[index], args,
-                                 random.Random(args.seed + index))
-            group.append([index, gen, next(gen), 0, time.time()])
+    def start(index):
+        return attack_one_gen(attacker, tok, codes[index], subs[index], labels[index], args,
+                              random.Random(args.seed + index))
 
-    def advance(group, answers):
-        still = []
-        for c, ans in zip(group, answers):
-            c[3] += c[2].n
-            try:
-                c[2] = c[1].send(ans)
-                still.append(c)
-            except StopIteration as stop:
-                res, attack_type = stop.value
-                done[c[0]] = (res, attack_type, c[3], (time.time() - c[4]) / 60)
-                if log:
-                    log(_record(c[0], *done[c[0]], None))
-        return still
+    def on_done(index, value, queries, ts):
+        res, attack_type = value
+        dt = (time.time() - ts) / 60
+        if log:
+            log(_record(index, res, attack_type, queries, dt, None))
+        writer.finish(index, lambda rec: _record(index, res, attack_type, queries, dt, rec))
 
-    # live entries: [index, generator, pending payload, queries, t_start].  With a model that can
-    # submit asynchronously the examples run as two groups: while one group's device batch runs,
-    # the host advances the other group's attacks (mutation, featurisation) on its answers.
-    groups = 2 if (pipeline and hasattr(model, "submit")) else 1
-    cap = max(1, max_inflight // groups)
-    live = [[] for _ in range(groups)]
-    pend = [None] * groups
-    while True:
-        for g in range(groups):
-            if pend[g] is not None:
-                live[g] = advance(live[g], pend[g].result())
-                pend[g] = None
-            refill(live[g], cap)
-            if live[g]:
-                payloads = [c[2] for c in live[g]]
-                if groups == 1:
-                    live[g] = advance(live[g], model.score_prepared(payloads))
-                else:
-                    pend[g] = model.submit(payloads)
-        if drained and not any(live) and all(x is None for x in pend):
-            break
-    # CSV rows in example order, as the reference's loop writes them
-    records = [_record(i, *done[i], recorder) for i in sorted(done)]
-    return _totals(records, time.time() - t0)
+    run_requests(model, _source(order, queue, writer), start, on_done, max_inflight, pipeline)
+    return _totals(writer.records(), time.time() - t0)
 
 
 def run_gi_attack(model, codes, subs, labels, args: AttackArgs, indices=None, tok=None,
@@ -286,16 +278,34 @@ def run_gi_attack(model, codes, subs, labels, args: AttackArgs, indices=None, to
     return _totals(records, time.time() - t0)
 
 
+def mhm_one_gen(attacker, tok, code, subs, label, args, n_candi, max_iter, prob_threshold,
+                original, rng):
+    """One example of mhm_attack.py:195-236 (Authorship mhm.py:192-233) as a request generator:
+    the original-prediction query, then (if correctly classified) the MCMC chain.  Returns
+    (is_success, result dict or None)."""
+    task = getattr(args, "task", "devign")
+    example = _example(tok, code, label, args.block_size, task, args)
+    _, preds = yield attacker.classifier.prepare([example])
+    if preds[0] != label:
+        return -4, None
+    replace = attacker._replace_uid_random if original else attacker._replace_uid
+    kind = "MHM-Origin" if original else "MHM"
+    res = yield from attacker._run_gen(tok, subs, code, label, n_candi, max_iter, prob_threshold,
+                                       replace, kind, rng)
+    return (1 if res["succ"] else (-1 if res["succ"] is not None else -3)), res
+
+
 def run_mhm_attack(model, codes, subs, labels, args: AttackArgs, indices=None, tok=None,
-                   n_candi=30, max_iter=100, prob_threshold=1, original=False, max_inflight=1):
+                   n_candi=30, max_iter=100, prob_threshold=1, original=False, max_inflight=1,
+                   queue=None):
     """mhm_attack.py:160-236 (MHM-NS; `original` = MHM with the random-token candidates).
 
     max_inflight = 1 is the reference loop (one global `random` stream seeded once).  With
-    max_inflight > 1 the examples' chains run interleaved through `MHM_Attacker.mcmc_batched`:
-    the original-prediction queries of all examples go out as one batch, then up to
-    `max_inflight` chains share every device batch; example `index` then draws from
+    max_inflight > 1 the examples run interleaved (batching.run_requests over mhm_one_gen): up
+    to `max_inflight` chains share every device batch; example `index` then draws from
     `random.Random(args.seed + index)` — the same per-example seeding `rng="per_example"` gives
-    the GA driver — and records stay in index order."""
+    the GA driver — and records stay in index order.  `queue` (batched form only) pulls the
+    examples from a dist.DynamicQueue shared by all ranks instead of `indices`."""
     tok = tok or Tokenizer()
     task = getattr(args, "task", "devign")
     set_seed(args.seed)
@@ -306,23 +316,22 @@ def run_mhm_attack(model, codes, subs, labels, args: AttackArgs, indices=None, t
     attacker = cls(args, model, None, tok, token2id, id2token)
     order = list(range(len(codes))) if indices is None else list(indices)
     records, t0 = [], time.time()
-    if max_inflight > 1:
-        exs = [_example(tok, codes[i], labels[i], args.block_size, task, args) for i in order]
-        _, preds = model.get_results(exs, args.eval_batch_size) if exs else ([], [])
-        by_index, jobs, job_index = {}, [], []
-        for index, p in zip(order, preds):
-            if p != labels[index]:
-                by_index[index] = dict(index=index, is_success=-4, queries=1)
-            else:
-                jobs.append((subs[index], codes[index], labels[index], args.seed + index))
-                job_index.append(index)
-        done = attacker.mcmc_batched(tok, jobs, _n_candi=n_candi, _max_iter=max_iter,
-                                     _prob_threshold=prob_threshold, original=original,
-                                     max_inflight=max_inflight)
-        for index, (res, q) in zip(job_index, done):
-            ok = 1 if res["succ"] else (-1 if res["succ"] is not None else -3)
-            by_index[index] = dict(index=index, is_success=ok, queries=1 + q)
-        records = [by_index[i] for i in order]
+    if max_inflight > 1 or queue is not None:
+        from .batching import run_requests
+
+        by_index = {}
+
+        def start(index):
+            return mhm_one_gen(attacker, tok, codes[index], subs[index], labels[index], args,
+                               n_candi, max_iter, prob_threshold, original,
+                               random.Random(args.seed + index))
+
+        def on_done(index, value, queries, _ts):
+            by_index[index] = dict(index=index, is_success=value[0], queries=queries)
+
+        run_requests(model, _source(order, queue, _InOrderWriter(None)), start, on_done,
+                     max(2, max_inflight))
+        records = [by_index[i] for i in sorted(by_index)]
         order = []
     for index in order:
         example = _example(tok, codes[index], labels[index], args.block_size, task, args)

@@ -55,8 +55,9 @@ def parse_args():
     ap.add_argument("--precision", default="f32x3", choices=["fp32", "f32x3", "bf16"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="CPU scoring microbenchmark budget (cpu_baseline)")
-    ap.add_argument("--cpu-e2e-seconds", type=float, default=20.0,
-                    help="CPU config-1 greedy attack budget (config1.cpu)")
+    ap.add_argument("--cpu-e2e-seconds", type=float, default=360.0,
+                    help="cap (s) of the CPU config-1 greedy attack (config1.cpu); the run "
+                         "normally completes all 16 functions well inside it")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--attack-examples", type=int, default=400,
                     help="examples of test_subs_0_400 in the config-2 GA attack leg (0 disables)")
@@ -129,23 +130,27 @@ def pmc_traffic_per_launch(precision):
 
 
 def host_cores():
-    """(threads this job may use, physical cores of the host)."""
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    phys = set()
-    try:
-        cur = {}
-        for line in open("/proc/cpuinfo"):
-            if ":" in line:
-                k, v = [x.strip() for x in line.split(":", 1)]
-                cur[k] = v
-            elif cur:
-                phys.add((cur.get("physical id"), cur.get("core id")))
-                cur = {}
-        if cur:
-            phys.add((cur.get("physical id"), cur.get("core id")))
-    except OSError:
-        pass
-    return threads, (len(phys) or None)
+    """CPU threads for the CPU reference path: one per PHYSICAL core this process may run on
+    (its sched affinity mapped through sysfs topology, so SMT siblings count once).  Returns
+    (threads, facts) — facts states the affinity, the physical cores behind it and the host's
+    physical cores, so the line says exactly what was used."""
+    aff = sorted(os.sched_getaffinity(0))
+
+    def core_of(c):
+        base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+        try:
+            return (open(base + "physical_package_id").read().strip(),
+                    open(base + "core_id").read().strip())
+        except OSError:
+            return ("?", str(c))
+    mine = {core_of(c) for c in aff}
+    host = set()
+    for d in glob.glob("/sys/devices/system/cpu/cpu[0-9]*"):
+        host.add(core_of(int(d.rsplit("cpu", 1)[1])))
+    threads = max(1, len(mine))
+    return threads, {"affinity_cpus": len(aff), "physical_cores_in_affinity": len(mine),
+                     "host_physical_cores": len(host) or None,
+                     "job_share_threads": int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None}
 
 
 # ------------------------------------------------------------------------------------------ legs
@@ -177,6 +182,9 @@ def time_steps(eng, ids_dev, lens, out, steps, warmup, dev, dist, profile):
 
 
 def cpu_baseline(L, seconds, threads):
+    """The reference's CPU path on the scoring step: oracle/roberta_cpu.py (PyTorch-CPU fp32 eager
+    restatement of Model.get_results' forward) over [64, L] batches — the DataLoader batch of
+    model.py:40 — on `threads` torch threads; whole batches until `seconds` have passed."""
     import numpy as np
     import torch
 
@@ -186,18 +194,19 @@ def cpu_baseline(L, seconds, threads):
     torch.set_num_threads(threads)
     sd = synthetic_state_dict(seed=0, head="sigmoid1")
     rng = np.random.default_rng(0)
-    B = 8
+    B = 64
     ids = rng.integers(4, 50264, size=(B, L)).astype(np.int64)
     ids[:, 0], ids[:, -1] = 0, 2
-    ora.score(sd, ids[:1, :64], "sigmoid1")  # warm up allocator / threads
+    ora.score(sd, ids[:2, :64], "sigmoid1")  # warm up allocator / threads
     done, t0 = 0, time.perf_counter()
     while True:
         ora.score(sd, ids, "sigmoid1")
         done += B
         el = time.perf_counter() - t0
+        log(f"CPU baseline: {done} queries in {el:.1f} s ({threads} threads)")
         if el >= seconds:
             break
-    return done / el, f"{done} queries of L={L} (batches of {B}) in {el:.1f} s"
+    return done / el, f"{done} queries of L={L} (batches of {B}, model.py:40) in {el:.1f} s"
 
 
 def cpu_victim(threads):
@@ -213,7 +222,7 @@ def cpu_victim(threads):
     torch.set_num_threads(threads)
     sd = synthetic_state_dict(seed=VICTIM_SEED, head="sigmoid1", out_std=VICTIM_OUT_STD)
 
-    state = {"deadline": None, "scored": 0}
+    state = {"deadline": None, "scored": 0, "t0": time.time()}
 
     def score(ids):
         out = []
@@ -222,6 +231,9 @@ def cpu_victim(threads):
                 raise TimeoutError  # bounded sample: stop at the next batch past the budget
             out.append(ora.score(sd, ids[s:s + 64], "sigmoid1"))
             state["scored"] += out[-1].shape[0]
+            el = time.time() - state["t0"]
+            log(f"config-1 CPU: {state['scored']} queries in {el:.0f} s "
+                f"({state['scored'] / el:.2f} q/s, {threads} threads)")
         return np.concatenate(out)
 
     v = HostIdsVictim(score)
@@ -247,7 +259,7 @@ def greedy_run(model, codes, subs, labels, indices):
     wall = time.time() - t0
     st = getattr(model, "state", None)
     return dict(examples=len(done), queries=st["scored"] if st else model.query - q0, wall_s=wall,
-                successes=sum(r["is_success"] == 1 for r in done))
+                successes=sum(r["is_success"] == 1 for r in done), records=done)
 
 
 def config1_leg(dev, precision, threads, cpu_seconds):
@@ -271,14 +283,20 @@ def config1_leg(dev, precision, threads, cpu_seconds):
     if cpu_seconds > 0:
         cv = cpu_victim(threads)
         cv.state["deadline"] = time.time() + cpu_seconds
+        cv.state["t0"] = time.time()
         c = greedy_run(cv, codes, subs, labels, list(range(16)))
         res["cpu"] = {"kind": "port", "cores": threads, "examples_completed": c["examples"],
+                      "complete": c["examples"] == 16,
                       "queries": c["queries"], "wall_s": round(c["wall_s"], 2),
                       "victim_queries_per_s": round(c["queries"] / c["wall_s"], 3),
                       "sample": f"the same greedy loop (host featurisation + oracle/roberta_cpu.py "
                                 f"fp32 eager scoring of padded 512-id rows in batches of 64, "
-                                f"torch threads={threads}) over the first {cpu_seconds:.0f} s "
-                                f"(stopped at the first batch past the budget)"}
+                                f"torch threads={threads}, one per physical core of the "
+                                f"process's affinity), all 16 functions unless the "
+                                f"{cpu_seconds:.0f} s cap stops it at the first batch past it"}
+        key = lambda r: (r["is_success"], r["queries"], r.get("adv_code"))  # noqa: E731
+        res["cpu"]["same_outcome_as_gpu"] = sum(key(a) == key(b) for a, b in
+                                                zip(g["records"], c["records"]))
         res["gpu_vs_cpu_queries_per_s"] = round(res["gpu"]["victim_queries_per_s"]
                                                 / max(res["cpu"]["victim_queries_per_s"], 1e-9), 1)
     return res
@@ -286,13 +304,10 @@ def config1_leg(dev, precision, threads, cpu_seconds):
 
 def attack_leg(dev, n_examples, deadline_s, inflight, rank, world, precision):
     """End-to-end config-2 workload: greedy -> GA attack (gi_attack.py --use_ga) over the first
-    `n_examples` of test_subs_0_400, block 512, eval_batch_size 64, with cross-example batching
-    (drivers.run_gi_attack_batched); ranks pull examples from one shared queue."""
-    import numpy as np
-    import torch
-
-    from apmc_amd.dist import DynamicQueue, call_key
-    from apmc_amd.drivers import AttackArgs, load_fixture, run_gi_attack_batched
+    `n_examples` of test_subs_0_400, block 512, eval_batch_size 64, with cross-example batching;
+    ranks pull examples from one shared queue (dist.run_sharded_gi_batched)."""
+    from apmc_amd.dist import run_sharded_gi_batched
+    from apmc_amd.drivers import AttackArgs, load_fixture
     from apmc_amd.model import Model
     from apmc_amd.weights import synthetic_state_dict
 
@@ -300,41 +315,24 @@ def attack_leg(dev, n_examples, deadline_s, inflight, rank, world, precision):
     model = Model(synthetic_state_dict(seed=VICTIM_SEED, head="sigmoid1", out_std=VICTIM_OUT_STD),
                   task="devign", precision=precision, device=dev.index)
     args = AttackArgs(block_size=512, eval_batch_size=64, seed=123456, rng="per_example")
-    queue = DynamicQueue(len(codes), key=call_key("bench_attack_queue"),
-                         deadline=time.time() + deadline_s)
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-    out = run_gi_attack_batched(model, codes, subs, labels, args, queue=queue,
-                                max_inflight=inflight)
-    recs = out["records"]
-    stats = np.array([out["examples"], out["total_cnt"], out["success"], out["queries"],
-                      out["wall_s"], sum(r["attack_type"] == "GA" for r in recs),
-                      sum(r["attack_type"] == "GA" and r["is_success"] == 1 for r in recs)],
-                     dtype=np.float64)
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor(stats, device=dev)
-        g = [torch.zeros_like(t) for _ in range(world)]
-        dist.all_gather(g, t)
-        allst = torch.stack(g).cpu().numpy()
-    else:
-        allst = stats[None]
-    ex, cnt, suc, q = allst[:, 0].sum(), allst[:, 1].sum(), allst[:, 2].sum(), allst[:, 3].sum()
-    wall = allst[:, 4].max()
+    _, t = run_sharded_gi_batched(model, codes, subs, labels, args, max_inflight=inflight,
+                                  device=dev, deadline=time.time() + deadline_s,
+                                  key="bench_attack_queue")
     model.engine.close()
+    wall = t["wall_s"]
     return {"workload": "CodeBERT Devign greedy->GA attack (gi_attack --use_ga), "
                         f"test_subs_0_400.jsonl examples [0, {n_examples}), block 512, "
                         "eval_batch_size 64, attack-sensitive synthetic victim "
                         f"(seed {VICTIM_SEED}, out_proj std {VICTIM_OUT_STD})",
             "precision": precision,
-            "examples": int(ex), "complete": bool(ex == n_examples),
-            "correctly_classified": int(cnt), "successes": int(suc),
-            "success_rate": round(suc / cnt, 4) if cnt else None,
-            "ga_runs": int(allst[:, 5].sum()), "ga_successes": int(allst[:, 6].sum()),
-            "victim_queries": int(q), "wall_s": round(wall, 2),
-            "victim_queries_per_s": round(q / wall, 2),
-            "attacked_examples_per_min": round(60 * ex / wall, 3),
+            "examples": t["examples"], "complete": t["examples"] == n_examples,
+            "correctly_classified": t["total_cnt"], "successes": t["success"],
+            "success_rate": round(t["success_rate"], 4) if t["total_cnt"] else None,
+            "ga_runs": t["ga_runs"], "ga_successes": t["ga_successes"],
+            "victim_queries": t["queries"], "wall_s": round(wall, 2),
+            "victim_queries_per_s": round(t["queries"] / wall, 2),
+            "attacked_examples_per_min": round(60 * t["examples"] / wall, 3),
+            "per_rank": t["per_rank"],
             "rng": "random.Random(123456 + index) per example",
             "batching": f"cross-example: up to {inflight} examples' requests per device batch",
             "sharding": "dynamic queue (torch.distributed store counter)"}
@@ -343,12 +341,10 @@ def attack_leg(dev, n_examples, deadline_s, inflight, rank, world, precision):
 def mhm_leg(dev, n_examples, seq_examples, rank, world, precision):
     """Config-5 baseline workload: MHM-NS (mhm_attack.py, n_candi 30, max_iter 100, threshold 1)
     over test_subs_0_400 with the CodeBERT Devign victim.  Batched: the first `n_examples` fixture
-    examples (strided over ranks) with every chain in flight at once (`mcmc_batched`); sequential:
-    the reference loop (one ≤31-candidate batch per query round) over the first `seq_examples`
-    of them, for the comparison (rank 0, N=1 only)."""
-    import numpy as np
-    import torch
-
+    examples pulled from one queue shared by the ranks (dist.run_sharded_mhm), every chain a
+    rank holds in flight at once; sequential: the reference loop (one <=31-candidate batch per
+    query round) over the first `seq_examples` of them, for the comparison (rank 0, N=1 only)."""
+    from apmc_amd.dist import run_sharded_mhm
     from apmc_amd.drivers import AttackArgs, load_fixture, run_mhm_attack
     from apmc_amd.model import Model
     from apmc_amd.weights import synthetic_state_dict
@@ -357,34 +353,22 @@ def mhm_leg(dev, n_examples, seq_examples, rank, world, precision):
     model = Model(synthetic_state_dict(seed=VICTIM_SEED, head="sigmoid1", out_std=VICTIM_OUT_STD),
                   task="devign", precision=precision, device=dev.index)
     args = AttackArgs(block_size=512, eval_batch_size=64, seed=123456)
-    mine = list(range(rank, n_examples, world))
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-    out = run_mhm_attack(model, codes, subs, labels, args, indices=mine, max_iter=100,
-                         prob_threshold=1, max_inflight=len(mine))
-    st = np.array([out["examples"], out["total_cnt"], out["success"], out["queries"],
-                   out["wall_s"]], dtype=np.float64)
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor(st, device=dev)
-        g = [torch.zeros_like(t) for _ in range(world)]
-        dist.all_gather(g, t)
-        allst = torch.stack(g).cpu().numpy()
-    else:
-        allst = st[None]
-    ex, cnt, suc, q = allst[:, :4].sum(0)
-    wall = allst[:, 4].max()
+    _, t = run_sharded_mhm(model, codes, subs, labels, args, max_iter=100, prob_threshold=1,
+                           max_inflight=64, device=dev, n=n_examples, key="bench_mhm_queue")
+    wall = t["wall_s"]
     res = {"workload": "MHM-NS (mhm_attack.py: n_candi 30, max_iter 100) CodeBERT Devign victim, "
                        f"test_subs_0_400 examples [0, {n_examples}), block 512",
-           "precision": precision, "examples": int(ex), "correctly_classified": int(cnt),
-           "successes": int(suc), "success_rate": round(suc / cnt, 4) if cnt else None,
-           "victim_queries": int(q), "wall_s": round(wall, 2),
-           "victim_queries_per_s": round(q / wall, 2),
-           "attacked_examples_per_min": round(60 * ex / wall, 3),
-           "mode": "cross-example batched chains (mcmc_batched), random.Random(123456 + index)"}
+           "precision": precision, "examples": t["examples"],
+           "correctly_classified": t["total_cnt"], "successes": t["success"],
+           "success_rate": round(t["success_rate"], 4) if t["total_cnt"] else None,
+           "victim_queries": t["queries"], "wall_s": round(wall, 2),
+           "victim_queries_per_s": round(t["queries"] / wall, 2),
+           "attacked_examples_per_min": round(60 * t["examples"] / wall, 3),
+           "per_rank": t["per_rank"],
+           "mode": "cross-example batched chains (up to 64 per device batch), "
+                   "random.Random(123456 + index), dynamic queue"}
     if rank == 0 and world == 1 and seq_examples > 0:
-        seq = run_mhm_attack(model, codes, subs, labels, args, indices=mine[:seq_examples],
+        seq = run_mhm_attack(model, codes, subs, labels, args, indices=range(seq_examples),
                              max_iter=100, prob_threshold=1, max_inflight=1)
         res["sequential"] = {"examples": seq["examples"], "victim_queries": seq["queries"],
                              "wall_s": round(seq["wall_s"], 2),
@@ -395,20 +379,14 @@ def mhm_leg(dev, n_examples, seq_examples, rank, world, precision):
     return res
 
 
-def _gather_sum_max(vals, dev, world, nsum):
-    """all-gather one float64 vector per rank; sum the first nsum entries, max the rest."""
-    import numpy as np
-    import torch
-    v = np.asarray(vals, dtype=np.float64)
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor(v, device=dev)
-        g = [torch.zeros_like(t) for _ in range(world)]
-        dist.all_gather(g, t)
-        allv = torch.stack(g).cpu().numpy()
-    else:
-        allv = v[None]
-    return np.concatenate([allv[:, :nsum].sum(0), allv[:, nsum:].max(0)])
+def _summary(t):
+    wall = t["wall_s"]
+    return {"examples": t["examples"], "attacked": t["total_cnt"], "successes": t["success"],
+            "success_rate": round(t["success_rate"], 4) if t["total_cnt"] else None,
+            "victim_queries": t["queries"], "wall_s": round(wall, 2),
+            "victim_queries_per_s": round(t["queries"] / wall, 1) if wall else None,
+            "attacked_examples_per_min": round(60 * t["examples"] / wall, 2) if wall else None,
+            "per_rank": t["per_rank"]}
 
 
 def aa_leg(dev, n_examples, n_gcb, rank, world, precision):
@@ -418,10 +396,10 @@ def aa_leg(dev, n_examples, n_gcb, rank, world, precision):
     CodeBERT victim and programs of valid_subs.jsonl, then the GraphCodeBERT victim's GA
     (GraphCodeBERT/Authorship-Attribution, code_length 512 + data_flow_length 128) on the first
     n_gcb programs.  Synthetic victims (seed 5, out_proj std 8) do not know the authors, so each
-    program's label is the victim's own prediction (every program is attacked)."""
-    from apmc_amd.dist import DynamicQueue, call_key
-    from apmc_amd.drivers import AttackArgs, _example, load_fixture, run_gi_attack_batched, \
-        run_mhm_attack
+    program's label is the victim's own prediction (every program is attacked).  Each half pulls
+    its programs from one queue shared by the ranks."""
+    from apmc_amd.dist import run_sharded_gi_batched, run_sharded_mhm
+    from apmc_amd.drivers import AttackArgs, _example, load_fixture
     from apmc_amd.graph import GraphModel
     from apmc_amd.host import Tokenizer
     from apmc_amd.model import Model
@@ -437,33 +415,16 @@ def aa_leg(dev, n_examples, n_gcb, rank, world, precision):
     res = {"workload": f"Authorship-Attribution valid_subs.jsonl programs [0, {len(codes)}), "
                        "66-way CodeBERT victim (synthetic, labels = its own predictions)",
            "precision": precision}
-
-    def summary(vals, examples_key="examples"):
-        ex, cnt, suc, q, wall = vals
-        return {"examples": int(ex), "attacked": int(cnt), "successes": int(suc),
-                "success_rate": round(suc / cnt, 4) if cnt else None,
-                "victim_queries": int(q), "wall_s": round(wall, 2),
-                "victim_queries_per_s": round(q / wall, 1) if wall else None,
-                "attacked_examples_per_min": round(60 * ex / wall, 2) if wall else None}
-
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
     args = AttackArgs(block_size=512, eval_batch_size=32, seed=123456, rng="per_example",
                       task="authorship")
-    queue = DynamicQueue(len(codes), key=call_key("bench_aa_ga_queue"))
-    out = run_gi_attack_batched(model, codes, subs, labels, args, queue=queue, max_inflight=64)
-    res["ga"] = summary(_gather_sum_max([out["examples"], out["total_cnt"], out["success"],
-                                         out["queries"], out["wall_s"]], dev, world, 4))
-    res["ga"]["mode"] = "greedy -> GA (attack.py), cross-example batched"
+    _, t = run_sharded_gi_batched(model, codes, subs, labels, args, max_inflight=64, device=dev,
+                                  key="bench_aa_ga_queue")
+    res["ga"] = dict(_summary(t), mode="greedy -> GA (attack.py), cross-example batched")
     log("authorship leg: MHM-NS")
     margs = AttackArgs(block_size=512, eval_batch_size=64, seed=123456, task="authorship")
-    mine = list(range(rank, len(codes), world))
-    out = run_mhm_attack(model, codes, subs, labels, margs, indices=mine, max_iter=100,
-                         prob_threshold=1, max_inflight=max(1, len(mine)))
-    res["mhm"] = summary(_gather_sum_max([out["examples"], out["total_cnt"], out["success"],
-                                          out["queries"], out["wall_s"]], dev, world, 4))
-    res["mhm"]["mode"] = "MHM-NS (mhm.py), cross-example batched chains"
+    _, t = run_sharded_mhm(model, codes, subs, labels, margs, max_iter=100, prob_threshold=1,
+                           max_inflight=128, device=dev, key="bench_aa_mhm_queue")
+    res["mhm"] = dict(_summary(t), mode="MHM-NS (mhm.py), cross-example batched chains")
     model.engine.close()
     if n_gcb > 0:
         log("authorship leg: GraphCodeBERT GA")
@@ -474,14 +435,11 @@ def aa_leg(dev, n_examples, n_gcb, rank, world, precision):
         gcodes, gsubs = codes[:n_gcb], subs[:n_gcb]
         glabels = [int(gmodel.get_results([_example(tok, c, 0, 512, "gcb_authorship", gargs)])[1][0])
                    for c in gcodes]
-        queue = DynamicQueue(len(gcodes), key=call_key("bench_aa_gcb_queue"))
-        out = run_gi_attack_batched(gmodel, gcodes, gsubs, glabels, gargs, queue=queue,
-                                    max_inflight=64)
-        res["gcb_ga"] = summary(_gather_sum_max([out["examples"], out["total_cnt"],
-                                                 out["success"], out["queries"], out["wall_s"]],
-                                                dev, world, 4))
-        res["gcb_ga"]["mode"] = ("GraphCodeBERT victim, greedy -> GA (GraphAuthorshipAttacker), "
-                                 f"programs [0, {len(gcodes)}), L = 640 with the data-flow mask")
+        _, t = run_sharded_gi_batched(gmodel, gcodes, gsubs, glabels, gargs, max_inflight=64,
+                                      device=dev, key="bench_aa_gcb_queue")
+        res["gcb_ga"] = dict(_summary(t),
+                             mode="GraphCodeBERT victim, greedy -> GA (GraphAuthorshipAttacker), "
+                                  f"programs [0, {len(gcodes)}), L = 640 with the data-flow mask")
         gmodel.engine.close()
     return res
 
@@ -492,8 +450,8 @@ def clone_leg(dev, n_examples, rank, world, precision):
     greedy -> GA on code1 of each pair, both codes through the graph forward at L = 640 with the
     data-flow mask, the pair head over [code1 | code2] CLS rows.  Synthetic victim (seed 5,
     out_proj std 8); labels are its own predictions, so every pair is attacked."""
-    from apmc_amd.dist import DynamicQueue, call_key
-    from apmc_amd.drivers import AttackArgs, _example, load_fixture, run_gi_attack_batched
+    from apmc_amd.dist import run_sharded_gi_batched
+    from apmc_amd.drivers import AttackArgs, _example, load_fixture
     from apmc_amd.graph import GraphModel
     from apmc_amd.host import Tokenizer
     from apmc_amd.weights import synthetic_state_dict
@@ -506,24 +464,17 @@ def clone_leg(dev, n_examples, rank, world, precision):
     gmodel = GraphModel(sd, task="clone", args=gargs, precision=precision, device=dev.index)
     labels = [int(gmodel.get_results([_example(tok, c, 0, 512, "gcb_clone", gargs)])[1][0])
               for c in codes]
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-    queue = DynamicQueue(len(codes), key=call_key("bench_clone_gcb_queue"))
-    out = run_gi_attack_batched(gmodel, codes, subs, labels, gargs, queue=queue, max_inflight=64)
-    ex, cnt, suc, q, wall = _gather_sum_max([out["examples"], out["total_cnt"], out["success"],
-                                             out["queries"], out["wall_s"]], dev, world, 4)
+    _, t = run_sharded_gi_batched(gmodel, codes, subs, labels, gargs, max_inflight=64,
+                                  device=dev, key="bench_clone_gcb_queue")
     gmodel.engine.close()
-    return {"workload": f"GraphCodeBERT BigCloneBench pairs test_subs_0_500.jsonl [0, {len(codes)}),"
-                        " greedy -> GA on code1, code_length 512 + data_flow_length 128 per code, "
-                        "pair head (synthetic victim, labels = its own predictions)",
-            "precision": precision, "examples": int(ex), "attacked": int(cnt),
-            "successes": int(suc), "success_rate": round(suc / cnt, 4) if cnt else None,
-            "victim_queries": int(q), "wall_s": round(wall, 2),
-            "victim_queries_per_s": round(q / wall, 1) if wall else None,
-            "sequences_per_s": round(2 * q / wall, 1) if wall else None,
-            "attacked_examples_per_min": round(60 * ex / wall, 2) if wall else None,
-            "batching": "cross-example: up to 64 pairs' requests per device batch"}
+    out = _summary(t)
+    out["sequences_per_s"] = round(2 * t["queries"] / t["wall_s"], 1) if t["wall_s"] else None
+    return dict({"workload": f"GraphCodeBERT BigCloneBench pairs test_subs_0_500.jsonl "
+                             f"[0, {len(codes)}), greedy -> GA on code1, code_length 512 + "
+                             "data_flow_length 128 per code, pair head (synthetic victim, "
+                             "labels = its own predictions)",
+                 "precision": precision}, **out,
+                batching="cross-example: up to 64 pairs' requests per device batch")
 
 
 def subs_leg(dev, seconds, rank, world, precision):
@@ -705,7 +656,7 @@ def main():
     if fp32_mode:
         res["fp32_mode"] = fp32_mode
     eng.close()
-    threads, phys = host_cores()
+    threads, cpu_facts = host_cores()
     log(f"scoring step: {value:.1f} q/s")
     if args.attack_examples > 0:
         log("config-2 attack leg")
@@ -730,13 +681,18 @@ def main():
         res["mhm"] = mhm_leg(dev, args.mhm_examples, args.mhm_seq_examples, rank, world,
                              args.precision)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        log("CPU baseline")
+        log(f"CPU baseline ({threads} threads)")
         v, sample = cpu_baseline(L, args.cpu_seconds, threads)
         res["cpu_baseline"] = {"value": v, "unit": "victim queries/s", "cores": threads,
                                "kind": "port",
                                "sample": sample + f", oracle/roberta_cpu.py fp32 eager, torch "
-                                                  f"threads={threads} (this job's CPU share; "
-                                                  f"host has {phys} physical cores)"}
+                                                  f"threads={threads} = one per physical core "
+                                                  f"of this process's CPU affinity",
+                               **cpu_facts}
+        share = cpu_facts.get("job_share_threads")
+        if share and share < threads:
+            v16, s16 = cpu_baseline(L, args.cpu_seconds, share)
+            res["cpu_baseline"]["job_share"] = {"value": v16, "cores": share, "sample": s16}
         res["speedup_vs_cpu"] = round(value / v, 2)
     if rank == 0:
         print(json.dumps(res), flush=True)

@@ -256,11 +256,16 @@ def test_graphcodebert_greedy_then_ga_matches_text_oracle():
     assert kinds
 
 
+# config-5 MHM-NS shape (mhm_attack.py:215-217 / Authorship mhm.py:198-206): block 512,
+# n_candi 30, max_iter 100, _prob_threshold 1
+MHM_BLOCK, MHM_ITERS, MHM_THRESHOLD = 512, 100, 1
+
+
 @pytest.mark.parametrize("kind", ["mcmc", "mcmc_random"])
 def test_mhm_matches_text_oracle(victim, kind):
-    """MHM-NS baseline (attacker.py:466-738): product MHM_Attacker (host mutants, engine scoring)
-    vs oracle/mhm_ref.py over text, same Python `random` seed: identical outcome, adversarial
-    code, replacement chain and query count."""
+    """MHM-NS baseline (attacker.py:466-738) at the config-5 shape: product MHM_Attacker (host
+    mutants, engine scoring) vs oracle/mhm_ref.py over text, same Python `random` seed: identical
+    outcome, adversarial code, replacement chain and query count over 100-iteration chains."""
     from apmc_amd.attacker import MHM_Attacker
     from apmc_amd.drivers import AttackArgs, load_fixture
     from apmc_amd.host import Tokenizer
@@ -269,7 +274,7 @@ def test_mhm_matches_text_oracle(victim, kind):
 
     codes, subs, labels = load_fixture(FIXTURE, 0, 120)
     tok = Tokenizer()
-    args = AttackArgs(block_size=BLOCK, eval_batch_size=32)
+    args = AttackArgs(block_size=MHM_BLOCK, eval_batch_size=64)
     vocab = sorted({w for s in subs[:60] for v in s.values() for w in v})
     idx2token = vocab if kind == "mcmc_random" else None
     att = MHM_Attacker(args, victim, None, tok, {w: i for i, w in enumerate(vocab)}, vocab)
@@ -278,34 +283,93 @@ def test_mhm_matches_text_oracle(victim, kind):
         code, sb, lab = codes[i], subs[i], labels[i]
         random.seed(3000 + i)
         q0 = victim.query
-        res = getattr(att, kind)(tok, sb, code, lab, _n_candi=30, _max_iter=12)
+        res = getattr(att, kind)(tok, sb, code, lab, _n_candi=30, _max_iter=MHM_ITERS,
+                                 _prob_threshold=MHM_THRESHOLD)
         q_prod = victim.query - q0
         random.seed(3000 + i)
-        v = attack_ref.Victim(_score_fn(victim), BLOCK)
-        ref = mhm_ref.mcmc(v, isUID, sb, code, lab, n_candi=30, max_iter=12, idx2token=idx2token)
+        v = attack_ref.Victim(_score_fn(victim), MHM_BLOCK)
+        ref = mhm_ref.mcmc(v, isUID, sb, code, lab, n_candi=30, max_iter=MHM_ITERS,
+                           prob_threshold=MHM_THRESHOLD, idx2token=idx2token)
         assert res["succ"] == ref["succ"], i
         assert q_prod == v.query, (i, q_prod, v.query)
         if res["succ"] is not None:
-            assert res["tokens"] == ref["tokens"], i
-            assert res["replace_info"] == ref["replace_info"], i
-            assert res["nb_changed_var"] == ref["nb_changed_var"]
-            assert res["nb_changed_pos"] == ref["nb_changed_pos"]
-            assert res["prog_length"] == ref["prog_length"]
+            for k in ("tokens", "replace_info", "nb_changed_var", "nb_changed_pos",
+                      "prog_length", "new_pred"):
+                assert res[k] == ref[k], (i, k)
         seen.append(res["succ"])
+    print(kind, seen)
     assert any(s is not None for s in seen)
 
 
+def test_authorship_mhm_matches_text_oracle():
+    """Config 5's baseline half: MHM-NS on the 66-way authorship victim
+    (CodeXGLUE/Authorship-Attribution/code/attacker.py:440-666, driven as mhm.py:160-213: Python
+    leaves, raw-text features, argmax predictions; block 512, n_candi 30, max_iter 100,
+    _prob_threshold 1) on the HIP engine against oracle/mhm_ref.py scoring the same mutant texts
+    with the same engine: identical outcome, adversarial code, replacement chain and query count.
+    Labels are the victim's own predictions (the synthetic victim does not know the authors), so
+    every program is attacked; the sample must include a success."""
+    from apmc_amd.attacker import AuthorshipMHM_Attacker
+    from apmc_amd.drivers import AttackArgs, _example
+    from apmc_amd.host import Tokenizer
+    from apmc_amd.model import Model
+    from apmc_amd.utils import isUID
+    from oracle import mhm_ref
+    from test_task_attacks import fixture
+
+    model = Model(synthetic_sd(seed=5, head="softmaxN", num_labels=66, out_std=8.0),
+                  task="authorship")
+
+    def score(ids):
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        lens = (ids != 1).sum(1).astype(np.int32)
+        return model.engine.score(torch.from_numpy(ids).cuda(), lens).cpu().numpy()
+
+    codes, subs, _ = fixture("authorship", 6)
+    tok = Tokenizer()
+    labels = [int(p) for p in model.get_results([_example(tok, c, 0, MHM_BLOCK, "authorship")
+                                                 for c in codes])[1]]
+    args = AttackArgs(block_size=MHM_BLOCK, eval_batch_size=64, task="authorship",
+                      lang="python")
+    vocab = sorted({w for s in subs for v in s.values() for w in v})
+    att = AuthorshipMHM_Attacker(args, model, None, tok, {w: i for i, w in enumerate(vocab)},
+                                 vocab)
+    seen = []
+    for i in range(len(codes)):
+        random.seed(3300 + i)
+        q0 = model.query
+        res = att.mcmc(tok, codes[i], labels[i], _n_candi=30, _max_iter=MHM_ITERS,
+                       _prob_threshold=MHM_THRESHOLD, subs=subs[i])
+        q_prod = model.query - q0
+        random.seed(3300 + i)
+        v = attack_ref.Victim(score, MHM_BLOCK, task="authorship")
+        ref = mhm_ref.mcmc(v, isUID, subs[i], codes[i], labels[i], n_candi=30,
+                           max_iter=MHM_ITERS, prob_threshold=MHM_THRESHOLD, lang="python",
+                           skip_known=False)
+        assert res["succ"] == ref["succ"], i
+        assert q_prod == v.query, (i, q_prod, v.query)
+        if res["succ"] is not None:
+            for k in ("tokens", "replace_info", "nb_changed_var", "nb_changed_pos",
+                      "prog_length", "new_pred"):
+                assert res[k] == ref[k], (i, k)
+        seen.append((res["succ"], q_prod))
+    print("authorship mhm", seen)
+    assert sum(s is True for s, _ in seen) >= 1 and len(seen) >= 4, seen
+    model.engine.close()
+
+
 def test_mhm_batched_equals_sequential_on_engine(victim):
-    """Cross-example batched MHM-NS (mcmc_batched) on the HIP engine: many
-    chains share each device batch, and every chain still equals `random.seed(s); mcmc(...)` run
-    alone (the engine scores rows batch-invariantly), with the same per-example query counts."""
+    """Cross-example batched MHM-NS (mcmc_batched) on the HIP engine at the
+    config-5 shape: many chains share each device batch, and every chain still equals
+    `random.seed(s); mcmc(...)` run alone (the engine scores rows batch-invariantly), with the
+    same per-example query counts."""
     from apmc_amd.attacker import MHM_Attacker
     from apmc_amd.drivers import AttackArgs, load_fixture
     from apmc_amd.host import Tokenizer
 
     codes, subs, labels = load_fixture(FIXTURE, 0, 120)
     tok = Tokenizer()
-    args = AttackArgs(block_size=BLOCK, eval_batch_size=32)
+    args = AttackArgs(block_size=MHM_BLOCK, eval_batch_size=64)
     vocab = sorted({w for s in subs[:60] for v in s.values() for w in v})
     att = MHM_Attacker(args, victim, None, tok, {w: i for i, w in enumerate(vocab)}, vocab)
     jobs = [(subs[i], codes[i], labels[i], 5000 + i) for i in _pick(codes, subs, 8)]
@@ -313,15 +377,14 @@ def test_mhm_batched_equals_sequential_on_engine(victim):
     for sb, code, lab, seed in jobs:
         random.seed(seed)
         q0 = victim.query
-        res = att.mcmc(tok, sb, code, lab, _n_candi=30, _max_iter=10)
+        res = att.mcmc(tok, sb, code, lab, _n_candi=30, _max_iter=MHM_ITERS,
+                       _prob_threshold=MHM_THRESHOLD)
         seq.append((res, victim.query - q0))
-    got = att.mcmc_batched(tok, jobs, _n_candi=30, _max_iter=10, max_inflight=8)
+    got = att.mcmc_batched(tok, jobs, _n_candi=30, _max_iter=MHM_ITERS,
+                           _prob_threshold=MHM_THRESHOLD, max_inflight=8)
     for j, ((rs, qs), (rb, qb)) in enumerate(zip(seq, got)):
         assert qs == qb, j
-        assert rs["succ"] == rb["succ"], j
-        if rs["succ"] is not None:
-            assert rs["tokens"] == rb["tokens"], j
-            assert rs["replace_info"] == rb["replace_info"], j
+        assert rs == rb, j
 
 
 @pytest.mark.parametrize("task", ["clone", "authorship"])

@@ -139,3 +139,56 @@ def test_sharded_substitutes_match_single_process(tmp_path):
     tot = json.loads((tmp_path / "tot.json").read_text())
     assert tot["items"] == N_EX and all(r[0] >= 1 for r in tot["per_rank"])
     assert not list(tmp_path.glob("subs.jsonl.rank*"))
+
+
+def _batched_worker(rank, world, port, outdir):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), LOCAL_RANK=str(rank))
+    sys.path.insert(0, str(ROOT))
+    import _apmc  # noqa: F401
+    from apmc_amd.dist import init_from_env, run_sharded_gi_batched, run_sharded_mhm
+    from apmc_amd.drivers import AttackArgs, load_fixture
+    import torch.distributed as dist
+
+    init_from_env("gloo")
+    codes, subs, labels = load_fixture(FIXTURE, 0, N_EX)
+    args = AttackArgs(block_size=128, eval_batch_size=8, rng="per_example")
+    gi, gi_tot = run_sharded_gi_batched(FakeVictim(), codes, subs, labels, args, max_inflight=4)
+    mhm, mhm_tot = run_sharded_mhm(FakeVictim(), codes, subs, labels, args, max_iter=8,
+                                   max_inflight=4)
+    if rank == 0:
+        import json
+        (pathlib.Path(outdir) / "batched.json").write_text(json.dumps(
+            {"gi": gi, "gi_tot": gi_tot, "mhm": mhm, "mhm_tot": mhm_tot}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_batched_drivers_match_single_process(tmp_path):
+    """The bench legs' multi-GPU form (dist.run_sharded_gi_batched / run_sharded_mhm: one dynamic
+    queue per leg, cross-example batching inside each rank, all-gathered totals with per-rank
+    rows, records merged by index) on 2 gloo ranks equals the single-process batched drivers."""
+    sys.path.insert(0, str(ROOT))
+    import json
+    import random
+    import _apmc  # noqa: F401
+    from apmc_amd.drivers import AttackArgs, load_fixture, run_gi_attack_batched, run_mhm_attack
+
+    port = 33500 + random.Random(os.getpid()).randint(0, 2000)
+    mp.spawn(_batched_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    got = json.loads((tmp_path / "batched.json").read_text())
+
+    codes, subs, labels = load_fixture(FIXTURE, 0, N_EX)
+    args = AttackArgs(block_size=128, eval_batch_size=8, rng="per_example")
+    gi = run_gi_attack_batched(FakeVictim(), codes, subs, labels, args, max_inflight=4)
+    keys = ["index", "is_success", "attack_type", "queries", "adv_code", "replace_info"]
+    assert [{k: r[k] for k in keys} for r in got["gi"]] == \
+        [{k: r[k] for k in keys} for r in gi["records"]]
+    assert got["gi_tot"]["queries"] == gi["queries"] and got["gi_tot"]["examples"] == N_EX
+    mhm = run_mhm_attack(FakeVictim(), codes, subs, labels, args, max_iter=8, max_inflight=4)
+    assert got["mhm"] == mhm["records"]
+    assert got["mhm_tot"]["queries"] == mhm["queries"]
+    assert {r["is_success"] for r in mhm["records"]} & {1, -1}
+    for tot in (got["gi_tot"], got["mhm_tot"]):
+        assert len(tot["per_rank"]) == 2 and all(r["examples"] >= 1 for r in tot["per_rank"])
+        assert sum(r["examples"] for r in tot["per_rank"]) == N_EX
