@@ -3,10 +3,30 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <map>
+#include <mutex>
+#include <utility>
+
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef short shortx8 __attribute__((ext_vector_type(8)));
 typedef unsigned short ushortx4 __attribute__((ext_vector_type(4)));
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device): the attribute is
+// per device, so a process driving two GPUs sets it on each; thread-safe.
+inline hipError_t ensure_dynamic_lds(const void* fn, size_t lds) {
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, size_t> done;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> g(mu);
+  size_t& have = done[{fn, dev}];
+  if (have >= lds) return hipSuccess;
+  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e == hipSuccess) have = lds;
+  return e;
+}
 
 #define AE_HIDDEN 768
 #define AE_HEAD_DIM 64

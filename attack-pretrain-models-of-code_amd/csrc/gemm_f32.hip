@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_nt_kernel(
         }
         continue;
       }
-      const float bv = bias[col];
+      const float bv = bias ? bias[col] : 0.f;  // null bias: same rule as splitk_reduce
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * 64 + a * 32 + mfma32_row(r, lh);

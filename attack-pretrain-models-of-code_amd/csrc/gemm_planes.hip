@@ -942,13 +942,8 @@ template <int NP, int EPI, int DIAG>
 hipError_t pp_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R, float* C,
                      __bf16* Cp, int M, int N, int K, int group_m, hipStream_t st) {
   constexpr int lds = 2 * (256 + 256) * PK_ROWB;  // 128 KiB
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_pp_kernel<NP, EPI, DIAG>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
+  if (hipError_t e = ensure_dynamic_lds((const void*)gemm_pp_kernel<NP, EPI, DIAG>, lds); e != hipSuccess)
+    return e;
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
   hipLaunchKernelGGL((gemm_pp_kernel<NP, EPI, DIAG>), dim3(tiles), dim3(512), lds, st, A, W, bias,
                      R, C, Cp, M, N, K, group_m);
@@ -981,13 +976,8 @@ template <int NP, int EPI, bool NT = false>
 hipError_t pp192_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R,
                         float* C, int M, int N, int K, int group_m, hipStream_t st) {
   constexpr int lds = 2 * (256 + 192) * PK_ROWB;  // 112 KiB
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_pp192_kernel<NP, EPI, NT>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
+  if (hipError_t e = ensure_dynamic_lds((const void*)gemm_pp192_kernel<NP, EPI, NT>, lds); e != hipSuccess)
+    return e;
   const int tiles = ((M + 255) / 256) * ((N + 191) / 192);
   hipLaunchKernelGGL((gemm_pp192_kernel<NP, EPI, NT>), dim3(tiles), dim3(512), lds, st, A, W, bias, R,
                      C, M, N, K, group_m);
@@ -1034,13 +1024,8 @@ template <int BN, int NP, int EPI, int DIAG>
 hipError_t pk_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R, float* C,
                      __bf16* Cp, int M, int N, int K, hipStream_t st) {
   constexpr int lds = pk_stages<BN>() * (PK_BM + BN) * PK_ROWB;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_pk_kernel<BN, NP, EPI, DIAG>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
+  if (hipError_t e = ensure_dynamic_lds((const void*)gemm_pk_kernel<BN, NP, EPI, DIAG>, lds); e != hipSuccess)
+    return e;
   const int tiles = ((M + PK_BM - 1) / PK_BM) * ((N + BN - 1) / BN);
   hipLaunchKernelGGL((gemm_pk_kernel<BN, NP, EPI, DIAG>), dim3(tiles), dim3(512), lds, st, A, W,
                      bias, R, C, Cp, M, N, K, PK_GROUP_M);

@@ -230,7 +230,7 @@ __global__ __launch_bounds__(512, (BM * BN >= 256 * 256 ? 2 : 4)) void gemm_x3_k
         }
         continue;
       }
-      const float bv = bias[col];
+      const float bv = bias ? bias[col] : 0.f;  // null bias: same rule as splitk_reduce
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * (BM / WM) + a * 32 + mfma32_row(r, lh);

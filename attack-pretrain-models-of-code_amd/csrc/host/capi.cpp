@@ -121,12 +121,12 @@ int32_t ah_gcb_features_batch(ah_tokenizer* tok, int32_t n, const char* const* c
   ah::GcbArgs a{(ah::Lang)lang, (ah::DfgVariant)variant, (flags & AH_GCB_NORMALIZE) != 0,
                 (flags & AH_GCB_RUN_TRUNC) != 0, code_length, data_flow_length, e_cap};
   const int nthr = std::max(1, std::min(std::min(threads, n), 64));
-  {
-    std::lock_guard<std::mutex> g(tok->mu);
-    while ((int)tok->clones.size() < nthr) {
-      tok->clones.emplace_back(new ah::Tokenizer(tok->t));
-      tok->leaf_caches.emplace_back(new std::unordered_map<std::string, std::vector<int32_t>>[2]);
-    }
+  // the whole batch holds the tokenizer: its worker clones and their BPE / leaf caches are
+  // shared state, so concurrent calls on one tokenizer serialise here
+  std::lock_guard<std::mutex> g(tok->mu);
+  while ((int)tok->clones.size() < nthr) {
+    tok->clones.emplace_back(new ah::Tokenizer(tok->t));
+    tok->leaf_caches.emplace_back(new std::unordered_map<std::string, std::vector<int32_t>>[2]);
   }
   std::vector<std::string> errs(nthr);
   std::vector<char> ok(nthr, 1);

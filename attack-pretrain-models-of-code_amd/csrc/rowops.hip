@@ -419,13 +419,9 @@ hipError_t ae_launch_graph_mask(const int* ids, const int* meta, const int* span
                                 hipStream_t st) {
   if (n <= 0) return hipSuccess;
   const size_t lds = (size_t)L * (L / 32) * 4;
-  static size_t attr = 0;
-  if (lds > 65536 && attr < lds) {
-    hipError_t e = hipFuncSetAttribute((const void*)graph_mask_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    attr = lds;
-  }
+  if (lds > 65536)
+    if (hipError_t e = ensure_dynamic_lds((const void*)graph_mask_kernel, lds); e != hipSuccess)
+      return e;
   hipLaunchKernelGGL(graph_mask_kernel, dim3(n), dim3(256), lds, st, ids, meta, spans, edges, L,
                      e_cap, bits);
   return hipGetLastError();

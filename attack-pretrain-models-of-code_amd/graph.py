@@ -216,9 +216,7 @@ def compact_features(f, e_cap: int | None = None) -> dict:
         if a < ni and b < ni:
             spans[k] = a | (b << 16)
     edges = [k | (t << 16) for k, ts in enumerate(f.dfg_to_dfg) for t in ts if ni + t < L]
-    if len(edges) > e_cap:
-        raise ValueError("more data-flow edges than e_cap")
-    e = np.zeros((e_cap,), np.int32)
+    e = np.zeros((max(e_cap, len(edges)),), np.int32)
     e[:len(edges)] = edges
     meta = np.asarray([ni, int((pos != 1).sum()), nn, len(edges)], np.int32)
     return {"ids": ids[None], "pos": pos[None], "meta": meta[None], "spans": spans[None],
@@ -245,8 +243,16 @@ def graph_mask_from_compact(ids, meta, spans, edges) -> np.ndarray:
     return m
 
 
+def _pad_edges(arrays):
+    """Edge arrays of one width (zero-padded; meta[:, 3] says how many are real)."""
+    w = max(a.shape[1] for a in arrays)
+    return [a if a.shape[1] == w else np.pad(a, ((0, 0), (0, w - a.shape[1]))) for a in arrays]
+
+
 def _cat_compact(parts):
-    return {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
+    out = {k: np.concatenate([p[k] for p in parts]) for k in parts[0] if k != "edges"}
+    out["edges"] = np.concatenate(_pad_edges([p["edges"] for p in parts]))
+    return out
 
 
 class CompactGraphDataset:
@@ -321,6 +327,8 @@ def compact_pairs(c1: dict, c2_one: dict) -> CompactGraphDataset:
     out = {}
     for k in c1:
         a, b = c1[k], np.repeat(c2_one[k], n, axis=0)
+        if k == "edges":
+            a, b = _pad_edges([a, b])
         if a.shape[1:] != b.shape[1:]:
             raise ValueError(f"pair feature widths differ for {k}")
         out[k] = np.stack([a, b], 1).reshape((2 * n,) + a.shape[1:])

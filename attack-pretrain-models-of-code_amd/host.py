@@ -160,16 +160,23 @@ class Tokenizer:
         n, L = len(codes), code_length + data_flow_length
         e_cap = e_cap or 4 * L
         threads = threads or gcb_threads()
-        out = {"ids": np.empty((n, L), np.int32), "pos": np.empty((n, L), np.int32),
-               "meta": np.empty((n, 4), np.int32), "spans": np.empty((n, L), np.int32),
-               "edges": np.zeros((n, e_cap), np.int32)}
         flags = (1 if normalize else 0) | (2 if run_trunc else 0)
-        if n and self.lib.ah_gcb_features_batch(
-                self.h, n, _cstrs(codes), LANG[lang], variant, flags, code_length,
-                data_flow_length, e_cap, threads, *(_i32p(out[k]) for k in
-                                                    ("ids", "pos", "meta", "spans", "edges"))) < 0:
-            _err("ah_gcb_features_batch")
-        return out
+        strs = _cstrs(codes)
+        while True:
+            out = {"ids": np.empty((n, L), np.int32), "pos": np.empty((n, L), np.int32),
+                   "meta": np.empty((n, 4), np.int32), "spans": np.empty((n, L), np.int32),
+                   "edges": np.zeros((n, e_cap), np.int32)}
+            if not n or self.lib.ah_gcb_features_batch(
+                    self.h, n, strs, LANG[lang], variant, flags, code_length, data_flow_length,
+                    e_cap, threads, *(_i32p(out[k]) for k in
+                                      ("ids", "pos", "meta", "spans", "edges"))) >= 0:
+                return out
+            msg = _LIB.ah_last_error().decode(errors="replace")
+            # the reference has no edge limit: an edge-heavy query (long comesFrom lists) gets a
+            # wider edge array; every consumer pads widths when it joins batches
+            if "e_cap" not in msg or e_cap >= 64 * L:
+                _err("ah_gcb_features_batch")
+            e_cap *= 4
 
     def convert_tokens_to_ids(self, tokens):
         """tokenizer.convert_tokens_to_ids (a token string not in the vocabulary -> unk id)."""

@@ -134,7 +134,9 @@ int32_t ah_remove_comments(const char *code, char *out, int32_t cap);
  *   spans_out [n, L]                 node k's dfg_to_code span a | b << 16 if both < node_index,
  *                                    else -1 (entries past the node count are -1)
  *   edges_out [n, e_cap]             node | target << 16 of dfg_to_dfg (column inside L)
- * Returns n, or -1 (ah_last_error) e.g. when a query has more than e_cap edges. */
+ * Returns n, or -1 (ah_last_error) e.g. when a query has more than e_cap edges (the error text
+ * names e_cap; the caller retries with a wider edge array).  Concurrent calls on one tokenizer
+ * are serialised (the worker clones and their caches belong to the tokenizer). */
 #define AH_GCB_NORMALIZE 1
 #define AH_GCB_RUN_TRUNC 2
 int32_t ah_gcb_features_batch(ah_tokenizer *tok, int32_t n, const char *const *codes, int32_t lang,

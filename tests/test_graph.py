@@ -240,6 +240,51 @@ def test_batch_featuriser_matches_python_features(task, run_trunc):
         assert (m == m2).all(), i
 
 
+def edge_heavy_python():
+    """A program whose data-flow graph has far more node-to-node edges than 4 x L at small
+    code_length: 60 uses of a name defined in 24 if/elif branches (each use comes from all 24
+    definitions)."""
+    lines = ["def f(c):", "    if c == 0:", "        v = 0"]
+    for i in range(1, 24):
+        lines += [f"    elif c == {i}:", f"        v = {i}"]
+    return "\n".join(lines + ["    y = " + " + ".join(["v"] * 60), "    return y"])
+
+
+def test_edge_heavy_query_widens_edge_array():
+    """the reference has no edge limit, so a query with more data-flow edges than the
+    default edge capacity (4 x L) must not fail the batch: the featuriser retries with a wider
+    array, and the compact features still rebuild GraphCodeDataset's exact mask; joining such a
+    batch with ordinary ones pads the edge arrays."""
+    import _apmc  # noqa: F401
+    from apmc_amd.drivers import AttackArgs
+    from apmc_amd.graph import TASK_FEATURES, _cat_compact, convert_code_to_features, \
+        graph_mask, graph_mask_from_compact
+    from apmc_amd.host import Tokenizer
+
+    tok = Tokenizer()
+    lang, normalize, variant = TASK_FEATURES["authorship"]
+    cl, dfl = 32, 128
+    texts = [edge_heavy_python()] + _task_texts("authorship", 3)
+    c = tok.gcb_features(texts, lang, variant, normalize, cl, dfl)
+    assert c["meta"][0][3] > 4 * (cl + dfl) and c["edges"].shape[1] >= c["meta"][0][3]
+    args = AttackArgs(code_length=cl, data_flow_length=dfl)
+    for i, t in enumerate(texts):
+        f = convert_code_to_features(t, tok, 0, args, lang, normalize, variant=variant)
+        assert c["ids"][i].tolist() == f.input_ids, i
+        m = graph_mask(f.input_ids, f.position_idx, f.dfg_to_code, f.dfg_to_dfg)
+        assert (m == graph_mask_from_compact(c["ids"][i], c["meta"][i], c["spans"][i],
+                                             c["edges"][i])).all(), i
+    plain = tok.gcb_features(texts[1:], lang, variant, normalize, cl, dfl)
+    assert plain["edges"].shape[1] < c["edges"].shape[1]
+    joined = _cat_compact([plain, c])
+    assert joined["edges"].shape == (len(texts) + 3, c["edges"].shape[1])
+    for i in range(3):
+        assert (graph_mask_from_compact(joined["ids"][i], joined["meta"][i], joined["spans"][i],
+                                        joined["edges"][i]) ==
+                graph_mask_from_compact(plain["ids"][i], plain["meta"][i], plain["spans"][i],
+                                        plain["edges"][i])).all()
+
+
 @pytest.mark.gpu
 def test_device_graph_mask_matches_host(gpu):
     """ae_graph_mask (rowops.hip) builds exactly pack_mask(graph_mask) of every query, for the
@@ -258,8 +303,9 @@ def test_device_graph_mask_matches_host(gpu):
                  num_labels=1, shape=shape, precision="fp32")
     for task in ("devign", "clone", "authorship"):
         lang, normalize, variant = TASK_FEATURES[task]
-        for cl, dfl in ((512, 128), (64, 32)):
-            c = tok.gcb_features(_task_texts(task, 12), lang, variant, normalize, cl, dfl)
+        for cl, dfl in ((512, 128), (64, 32), (32, 128)):
+            texts = _task_texts(task, 12) + ([edge_heavy_python()] if task == "authorship" else [])
+            c = tok.gcb_features(texts, lang, variant, normalize, cl, dfl)
             t = {k: torch.from_numpy(v).cuda() for k, v in c.items()}
             bits = eng.graph_mask(t["ids"], t["meta"], t["spans"], t["edges"]).cpu().numpy()
             for i in range(len(c["ids"])):
