@@ -34,6 +34,10 @@ hipError_t ae_launch_attention_x3(const float*, float*, unsigned short*, const i
 hipError_t ae_launch_gemm_packed(const unsigned short*, const unsigned short*, const float*,
                                  const float*, float*, unsigned short*, int, int, int, int, int,
                                  hipStream_t);
+hipError_t ae_launch_gemm_packed_ln(const unsigned short*, const unsigned short*, const float*,
+                                    const float*, float*, unsigned short*, int, int, int, int,
+                                    const float*, const float*, float, uint64_t*, int*, int*,
+                                    hipStream_t);
 hipError_t ae_launch_compact(const int*, const int*, const int*, int, int, int, int, int*, int*,
                              int*, int*, hipStream_t);
 hipError_t ae_launch_embed_ln(const int*, const int*, const float*, const float*, const float*,
@@ -104,6 +108,10 @@ struct ae_engine {
   // packed bf16 activation planes of the split-precision path (gemm_planes.hip layout, np planes):
   // LN output, attention context, FFN1 output.  Allocated only when `planes` is on.
   unsigned short *xp = nullptr, *cp = nullptr, *hp = nullptr;
+  // row statistics and per-row-block counters of the fused residual + LayerNorm GEMM epilogue
+  // (gemm_planes.hip PK_EPI_RES_LN); the counters are zero between launches
+  uint64_t* lnst = nullptr;
+  int* lnctr = nullptr;
   bool planes = false;
   int np = 1;
   int *tok_ids = nullptr, *tok_pos = nullptr, *src_col = nullptr, *cu = nullptr, *one = nullptr;
@@ -216,9 +224,11 @@ int ensure_workspace(ae_engine* e, size_t T, size_t n) {
     HIPC(hipDeviceSynchronize());
     for (void* p : {(void*)e->x, (void*)e->qkv, (void*)e->ctx, (void*)e->tmp, (void*)e->h1,
                     (void*)e->tok_ids, (void*)e->tok_pos, (void*)e->src_col, (void*)e->xp,
-                    (void*)e->cp, (void*)e->hp})
+                    (void*)e->cp, (void*)e->hp, (void*)e->lnst, (void*)e->lnctr})
       dev_free(e, p);
     e->xp = e->cp = e->hp = nullptr;
+    e->lnst = nullptr;
+    e->lnctr = nullptr;
     int rc = 0;
     if ((rc = dev_alloc(e, (void**)&e->x, nt * H * 4))) return rc;
     if ((rc = dev_alloc(e, (void**)&e->qkv, nt * 3 * H * 4))) return rc;
@@ -232,6 +242,10 @@ int ensure_workspace(ae_engine* e, size_t T, size_t n) {
       if ((rc = dev_alloc(e, (void**)&e->xp, nt * H * 2 * e->np))) return rc;
       if ((rc = dev_alloc(e, (void**)&e->cp, nt * H * 2 * e->np))) return rc;
       if ((rc = dev_alloc(e, (void**)&e->hp, nt * F * 2 * e->np))) return rc;
+      const size_t blocks = (nt + 255) / 256;
+      if ((rc = dev_alloc(e, (void**)&e->lnst, blocks * 256 * 4 * 8))) return rc;
+      if ((rc = dev_alloc(e, (void**)&e->lnctr, 2 * blocks * 4))) return rc;
+      HIPC(hipMemset(e->lnctr, 0, 2 * blocks * 4));
     }
     e->cap_T = nt;
   }
@@ -327,6 +341,17 @@ int gemm_pk(ae_engine* e, const unsigned short* A, const unsigned short* Wp, con
   return AE_OK;
 }
 
+// The O-projection / FFN2 of the split-precision path with the layer's residual add and
+// LayerNorm fused into the epilogue: x = LN(A·W^T + bias + x), written as f32 and packed planes.
+int gemm_pk_ln(ae_engine* e, const unsigned short* A, const unsigned short* Wp, const float* bias,
+               const float* g, const float* b, int M, int K, hipStream_t st) {
+  const int H = e->cfg.hidden;
+  Prof p(e, st, e->prof_kind == AE_KIND_GEMM_ANY, 2.0 * M * H * K);
+  HIPC(ae_launch_gemm_packed_ln(A, Wp, bias, e->x, e->x, e->xp, M, H, K, e->np, g, b,
+                                e->cfg.ln_eps, e->lnst, e->lnctr, e->err, st));
+  return AE_OK;
+}
+
 // Runs the encoder over compacted tokens; on return the last-layer CLS rows are in e->xc
 // (cls_only) or all rows in e->x.
 int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint32_t* mask_bits,
@@ -367,17 +392,12 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
                                     mask_bits, L, e->np, st));
     }
     if (!last_cls && pl) {
-      if ((rc = gemm_pk(e, e->cp, w.wo_p, w.bo, e->x, e->tmp, nullptr, (int)T, H, H,
-                        EPI_BIAS_RESIDUAL, st, false)))
-        return rc;
-      HIPC(ae_launch_layernorm(e->tmp, w.ln1g, w.ln1b, eps, (int)T, e->x, e->xp, e->np, st));
+      // O-proj + residual + LN1 and FFN2 + residual + LN2 each one kernel (x updated in place)
+      if ((rc = gemm_pk_ln(e, e->cp, w.wo_p, w.bo, w.ln1g, w.ln1b, (int)T, H, st))) return rc;
       if ((rc = gemm_pk(e, e->xp, w.w1_p, w.b1, nullptr, nullptr, e->hp, (int)T, F, H,
                         EPI_BIAS_GELU, st, true)))
         return rc;
-      if ((rc = gemm_pk(e, e->hp, w.w2_p, w.b2, e->x, e->tmp, nullptr, (int)T, H, F,
-                        EPI_BIAS_RESIDUAL, st, false)))
-        return rc;
-      HIPC(ae_launch_layernorm(e->tmp, w.ln2g, w.ln2b, eps, (int)T, e->x, e->xp, e->np, st));
+      if ((rc = gemm_pk_ln(e, e->hp, w.w2_p, w.b2, w.ln2g, w.ln2b, (int)T, F, st))) return rc;
     } else if (!last_cls) {
       if ((rc = gemm(e, e->ctx, w.wo, w.wo_h, w.wo_l, w.bo, e->x, e->tmp, (int)T, H, H, EPI_BIAS_RESIDUAL,
                      st, false)))

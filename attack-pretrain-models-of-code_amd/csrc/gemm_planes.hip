@@ -42,7 +42,27 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // PK_EPI_BIAS_PACKED: +bias -> packed planes (the QKV output feeding attention_pp.hip); only the
 // ping-pong 256 x 256 kernel has it
-enum { PK_EPI_BIAS = 0, PK_EPI_GELU_PACKED = 1, PK_EPI_RES = 2, PK_EPI_TANH = 3, PK_EPI_BIAS_PACKED = 4 };
+// PK_EPI_RES_LN: +bias +residual -> LayerNorm over the whole 768-wide row -> f32 + packed planes
+// (the O-projection / FFN2 + LayerNorm of every encoder layer; 256 x 192 kernel only, see below)
+enum { PK_EPI_BIAS = 0, PK_EPI_GELU_PACKED = 1, PK_EPI_RES = 2, PK_EPI_TANH = 3, PK_EPI_BIAS_PACKED = 4,
+       PK_EPI_RES_LN = 5 };
+
+// (mean, M2) of a row segment: M2 = sum of squared deviations from the segment mean
+struct RowStat {
+  float mean, m2;
+};
+
+// Arguments of the fused residual + LayerNorm epilogue (PK_EPI_RES_LN).
+struct LnArgs {
+  const float* gamma;
+  const float* beta;
+  float eps;
+  __bf16* xp;        // packed planes of the LayerNorm output ([M][NP * N])
+  uint64_t* stats;   // [tiles_m * 256][4] (mean, M2) of each row over each 192-column tile
+  int* arrive;       // [tiles_m] arrivals per 256-row block (self-resetting, zero between launches)
+  int* depart;       // [tiles_m]
+  int* err;          // set to 2 if a row block's partners never arrived (bounded wait)
+};
 
 namespace {
 constexpr int PK_BM = 256, PK_ROWB = 128;
@@ -739,7 +759,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
 template <int NP, int EPI, bool NT = false>
 __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
     const __bf16* __restrict__ A, const __bf16* __restrict__ W, const float* __restrict__ bias,
-    const float* __restrict__ R, float* __restrict__ C, int M, int N, int K, int group_m) {
+    const float* R, float* C, int M, int N, int K, int group_m, LnArgs ln) {
   extern __shared__ __attribute__((aligned(16))) unsigned char pk_smem[];
   constexpr int BM = 256, BN = 192, ROWB = PK_ROWB;
   constexpr int A_BYTES = BM * ROWB, STAGE = (BM + BN) * ROWB;  // 56 KiB per K-tile
@@ -747,11 +767,24 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
 
   const int tiles_n = (N + BN - 1) / BN;
   const int tiles_m = (M + BM - 1) / BM;
-  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int per_group = group_m * tiles_n;
-  const int g = t / per_group, first_m = g * group_m;
-  const int gsize = min(tiles_m - first_m, group_m);
-  const int tm0 = first_m + (t - g * per_group) % gsize, tn0 = (t - g * per_group) / gsize;
+  int tm0, tn0;
+  if constexpr (EPI == PK_EPI_RES_LN) {
+    // The 4 N-tiles of a 256-row block exchange row statistics, so they must be co-resident:
+    // blocks b, b+8, b+16, b+24 (one XCD, consecutive in its in-order dispatch) take the row
+    // block's 4 tiles; the XCDs interleave row blocks.  Grid = 32 * ceil(tiles_m / 8); blocks
+    // past the last row block leave before any exchange (all four partners of one do).
+    const int k = blockIdx.x >> 3;
+    tn0 = k & 3;
+    tm0 = (k >> 2) * 8 + (blockIdx.x & 7);
+    if (tm0 >= tiles_m) return;
+  } else {
+    const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+    const int per_group = group_m * tiles_n;
+    const int g = t / per_group, first_m = g * group_m;
+    const int gsize = min(tiles_m - first_m, group_m);
+    tm0 = first_m + (t - g * per_group) % gsize;
+    tn0 = (t - g * per_group) / gsize;
+  }
   const int m0 = tm0 * BM, n0 = tn0 * BN;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -896,6 +929,156 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
   }
   if (wm == 0) sync_load();  // same barrier count in both groups; every LDS read and DMA done
 
+  if constexpr (EPI == PK_EPI_RES_LN) {
+    // ---- fused residual + LayerNorm (rowops.hip layernorm_kernel's formula over the 768-wide
+    // row, whose 4 x 192 columns live in the 4 partner workgroups of this row block).
+    // acc[tm][tn] register 4 j + i of lane l = row wm*128 + sm*64 + tm*32 + (l & 31), column
+    // sn*96 + tn*32 + 8 j + 4 (l >> 5) + i of the tile (the transposed MFMA product).
+    const int cb0 = n0 + sn * 96;
+    const int rb0 = m0 + wm * 128 + sm * 64 + li;  // + 32 tm
+    // (1) v = (acc + bias) + residual, in place (R may alias C: each element is read here
+    // before this lane writes it, and no other workgroup touches this tile)
+#pragma unroll
+    for (int tn = 0; tn < 3; ++tn)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = cb0 + tn * 32 + 8 * j + 4 * lh;
+        const floatx4 bv = *reinterpret_cast<const floatx4*>(bias + col);
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm) {
+          const int row = rb0 + 32 * tm;
+          const floatx4 rv = row < M ? *reinterpret_cast<const floatx4*>(R + (size_t)row * N + col)
+                                     : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[tm][tn][4 * j + i] = (acc[tm][tn][4 * j + i] + bv[i]) + rv[i];
+        }
+      }
+    // (2) per row over the wave's 96 columns: mean and M2 (sum of squared deviations); the two
+    // lane halves hold 48 columns each
+    float mean96[2], m2_96[2];
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm) {
+      float sum = 0.f;
+#pragma unroll
+      for (int tn = 0; tn < 3; ++tn)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sum += acc[tm][tn][r];
+      sum += __shfl_xor(sum, 32, 64);
+      const float mu = sum * (1.f / 96.f);
+      float q = 0.f;
+#pragma unroll
+      for (int tn = 0; tn < 3; ++tn)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float d = acc[tm][tn][r] - mu;
+          q += d * d;
+        }
+      q += __shfl_xor(q, 32, 64);
+      mean96[tm] = mu;
+      m2_96[tm] = q;
+    }
+    // (3) the two waves of a row (sn = 0, 1) combine through LDS (Chan's pairwise merge, n = 96
+    // each, always in sn order so both get the same bits)
+    RowStat* lst = reinterpret_cast<RowStat*>(pk_smem);  // [8 waves][2 tm][32 rows]
+    if (lh == 0) {
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm) lst[(wave * 2 + tm) * 32 + li] = RowStat{mean96[tm], m2_96[tm]};
+    }
+    __syncthreads();
+    RowStat tile[2];
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm) {
+      const RowStat o = lst[((wave ^ 1) * 2 + tm) * 32 + li];
+      const RowStat mine{mean96[tm], m2_96[tm]};
+      const RowStat a = sn == 0 ? mine : o;
+      const RowStat b = sn == 0 ? o : mine;
+      const float d = a.mean - b.mean;
+      tile[tm] = RowStat{(a.mean + b.mean) * 0.5f, (a.m2 + b.m2) + 48.f * d * d};
+    }
+    // (4) publish this tile's (mean, M2) of its 256 rows; one lane signals for the workgroup
+    // after every wave's stores have completed (agent-scope 8-B stores / loads, L2-coherent:
+    // the partners share this XCD's L2, and the loads skip the CU's L1)
+    if (sn == 0 && lh == 0) {
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+        __hip_atomic_store(ln.stats + ((size_t)(rb0 + 32 * tm) * 4 + tn0),
+                           __builtin_bit_cast(uint64_t, tile[tm]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __hip_atomic_fetch_add(ln.arrive + tm0, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // bounded wait (~1 s): a partner that never arrives flags the engine instead of hanging
+      int ok = 0;
+      for (int spin = 0; spin < (1 << 20); ++spin) {
+        if (__hip_atomic_load(ln.arrive + tm0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= tiles_n) {
+          ok = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      if (!ok) __hip_atomic_store(ln.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    // (5) the row's statistics over all 768 columns: merge the 4 tiles ((0,1), (2,3), then the
+    // halves), the same order in every workgroup and wave
+    float mean[2], rstd[2];
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm) {
+      RowStat p[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        p[q] = __builtin_bit_cast(RowStat, __hip_atomic_load(ln.stats + (size_t)(rb0 + 32 * tm) * 4 + q,
+                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      const float d01 = p[0].mean - p[1].mean, d23 = p[2].mean - p[3].mean;
+      const float m01 = (p[0].mean + p[1].mean) * 0.5f, m23 = (p[2].mean + p[3].mean) * 0.5f;
+      const float q01 = (p[0].m2 + p[1].m2) + 96.f * d01 * d01;
+      const float q23 = (p[2].m2 + p[3].m2) + 96.f * d23 * d23;
+      const float d = m01 - m23;
+      mean[tm] = (m01 + m23) * 0.5f;
+      const float var = ((q01 + q23) + 192.f * d * d) * (1.f / 768.f);
+      rstd[tm] = rsqrtf(var + ln.eps);
+    }
+    __syncthreads();  // every wave has read the statistics
+    if (tid == 0) {
+      // the last of the 4 partners to leave re-arms the counters for the next launch
+      if (__hip_atomic_fetch_add(ln.depart + tm0, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+          tiles_n - 1) {
+        __hip_atomic_store(ln.arrive + tm0, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ln.depart + tm0, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    // (6) normalise in registers; write x (f32) and its packed planes
+#pragma unroll
+    for (int tn = 0; tn < 3; ++tn)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = cb0 + tn * 32 + 8 * j + 4 * lh;
+        const floatx4 gg = *reinterpret_cast<const floatx4*>(ln.gamma + col);
+        const floatx4 bb = *reinterpret_cast<const floatx4*>(ln.beta + col);
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm) {
+          const int row = rb0 + 32 * tm;
+          if (row >= M) continue;
+          floatx4 o;
+          ushortx4 h, l;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            o[i] = (acc[tm][tn][4 * j + i] - mean[tm]) * rstd[tm] * gg[i] + bb[i];
+            h[i] = f2bf(o[i]);
+            l[i] = f2bf(o[i] - __builtin_bit_cast(float, (uint32_t)h[i] << 16));
+          }
+          *reinterpret_cast<floatx4*>(C + (size_t)row * N + col) = o;
+          unsigned short* dst = reinterpret_cast<unsigned short*>(ln.xp) + (size_t)row * NP * N +
+                                (size_t)(col >> 5) * 32 * NP + (col & 31);
+          *reinterpret_cast<ushortx4*>(dst) = h;
+          if (NP == 2) *reinterpret_cast<ushortx4*>(dst + 32) = l;
+        }
+      }
+    return;
+  }
+
   // ---- epilogue: per 32-row pass (tm), the wave's 32 x 96 f32 block goes to its LDS region
   // (rows of 400 B: 384 + 16 pad, so 16 lanes of different rows hit 16 different bank slots),
   // then whole 384-B row segments go out with 16-B lanes (+ bias, tanh / residual)
@@ -974,13 +1157,15 @@ hipError_t pp_epi(int epi, const __bf16* A, const __bf16* W, const float* bias, 
 
 template <int NP, int EPI, bool NT = false>
 hipError_t pp192_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R,
-                        float* C, int M, int N, int K, int group_m, hipStream_t st) {
+                        float* C, int M, int N, int K, int group_m, hipStream_t st,
+                        LnArgs ln = LnArgs{}) {
   constexpr int lds = 2 * (256 + 192) * PK_ROWB;  // 112 KiB
   if (hipError_t e = ensure_dynamic_lds((const void*)gemm_pp192_kernel<NP, EPI, NT>, lds); e != hipSuccess)
     return e;
-  const int tiles = ((M + 255) / 256) * ((N + 191) / 192);
+  const int tiles_m = (M + 255) / 256;
+  const int tiles = EPI == PK_EPI_RES_LN ? 32 * ((tiles_m + 7) / 8) : tiles_m * ((N + 191) / 192);
   hipLaunchKernelGGL((gemm_pp192_kernel<NP, EPI, NT>), dim3(tiles), dim3(512), lds, st, A, W, bias, R,
-                     C, M, N, K, group_m);
+                     C, M, N, K, group_m, ln);
   return hipGetLastError();
 }
 
@@ -1119,6 +1304,28 @@ extern "C" hipError_t ae_launch_gemm_packed(const unsigned short* A, const unsig
              : pp_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
 }
 
+
+// C = LayerNorm(A·W^T + bias + R) over rows of N = 768 (the O-projection / FFN2 + LayerNorm of an
+// encoder layer), written as f32 C [M][768] and packed planes Cp [M][np*768]; R may equal C.
+// stats: [(M + 255) / 256 * 256][4] 8-B words; ctr: 2 * ((M + 255) / 256) ints, zero on the first
+// call (the kernel leaves them zero); err: the engine's device error word.
+extern "C" hipError_t ae_launch_gemm_packed_ln(const unsigned short* A, const unsigned short* W,
+                                               const float* bias, const float* R, float* C,
+                                               unsigned short* Cp, int M, int N, int K, int np,
+                                               const float* gamma, const float* beta, float eps,
+                                               uint64_t* stats, int* ctr, int* err,
+                                               hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  if (N != 768 || K % 64 != 0 || (np != 1 && np != 2) || !bias || !R || !C || !Cp || !gamma ||
+      !beta || !stats || !ctr || !err)
+    return hipErrorInvalidValue;
+  const int tiles_m = (M + 255) / 256;
+  LnArgs ln{gamma, beta, eps, reinterpret_cast<__bf16*>(Cp), stats, ctr, ctr + tiles_m, err};
+  auto a = reinterpret_cast<const __bf16*>(A);
+  auto w = reinterpret_cast<const __bf16*>(W);
+  if (np == 2) return pp192_launch<2, PK_EPI_RES_LN>(a, w, bias, R, C, M, N, K, PK_GROUP_M, st, ln);
+  return pp192_launch<1, PK_EPI_RES_LN>(a, w, bias, R, C, M, N, K, PK_GROUP_M, st, ln);
+}
 
 // Kernel experiments (tools/gemm_bench.py, tests): explicit tile width (0 = the production choice)
 // and a diagnostic variant (0 = the production kernel; see DIAG above — values 1-7 give WRONG

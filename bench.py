@@ -55,9 +55,10 @@ def parse_args():
     ap.add_argument("--precision", default="f32x3", choices=["fp32", "f32x3", "bf16"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="CPU scoring microbenchmark budget (cpu_baseline)")
-    ap.add_argument("--cpu-e2e-seconds", type=float, default=360.0,
-                    help="cap (s) of the CPU config-1 greedy attack (config1.cpu); the run "
-                         "normally completes all 16 functions well inside it")
+    ap.add_argument("--cpu-e2e-seconds", type=float, default=60.0,
+                    help="cap (s) of the CPU config-1 greedy attack (config1.cpu); all 16 "
+                         "functions take ~10 min on the box's cores (run once with a larger cap: "
+                         "profiles/r3d_config1_cpu_complete.jsonl)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--attack-examples", type=int, default=400,
                     help="examples of test_subs_0_400 in the config-2 GA attack leg (0 disables)")
@@ -658,6 +659,26 @@ def main():
     eng.close()
     threads, cpu_facts = host_cores()
     log(f"scoring step: {value:.1f} q/s")
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the CPU reference path on this host, at the job's CPU share and at one thread per
+        # physical core of the affinity (on a shared 8-GPU host the latter can be SLOWER: the
+        # other jobs' load); the best point is the baseline, every point is reported
+        sweep = sorted({t for t in (cpu_facts.get("job_share_threads"), threads // 2, threads)
+                        if t})
+        points = []
+        for t in sweep:
+            log(f"CPU baseline ({t} threads)")
+            v, sample = cpu_baseline(L, args.cpu_seconds, t)
+            points.append({"cores": t, "value": round(v, 4), "sample": sample})
+        best = max(points, key=lambda q: q["value"])
+        threads = best["cores"]
+        res["cpu_baseline"] = {"value": best["value"], "unit": "victim queries/s",
+                               "cores": best["cores"], "kind": "port",
+                               "sample": best["sample"] + f", oracle/roberta_cpu.py fp32 eager, "
+                                                          f"torch threads={best['cores']} (the "
+                                                          "fastest point of the sweep)",
+                               "thread_sweep": points, **cpu_facts}
+        res["speedup_vs_cpu"] = round(value / best["value"], 2)
     if args.attack_examples > 0:
         log("config-2 attack leg")
         res["attack"] = attack_leg(dev, args.attack_examples, args.attack_deadline,
@@ -680,20 +701,6 @@ def main():
         log("MHM-NS leg")
         res["mhm"] = mhm_leg(dev, args.mhm_examples, args.mhm_seq_examples, rank, world,
                              args.precision)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        log(f"CPU baseline ({threads} threads)")
-        v, sample = cpu_baseline(L, args.cpu_seconds, threads)
-        res["cpu_baseline"] = {"value": v, "unit": "victim queries/s", "cores": threads,
-                               "kind": "port",
-                               "sample": sample + f", oracle/roberta_cpu.py fp32 eager, torch "
-                                                  f"threads={threads} = one per physical core "
-                                                  f"of this process's CPU affinity",
-                               **cpu_facts}
-        share = cpu_facts.get("job_share_threads")
-        if share and share < threads:
-            v16, s16 = cpu_baseline(L, args.cpu_seconds, share)
-            res["cpu_baseline"]["job_share"] = {"value": v16, "cores": share, "sample": s16}
-        res["speedup_vs_cpu"] = round(value / v, 2)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if dist is not None:

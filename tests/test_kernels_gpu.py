@@ -255,3 +255,60 @@ def test_attention_pp_matches_f64(gpu, np_, case, variant):
     assert torch.isfinite(got).all()
     err = (got - ref).abs()
     assert (err <= tol).all(), float(err.max())
+
+
+@pytest.mark.parametrize("M,K,np_", [(300, 768, 2), (512, 3072, 2), (1000, 768, 1), (37, 768, 2),
+                                     (4097, 768, 2)])
+def test_gemm_packed_ln_matches_f64(gpu, M, K, np_):
+    """ae_launch_gemm_packed_ln (256 x 192 kernel, PK_EPI_RES_LN): x = LayerNorm(A·W^T + bias + x)
+    over 768-wide rows whose 4 column tiles live in 4 workgroups that exchange row statistics.
+    Against float64 of the split products; the residual aliases the output (in place, as the
+    engine runs it); three launches in a row reuse the self-resetting row-block counters (a
+    counter left non-zero would make a later launch read stale statistics or time out)."""
+    lib = _lib()
+    vp, i32 = ctypes.c_void_p, ctypes.c_int32
+    lib.ae_launch_gemm_packed_ln.argtypes = [vp] * 6 + [i32] * 4 + [vp, vp, ctypes.c_float] + \
+        [vp] * 4
+    lib.ae_launch_gemm_packed_ln.restype = ctypes.c_int
+    N = 768
+    g = torch.Generator().manual_seed(M + K)
+    W = torch.randn(N, K, generator=g) * 0.05
+    bias = torch.randn(N, generator=g) * 0.5
+    gamma = 1.0 + 0.1 * torch.randn(N, generator=g)
+    beta = 0.1 * torch.randn(N, generator=g)
+    Wh, Wl = _split(W)
+    dW = _pack(Wh, Wl, np_).cuda()
+    blocks = (M + 255) // 256
+    stats = torch.zeros(blocks * 256 * 4, dtype=torch.int64, device="cuda")
+    ctr = torch.zeros(2 * blocks, dtype=torch.int32, device="cuda")
+    err = torch.zeros(4, dtype=torch.int32, device="cuda")
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for it in range(3):
+        A = torch.randn(M, K, generator=g) * 0.7
+        X = torch.randn(M, N, generator=g) * 2.0 + 0.5
+        Ah, Al = _split(A)
+        y = Ah.double() @ Wh.double().T
+        if np_ == 2:
+            y = y + Ah.double() @ Wl.double().T + Al.double() @ Wh.double().T
+        y = y + bias.double() + X.double()
+        mu = y.mean(1, keepdim=True)
+        var = ((y - mu) ** 2).mean(1, keepdim=True)
+        ref = (y - mu) / torch.sqrt(var + 1e-5) * gamma.double() + beta.double()
+        scale = (A.abs().double() @ W.abs().double().T).amax(1, keepdim=True)
+        dA = _pack(Ah, Al, np_).cuda()
+        x = X.cuda()
+        xp = torch.zeros((M, np_ * N), dtype=torch.bfloat16, device="cuda")
+        rc = lib.ae_launch_gemm_packed_ln(_p(dA), _p(dW), _p(bias.cuda()), _p(x), _p(x), _p(xp),
+                                          M, N, K, np_, _p(gamma.cuda()), _p(beta.cuda()), 1e-5,
+                                          _p(stats), _p(ctr), _p(err), st)
+        assert rc == 0
+        torch.cuda.synchronize()
+        assert int(err[0]) == 0 and int(ctr.abs().sum()) == 0, it
+        got = x.double().cpu()
+        # LN amplifies the GEMM's f32-accumulation error by rstd * gamma
+        tol = (1e-5 * scale + 1e-6) * 1.2 / torch.sqrt(var + 1e-5) + 2e-6
+        assert torch.isfinite(got).all()
+        assert ((got - ref).abs() <= tol).all(), (it, float(((got - ref).abs() - tol).max()))
+        planes = _unpack(xp.cpu(), np_, N)
+        rel = 2e-5 if np_ == 2 else 5e-3
+        assert ((planes - got).abs() <= rel * got.abs() + 1e-7).all(), it
