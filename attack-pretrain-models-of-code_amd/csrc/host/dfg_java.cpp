@@ -313,6 +313,23 @@ class JTree {
       name = r;
       typed = true;
     }
+    if (!typed && q == 0) {
+      // a constructor with no modifier (`Name(T p) throws E {`): tree-sitter recovers it as a
+      // call — its parameters are plain leaves, not definitions — and the first exception type
+      // of `throws` as a declared name (the BigCloneBench fixture keys of `HttpRepository`)
+      leaves_to(root, name + 1);
+      leaves_to(root, close_of(p_) + 1);
+      if (at("throws") && is_ident(t(p_ + 1))) {
+        add_leaf(root, p_++);
+        const int lvd0 = make(J_LVD);
+        attach(root, lvd0);
+        const int d = make(J_DECLARATOR);
+        attach(lvd0, d);
+        nodes[d].a = add_leaf(d, p_++);
+      }
+      while (more() && !at("{") && !at(";")) add_leaf(root, p_++);
+      return;
+    }
     int lvd = -1;
     if (typed) {
       lvd = make(J_LVD);

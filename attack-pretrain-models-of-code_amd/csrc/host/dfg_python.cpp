@@ -775,7 +775,9 @@ class PyTree {
     const int g = make(P_GENERIC);
     add_leaf(g, p_++);
     limited(close, [&] {
-      if (find0("for") < lim_ && find0(",") == lim_) {  // f(x for x in y)
+      // f(x for x in y) and f(x for x, y in z): the first depth-0 `for` comes before any
+      // depth-0 comma (a comma before it makes an argument list)
+      if (find0("for") < lim_ && find0("for") < find0(",")) {
         attach(g, expression());
         comprehension_clauses(g);
       }

@@ -329,14 +329,14 @@ def key_parity(task):
 
 
 def test_dfg_java_python_vs_reference_fixture_keys():
-    """DFG_java / DFG_python (dfg_java.cpp, dfg_python.cpp) against the reference's own keys.
-    Measured (DESIGN.md §5 lists the residue by cause): Java on all 4000 BigCloneBench fixtures
-    85.3% exact / 96.0% truncation-consistent / 97.8% subsequence; the 500 in data/ and the 132
-    authorship programs are asserted here."""
+    """DFG_java / DFG_python (dfg_java.cpp, dfg_python.cpp) against the reference's own keys, at
+    the measured counts (DESIGN.md §5 classifies every remaining function by cause): Java 433 /
+    477 / 488 of the 500 BigCloneBench code1 in data/ exact / truncation-consistent / ordered
+    subsequence, Python 71 / 128 / 130 of the 132 authorship programs."""
     e, c, s, t = key_parity("clone")
-    assert t == 500 and e / t >= 0.84 and c / t >= 0.95 and s / t >= 0.96, (e, c, s, t)
+    assert t == 500 and e >= 433 and c >= 477 and s >= 488, (e, c, s, t)
     e, c, s, t = key_parity("authorship")
-    assert t == 132 and e / t >= 0.53 and c / t >= 0.96 and s / t >= 0.97, (e, c, s, t)
+    assert t == 132 and e >= 71 and c >= 128 and s >= 130, (e, c, s, t)
 
 
 def _names(code, lang):
