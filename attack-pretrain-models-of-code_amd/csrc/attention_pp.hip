@@ -26,6 +26,9 @@
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 constexpr int QPB = 128, KT = 32, OSTRIDE = 65;
@@ -70,11 +73,20 @@ __device__ __forceinline__ int vpos(int r, int x) {
 }
 }  // namespace
 
-// PIPE: software-pipelined loop — the S MFMAs of key tile kt + 1 issue in the same scheduling
+// PIPE 1: software-pipelined loop — the S MFMAs of key tile kt + 1 issue in the same scheduling
 // region as the exp / P-split VALU of tile kt (independent streams the SIMD co-issues), K and V in
 // separate 2-slot rings (K two tiles ahead, V one).
-template <int NP, bool HAS_MASK, bool PLANES, bool PIPE>
-__global__ __launch_bounds__(256, 2) void attn_pp_kernel(const unsigned short* __restrict__ qkvp,
+// PIPE 4 (production): PIPE 1 with the O rescale unconditional, so no branch splits the region
+// and tile kt's exp / P split really sits beside tile kt+1's S MFMAs, interleaved by
+// sched_group_barrier (K reads, then one MFMA per five vector instructions).
+// PIPE 2: PIPE 4 with fewer vector instructions per tile and nothing between the two streams:
+// the O rescale is unconditional (no branch splits the region, so the exp / split really sits
+// beside the next tile's S MFMAs, interleaved by sched_group_barrier), the tile max by 3-input
+// max, and the exp / P split on packed f32 pairs with P's hi plane the TRUNCATED bf16 of p (its
+// upper 16 bits, one shift-or per pair) and lo = bf16(p - hi), exact to 2^-16 of p as the
+// rounded split.
+template <int NP, bool HAS_MASK, bool PLANES, int PIPE>
+__global__ __launch_bounds__(256, PIPE == 5 ? 3 : 2) void attn_pp_kernel(const unsigned short* __restrict__ qkvp,
                                                          float* __restrict__ out,
                                                          unsigned short* __restrict__ op,
                                                          const int* __restrict__ cu,
@@ -159,7 +171,7 @@ __global__ __launch_bounds__(256, 2) void attn_pp_kernel(const unsigned short* _
     float mt = -INFINITY;
     if (!HAS_MASK && (kt + 1) * KT <= len) {  // full tile, no mask: no per-key select
 #pragma unroll
-      for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[r]);
+      for (int r = 0; r < 16; r += 2) mt = fmaxf(mt, fmaxf(s[r], s[r + 1]));
     } else {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -187,6 +199,33 @@ __global__ __launch_bounds__(256, 2) void attn_pp_kernel(const unsigned short* _
       pl[r >> 3][r & 7] = (__bf16)(p - (float)h);
     }
     return psum;
+  };
+  // PIPE 2's exp / split: packed pairs, truncated hi (see above)
+  auto exp_split2 = [&](floatx16& s, float m_new, bf16x8 (&ph)[2], bf16x8 (&pl)[2]) {
+    floatx2 acc2 = {0.f, 0.f};
+    const floatx2 mm = {m_new, m_new};
+    u32x4 hw[2], lw[2];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const floatx2 d = floatx2{s[2 * q], s[2 * q + 1]} - mm;
+      // (scalar copies: __builtin_bit_cast of an ext_vector ELEMENT reads element 0 — a clang
+      // lowering hazard this loop hit, every pair's second hi plane was its first's)
+      const float px = __builtin_amdgcn_exp2f(d.x), py = __builtin_amdgcn_exp2f(d.y);
+      acc2 += floatx2{px, py};
+      const uint32_t b0 = __builtin_bit_cast(uint32_t, px) & 0xffff0000u;
+      const uint32_t b1 = __builtin_bit_cast(uint32_t, py) & 0xffff0000u;
+      const float lx = px - __builtin_bit_cast(float, b0);
+      const float ly = py - __builtin_bit_cast(float, b1);
+      hw[q >> 2][q & 3] = (b0 >> 16) | b1;  // [hi(p.x) | hi(p.y) << 16]
+      const bf16x2 l2 = {(__bf16)lx, (__bf16)ly};
+      lw[q >> 2][q & 3] = __builtin_bit_cast(uint32_t, l2);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      ph[t] = __builtin_bit_cast(bf16x8, hw[t]);
+      pl[t] = __builtin_bit_cast(bf16x8, lw[t]);
+    }
+    return acc2.x + acc2.y;
   };
   // O^T += V^T P^T (2 k-steps of 16 keys, 2 d-tiles).  P^T straight from the S accumulator:
   // registers 8t..8t+7 of lane half h hold keys 16t + 4h + {0..3} and 16t + 8 + 4h + {0..3};
@@ -238,7 +277,7 @@ __global__ __launch_bounds__(256, 2) void attn_pp_kernel(const unsigned short* _
   };
 
   const int nkt = (len + KT - 1) / KT;
-  if (!PIPE) {
+  if (PIPE == 0) {
     // stage b = [K | V] of one tile, two stages
     issue1(0, AE_HIDDEN, lds0, false);
     issue1(0, 2 * AE_HIDDEN, lds0 + P::TILE, true);
@@ -290,11 +329,34 @@ __global__ __launch_bounds__(256, 2) void attn_pp_kernel(const unsigned short* _
       // one scheduling region: tile kt's exp / split on the VALU, tile kt + 1's S on the MFMA
       // (the last iteration's S of a tile past the end reads a stale slot and is discarded;
       // unconditional so the region has no branch)
-      const float psum = exp_split(s_cur, m_new, ph, pl);
-      s_mfma(lds + kslot(kt + 1), s_next);
+      float psum;
+      if constexpr (PIPE >= 2) {
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (PIPE >= 4) psum = exp_split(s_cur, m_new, ph, pl);
+        else psum = exp_split2(s_cur, m_new, ph, pl);
+        s_mfma(lds + kslot(kt + 1), s_next);
+        if constexpr (PIPE != 3) {
+          // the K fragment reads first, then one S MFMA per few vector instructions
+          __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+          for (int i = 0; i < 12; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+        psum = exp_split(s_cur, m_new, ph, pl);
+        s_mfma(lds + kslot(kt + 1), s_next);
+      }
       l_run = l_run * alpha + psum;
       m_run = m_new;
-      rescale(alpha);
+      if constexpr (PIPE >= 2) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+      } else {
+        rescale(alpha);
+      }
       pv_mfma(lds + vslot(kt), ph, pl);
       s_cur = s_next;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -332,7 +394,7 @@ __global__ __launch_bounds__(256, 2) void attn_pp_kernel(const unsigned short* _
 // qkvp: packed planes [T][np·2304] with Q pre-scaled by log2(e)/8; context to op (packed planes)
 // or out (f32 [T, 768]).  q_rows / max_q: the CLS-only launch of the last layer.
 namespace {
-template <bool PIPE>
+template <int PIPE>
 hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op, const int* cu,
                       const int* q_rows, int max_q, int n, int heads, const uint32_t* mask,
                       int mask_L, int np, hipStream_t stream) {
@@ -357,7 +419,10 @@ hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op
 #undef APP_LAUNCH
   return hipGetLastError();
 }
-constexpr bool APP_PIPE = true;  // production loop (tools/attn_bench.py A/B: pp1 190 us vs pp 203 us)
+// production loop: PIPE 4 (tools/attn_bench.py, B=64 x L=512, same box, interleaved rounds:
+// pp1 197.0 / pp4 192.6 us median, ragged 129.1 / 126.5; profiles/r3i_attn_ab.jsonl).  PIPE 2-3
+// (packed split) and 5 (3 workgroups per CU) measured no better than 4.
+constexpr int APP_PIPE = 4;
 }  // namespace
 
 extern "C" hipError_t ae_launch_attention_pp(const unsigned short* qkvp, float* out,
@@ -368,16 +433,27 @@ extern "C" hipError_t ae_launch_attention_pp(const unsigned short* qkvp, float* 
                               stream);
 }
 
-// Kernel experiments (tools/attn_bench.py, tests): variant 0 = two-stage loop, 1 = pipelined.
+// Kernel experiments (tools/attn_bench.py, tests): variant 0 = two-stage loop, 1 = pipelined,
+// 2 = pipelined with the packed / branch-free tile (PIPE 2 above), 3 = 2 without the
+// interleave hints, 4 = the production loop (rounded split, branch-free rescale, interleave
+// hints), 5 = 4 at three workgroups per CU.
 // (An XCD-aware workgroup order — the q-blocks of one (sequence, head) on one XCD — measured 2-3 %
 // slower, profiles/r2i_attn_pp_ab.jsonl: the K/V re-reads are Infinity-Cache hits, not the bound.)
 extern "C" hipError_t ae_bench_attention_pp(const unsigned short* qkvp, float* out,
                                             unsigned short* op, const int* cu, const int* q_rows,
                                             int max_q, int n, int heads, const uint32_t* mask,
                                             int mask_L, int np, int variant, hipStream_t stream) {
+  if (variant == 5)
+    return app_launch<5>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
+  if (variant == 4)
+    return app_launch<4>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
+  if (variant == 3)
+    return app_launch<3>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
+  if (variant == 2)
+    return app_launch<2>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
   if (variant == 1)
-    return app_launch<true>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
+    return app_launch<1>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
   if (variant == 0)
-    return app_launch<false>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
+    return app_launch<0>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
   return hipErrorInvalidValue;
 }

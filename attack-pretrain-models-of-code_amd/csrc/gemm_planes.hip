@@ -62,6 +62,10 @@ struct LnArgs {
   int* arrive;       // [tiles_m] arrivals per 256-row block (self-resetting, zero between launches)
   int* depart;       // [tiles_m]
   int* err;          // set to 2 if a row block's partners never arrived (bounded wait)
+  int mode;          // 0 = production; timing experiments (results WRONG for 1): 1 = no exchange
+                     // (each tile normalises with its own 192 columns' statistics), 2 = the
+                     // grouped XCD tile order of the other epilogues (partners may straddle two
+                     // XCDs when tiles_m % 32 != 0), 3 = row blocks interleaved over the XCDs
 };
 
 namespace {
@@ -768,16 +772,18 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
   const int tiles_n = (N + BN - 1) / BN;
   const int tiles_m = (M + BM - 1) / BM;
   int tm0, tn0;
-  if constexpr (EPI == PK_EPI_RES_LN) {
+  if (EPI == PK_EPI_RES_LN && ln.mode != 2) {
     // The 4 N-tiles of a 256-row block exchange row statistics, so they must be co-resident:
     // blocks b, b+8, b+16, b+24 (one XCD, consecutive in its in-order dispatch) take the row
-    // block's 4 tiles; the XCDs interleave row blocks.  Grid = 32 * ceil(tiles_m / 8); blocks
-    // past the last row block leave before any exchange (all four partners of one do).
-    const int k = blockIdx.x >> 3;
+    // block's 4 tiles; XCD x owns the contiguous row blocks [x * per, x * per + per) (mode 3:
+    // the XCDs interleave row blocks instead).  Grid = 32 * per; blocks past the last row block
+    // leave before any exchange (all four partners of one do).
+    const int k = blockIdx.x >> 3, per = (tiles_m + 7) / 8;
     tn0 = k & 3;
-    tm0 = (k >> 2) * 8 + (blockIdx.x & 7);
+    tm0 = ln.mode == 3 ? (k >> 2) * 8 + (blockIdx.x & 7) : (blockIdx.x & 7) * per + (k >> 2);
     if (tm0 >= tiles_m) return;
   } else {
+    if (EPI == PK_EPI_RES_LN && (int)blockIdx.x >= tiles_m * tiles_n) return;
     const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
     const int per_group = group_m * tiles_n;
     const int g = t / per_group, first_m = g * group_m;
@@ -936,23 +942,37 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
     // sn*96 + tn*32 + 8 j + 4 (l >> 5) + i of the tile (the transposed MFMA product).
     const int cb0 = n0 + sn * 96;
     const int rb0 = m0 + wm * 128 + sm * 64 + li;  // + 32 tm
-    // (1) v = (acc + bias) + residual, in place (R may alias C: each element is read here
-    // before this lane writes it, and no other workgroup touches this tile)
+    // (1) v = (acc + bias) + residual.  The residual rows come in coalesced (whole 384-B row
+    // segments, 16 B per lane) into the wave's LDS region — f32 rows of 400 B, conflict-free
+    // both ways — and go back out in the accumulator layout, one 32-row pass (tm) at a time.
+    // R may alias C: every element is read here before this workgroup writes it, and no other
+    // workgroup touches this tile.
+    constexpr int RS = 400;
+    unsigned char* reg = pk_smem + wave * 32 * RS;
+    const int prow0 = m0 + wm * 128 + sm * 64;  // first row of the wave's 64-row block
 #pragma unroll
-    for (int tn = 0; tn < 3; ++tn)
+    for (int tm = 0; tm < 2; ++tm) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = cb0 + tn * 32 + 8 * j + 4 * lh;
-        const floatx4 bv = *reinterpret_cast<const floatx4*>(bias + col);
+      for (int k = 0; k < 12; ++k) {
+        const int idx = k * 64 + lane, lr = idx / 24, c = idx % 24;
+        const int row = prow0 + tm * 32 + lr;
+        const floatx4 f = row < M ? *reinterpret_cast<const floatx4*>(R + (size_t)row * N + cb0 + 4 * c)
+                                  : floatx4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<floatx4*>(reg + lr * RS + c * 16) = f;
+      }
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 #pragma unroll
-        for (int tm = 0; tm < 2; ++tm) {
-          const int row = rb0 + 32 * tm;
-          const floatx4 rv = row < M ? *reinterpret_cast<const floatx4*>(R + (size_t)row * N + col)
-                                     : floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int tn = 0; tn < 3; ++tn)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int col = cb0 + tn * 32 + 8 * j + 4 * lh;
+          const floatx4 bv = *reinterpret_cast<const floatx4*>(bias + col);
+          const floatx4 rv = *reinterpret_cast<const floatx4*>(reg + li * RS + (tn * 8 + 2 * j + lh) * 16);
 #pragma unroll
           for (int i = 0; i < 4; ++i) acc[tm][tn][4 * j + i] = (acc[tm][tn][4 * j + i] + bv[i]) + rv[i];
         }
-      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read back before the next pass rewrites
+    }
     // (2) per row over the wave's 96 columns: mean and M2 (sum of squared deviations); the two
     // lane halves hold 48 columns each
     float mean96[2], m2_96[2];
@@ -979,7 +999,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
     }
     // (3) the two waves of a row (sn = 0, 1) combine through LDS (Chan's pairwise merge, n = 96
     // each, always in sn order so both get the same bits)
-    RowStat* lst = reinterpret_cast<RowStat*>(pk_smem);  // [8 waves][2 tm][32 rows]
+    // [8 waves][2 tm][32 rows], past the 8 wave regions
+    RowStat* lst = reinterpret_cast<RowStat*>(pk_smem + 8 * 32 * RS);
     if (lh == 0) {
 #pragma unroll
       for (int tm = 0; tm < 2; ++tm) lst[(wave * 2 + tm) * 32 + li] = RowStat{mean96[tm], m2_96[tm]};
@@ -1007,7 +1028,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) {
+    if (tid == 0 && ln.mode != 1) {
       __hip_atomic_fetch_add(ln.arrive + tm0, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // bounded wait (~1 s): a partner that never arrives flags the engine instead of hanging
       int ok = 0;
@@ -1029,8 +1050,10 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
       RowStat p[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        p[q] = __builtin_bit_cast(RowStat, __hip_atomic_load(ln.stats + (size_t)(rb0 + 32 * tm) * 4 + q,
-                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        p[q] = ln.mode == 1 ? tile[tm]
+                            : __builtin_bit_cast(RowStat, __hip_atomic_load(
+                                  ln.stats + (size_t)(rb0 + 32 * tm) * 4 + q, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT));
       const float d01 = p[0].mean - p[1].mean, d23 = p[2].mean - p[3].mean;
       const float m01 = (p[0].mean + p[1].mean) * 0.5f, m23 = (p[2].mean + p[3].mean) * 0.5f;
       const float q01 = (p[0].m2 + p[1].m2) + 96.f * d01 * d01;
@@ -1041,7 +1064,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
       rstd[tm] = rsqrtf(var + ln.eps);
     }
     __syncthreads();  // every wave has read the statistics
-    if (tid == 0) {
+    if (tid == 0 && ln.mode != 1) {
       // the last of the 4 partners to leave re-arms the counters for the next launch
       if (__hip_atomic_fetch_add(ln.depart + tm0, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
           tiles_n - 1) {
@@ -1049,33 +1072,45 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
         __hip_atomic_store(ln.depart + tm0, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-    // (6) normalise in registers; write x (f32) and its packed planes
+    // (6) normalise in registers; through the wave's LDS region again, write x (f32) and its
+    // packed planes as whole row segments (384 B of x, three 128-B [hi | lo] blocks of planes)
 #pragma unroll
-    for (int tn = 0; tn < 3; ++tn)
+    for (int tm = 0; tm < 2; ++tm) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = cb0 + tn * 32 + 8 * j + 4 * lh;
-        const floatx4 gg = *reinterpret_cast<const floatx4*>(ln.gamma + col);
-        const floatx4 bb = *reinterpret_cast<const floatx4*>(ln.beta + col);
+      for (int tn = 0; tn < 3; ++tn)
 #pragma unroll
-        for (int tm = 0; tm < 2; ++tm) {
-          const int row = rb0 + 32 * tm;
-          if (row >= M) continue;
+        for (int j = 0; j < 4; ++j) {
+          const int col = cb0 + tn * 32 + 8 * j + 4 * lh;
+          const floatx4 gg = *reinterpret_cast<const floatx4*>(ln.gamma + col);
+          const floatx4 bb = *reinterpret_cast<const floatx4*>(ln.beta + col);
           floatx4 o;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[i] = (acc[tm][tn][4 * j + i] - mean[tm]) * rstd[tm] * gg[i] + bb[i];
+          *reinterpret_cast<floatx4*>(reg + li * RS + (tn * 8 + 2 * j + lh) * 16) = o;
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < 12; ++k) {
+        const int idx = k * 64 + lane, lr = idx / 24, c = idx % 24;
+        const int row = prow0 + tm * 32 + lr;
+        const floatx4 o = *reinterpret_cast<const floatx4*>(reg + lr * RS + c * 16);
+        if (row < M) {
+          const int col = cb0 + 4 * c;
+          *reinterpret_cast<floatx4*>(C + (size_t)row * N + col) = o;
           ushortx4 h, l;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            o[i] = (acc[tm][tn][4 * j + i] - mean[tm]) * rstd[tm] * gg[i] + bb[i];
             h[i] = f2bf(o[i]);
             l[i] = f2bf(o[i] - __builtin_bit_cast(float, (uint32_t)h[i] << 16));
           }
-          *reinterpret_cast<floatx4*>(C + (size_t)row * N + col) = o;
           unsigned short* dst = reinterpret_cast<unsigned short*>(ln.xp) + (size_t)row * NP * N +
                                 (size_t)(col >> 5) * 32 * NP + (col & 31);
           *reinterpret_cast<ushortx4*>(dst) = h;
           if (NP == 2) *reinterpret_cast<ushortx4*>(dst + 32) = l;
         }
       }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     return;
   }
 
@@ -1163,7 +1198,8 @@ hipError_t pp192_launch(const __bf16* A, const __bf16* W, const float* bias, con
   if (hipError_t e = ensure_dynamic_lds((const void*)gemm_pp192_kernel<NP, EPI, NT>, lds); e != hipSuccess)
     return e;
   const int tiles_m = (M + 255) / 256;
-  const int tiles = EPI == PK_EPI_RES_LN ? 32 * ((tiles_m + 7) / 8) : tiles_m * ((N + 191) / 192);
+  const int tiles = EPI == PK_EPI_RES_LN && ln.mode != 2 ? 32 * ((tiles_m + 7) / 8)
+                                                        : tiles_m * ((N + 191) / 192);
   hipLaunchKernelGGL((gemm_pp192_kernel<NP, EPI, NT>), dim3(tiles), dim3(512), lds, st, A, W, bias, R,
                      C, M, N, K, group_m, ln);
   return hipGetLastError();
@@ -1309,22 +1345,43 @@ extern "C" hipError_t ae_launch_gemm_packed(const unsigned short* A, const unsig
 // encoder layer), written as f32 C [M][768] and packed planes Cp [M][np*768]; R may equal C.
 // stats: [(M + 255) / 256 * 256][4] 8-B words; ctr: 2 * ((M + 255) / 256) ints, zero on the first
 // call (the kernel leaves them zero); err: the engine's device error word.
+namespace {
+hipError_t packed_ln(const unsigned short* A, const unsigned short* W, const float* bias,
+                     const float* R, float* C, unsigned short* Cp, int M, int N, int K, int np,
+                     const float* gamma, const float* beta, float eps, uint64_t* stats, int* ctr,
+                     int* err, int mode, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  if (N != 768 || K % 64 != 0 || (np != 1 && np != 2) || !bias || !R || !C || !Cp || !gamma ||
+      !beta || !stats || !ctr || !err)
+    return hipErrorInvalidValue;
+  const int tiles_m = (M + 255) / 256;
+  LnArgs ln{gamma, beta, eps, reinterpret_cast<__bf16*>(Cp), stats, ctr, ctr + tiles_m, err, mode};
+  auto a = reinterpret_cast<const __bf16*>(A);
+  auto w = reinterpret_cast<const __bf16*>(W);
+  if (np == 2) return pp192_launch<2, PK_EPI_RES_LN>(a, w, bias, R, C, M, N, K, PK_GROUP_M, st, ln);
+  return pp192_launch<1, PK_EPI_RES_LN>(a, w, bias, R, C, M, N, K, PK_GROUP_M, st, ln);
+}
+}  // namespace
+
 extern "C" hipError_t ae_launch_gemm_packed_ln(const unsigned short* A, const unsigned short* W,
                                                const float* bias, const float* R, float* C,
                                                unsigned short* Cp, int M, int N, int K, int np,
                                                const float* gamma, const float* beta, float eps,
                                                uint64_t* stats, int* ctr, int* err,
                                                hipStream_t st) {
-  if (M <= 0) return hipSuccess;
-  if (N != 768 || K % 64 != 0 || (np != 1 && np != 2) || !bias || !R || !C || !Cp || !gamma ||
-      !beta || !stats || !ctr || !err)
-    return hipErrorInvalidValue;
-  const int tiles_m = (M + 255) / 256;
-  LnArgs ln{gamma, beta, eps, reinterpret_cast<__bf16*>(Cp), stats, ctr, ctr + tiles_m, err};
-  auto a = reinterpret_cast<const __bf16*>(A);
-  auto w = reinterpret_cast<const __bf16*>(W);
-  if (np == 2) return pp192_launch<2, PK_EPI_RES_LN>(a, w, bias, R, C, M, N, K, PK_GROUP_M, st, ln);
-  return pp192_launch<1, PK_EPI_RES_LN>(a, w, bias, R, C, M, N, K, PK_GROUP_M, st, ln);
+  return packed_ln(A, W, bias, R, C, Cp, M, N, K, np, gamma, beta, eps, stats, ctr, err, 0, st);
+}
+
+// Timing experiments of the fused residual + LayerNorm GEMM (tools/gemm_bench.py): `mode` as
+// LnArgs::mode.  Not part of include/alert_engine.h.
+extern "C" hipError_t ae_bench_gemm_packed_ln(const unsigned short* A, const unsigned short* W,
+                                              const float* bias, const float* R, float* C,
+                                              unsigned short* Cp, int M, int N, int K, int np,
+                                              const float* gamma, const float* beta, float eps,
+                                              uint64_t* stats, int* ctr, int* err, int mode,
+                                              hipStream_t st) {
+  if (mode < 0 || mode > 3) return hipErrorInvalidValue;
+  return packed_ln(A, W, bias, R, C, Cp, M, N, K, np, gamma, beta, eps, stats, ctr, err, mode, st);
 }
 
 // Kernel experiments (tools/gemm_bench.py, tests): explicit tile width (0 = the production choice)

@@ -205,7 +205,7 @@ def _qkv_planes(qkv, np_):
     return _pack(hi, lo, np_)
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("np_", [2, 1])
 @pytest.mark.parametrize("case", ["ragged", "mask", "cls", "planes"])
 def test_attention_pp_matches_f64(gpu, np_, case, variant):
@@ -278,6 +278,8 @@ def test_gemm_packed_ln_matches_f64(gpu, M, K, np_):
     beta = 0.1 * torch.randn(N, generator=g)
     Wh, Wl = _split(W)
     dW = _pack(Wh, Wl, np_).cuda()
+    # device copies held by name: a temporary's memory is recycled before the launch reads it
+    db, dg, dbeta = bias.cuda(), gamma.cuda(), beta.cuda()
     blocks = (M + 255) // 256
     stats = torch.zeros(blocks * 256 * 4, dtype=torch.int64, device="cuda")
     ctr = torch.zeros(2 * blocks, dtype=torch.int32, device="cuda")
@@ -298,8 +300,8 @@ def test_gemm_packed_ln_matches_f64(gpu, M, K, np_):
         dA = _pack(Ah, Al, np_).cuda()
         x = X.cuda()
         xp = torch.zeros((M, np_ * N), dtype=torch.bfloat16, device="cuda")
-        rc = lib.ae_launch_gemm_packed_ln(_p(dA), _p(dW), _p(bias.cuda()), _p(x), _p(x), _p(xp),
-                                          M, N, K, np_, _p(gamma.cuda()), _p(beta.cuda()), 1e-5,
+        rc = lib.ae_launch_gemm_packed_ln(_p(dA), _p(dW), _p(db), _p(x), _p(x), _p(xp),
+                                          M, N, K, np_, _p(dg), _p(dbeta), 1e-5,
                                           _p(stats), _p(ctr), _p(err), st)
         assert rc == 0
         torch.cuda.synchronize()
