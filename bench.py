@@ -282,6 +282,8 @@ def config1_leg(dev, precision, threads, cpu_seconds):
                    "successes": g["successes"], "wall_s": round(g["wall_s"], 2),
                    "victim_queries_per_s": round(g["queries"] / g["wall_s"], 1)}}
     if cpu_seconds > 0:
+        import torch
+        host_threads = torch.get_num_threads()
         cv = cpu_victim(threads)
         cv.state["deadline"] = time.time() + cpu_seconds
         cv.state["t0"] = time.time()
@@ -298,6 +300,7 @@ def config1_leg(dev, precision, threads, cpu_seconds):
         key = lambda r: (r["is_success"], r["queries"], r.get("adv_code"))  # noqa: E731
         res["cpu"]["same_outcome_as_gpu"] = sum(key(a) == key(b) for a, b in
                                                 zip(g["records"], c["records"]))
+        torch.set_num_threads(host_threads)
         res["gpu_vs_cpu_queries_per_s"] = round(res["gpu"]["victim_queries_per_s"]
                                                 / max(res["cpu"]["victim_queries_per_s"], 1e-9), 1)
     return res
@@ -665,6 +668,8 @@ def main():
         # other jobs' load); the best point is the baseline, every point is reported
         sweep = sorted({t for t in (cpu_facts.get("job_share_threads"), threads // 2, threads)
                         if t})
+        import torch as _torch
+        host_threads = _torch.get_num_threads()  # the GPU legs' host work keeps its own setting
         points = []
         for t in sweep:
             log(f"CPU baseline ({t} threads)")
@@ -672,6 +677,7 @@ def main():
             points.append({"cores": t, "value": round(v, 4), "sample": sample})
         best = max(points, key=lambda q: q["value"])
         threads = best["cores"]
+        _torch.set_num_threads(host_threads)
         res["cpu_baseline"] = {"value": best["value"], "unit": "victim queries/s",
                                "cores": best["cores"], "kind": "port",
                                "sample": best["sample"] + f", oracle/roberta_cpu.py fp32 eager, "
