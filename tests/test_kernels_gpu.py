@@ -74,6 +74,14 @@ def _p(t):
     (64, 768, 3072, 2, 2, "192"),
     (257, 192, 192, 1, 0, "192"),
     (700, 576, 256, 2, 2, "192"),
+    # two workgroups per CU (gemm_w2.hip): ragged M / N, short and long K, every epilogue
+    (300, 256, 128, 2, 0, "w2"),
+    (512, 768, 768, 2, 2, "w2"),
+    (257, 512, 192, 2, 1, "w2"),
+    (1000, 384, 64, 1, 3, "w2"),
+    (700, 256, 256, 1, 1, "w2"),
+    (600, 3072, 768, 2, 1, "w2"),
+    (129, 2304, 3072, 2, 0, "w2"),
 ])
 def test_gemm_packed_matches_split_products(gpu, M, N, K, np_, epi, bn):
     lib = _lib()
@@ -101,7 +109,13 @@ def test_gemm_packed_matches_split_products(gpu, M, N, K, np_, epi, bn):
     C = torch.full((M, N), float("nan"), device="cuda")
     Cp = torch.zeros((M, np_ * N), dtype=torch.bfloat16, device="cuda")
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    if bn:  # explicit tile width through the experiment entry point (production kernel, diag 0)
+    if bn == "w2":
+        lib.ae_launch_gemm_w2.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_int32] * 6 + \
+            [ctypes.c_void_p]
+        lib.ae_launch_gemm_w2.restype = ctypes.c_int
+        rc = lib.ae_launch_gemm_w2(_p(dA), _p(dW), _p(db), _p(dR), _p(C), _p(Cp), M, N, K, epi,
+                                   np_, 4, st)
+    elif bn:  # explicit tile width through the experiment entry point (production kernel, diag 0)
         rc = lib.ae_bench_gemm_packed(_p(dA), _p(dW), _p(db), _p(dR), _p(C), _p(Cp), M, N, K, epi,
                                       np_, int(bn), 0, st)
     else:
