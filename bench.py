@@ -281,6 +281,18 @@ def config1_leg(dev, precision, threads, cpu_seconds):
            "gpu": {"precision": precision, "examples": g["examples"], "queries": g["queries"],
                    "successes": g["successes"], "wall_s": round(g["wall_s"], 2),
                    "victim_queries_per_s": round(g["queries"] / g["wall_s"], 1)}}
+    full = sorted(glob.glob(str(ROOT / "profiles" / "*config1_cpu_full*.json")))
+    if full:
+        # the CPU path run to completion outside the bench (tools/config1_cpu_full.py): its
+        # per-function outcome / query count / adversarial-code hash against this GPU run's
+        from tools.config1_cpu_full import record_key
+        rec = json.load(open(full[-1]))
+        mine = [record_key(r) for r in g["records"]]
+        res["cpu_full_run"] = {k: rec[k] for k in ("kind", "cores", "cpu_count", "examples_completed",
+                                                   "complete", "queries", "successes", "wall_s",
+                                                   "victim_queries_per_s")}
+        res["cpu_full_run"]["record"] = "profiles/" + pathlib.Path(full[-1]).name
+        res["cpu_full_run"]["same_outcome_as_gpu"] = sum(a == b for a, b in zip(mine, rec["records"]))
     if cpu_seconds > 0:
         import torch
         host_threads = torch.get_num_threads()
