@@ -52,20 +52,21 @@ __device__ __forceinline__ float gelu_erf(float x) {
 }
 
 // exact-erf GELU through a rational erfc (Abramowitz & Stegun 7.1.26, |erf error| <= 1.5e-7):
-// erfc(z) = t·P5(t)·exp(-z²), t = 1/(1 + 0.3275911 z), z = |x|/√2, so GELU(x) = x - h (x >= 0) or
-// h (x < 0) with h = x·erfc(z)/2.  Over [-12, 12] it is within 3.3e-7 absolute of the float64
-// GELU (torch's f32 GELU: 1.2e-6 absolute), branch-free, 5 Horner FMAs + rcp + exp2 — the
-// split-precision FFN1 epilogue is VALU-bound on this (tools/gemm_bench.py diag 4 vs 0).
+// erfc(z) = t·P5(t)·exp(-z²) = E, t = 1/(1 + 0.3275911 z), z = |x|/√2.  With u = x/2,
+// GELU(x) = u + |u| - |u|·E (x >= 0: x - u·E; x < 0: u·E), so no compare / select: one FMA ends
+// it.  Over [-12, 12] it is within 3.3e-7 absolute of the float64 GELU (torch's f32 GELU: 1.2e-6
+// absolute), 5 Horner FMAs + rcp + exp2 — the split-precision FFN1 epilogue is VALU-bound on
+// this (tools/gemm_bench.py diag 4 vs 0).
 __device__ __forceinline__ float gelu_erfc_fast(float x) {
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.23164190207799160f, fabsf(x), 1.0f));
+  const float u = 0.5f * x, au = fabsf(u);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.46328380415598320f, au, 1.0f));
   float p = 1.061405429f;
   p = fmaf(p, t, -1.453152027f);
   p = fmaf(p, t, 1.421413741f);
   p = fmaf(p, t, -0.284496736f);
   p = fmaf(p, t, 0.254829592f);
-  const float e = __builtin_amdgcn_exp2f((x * -0.72134752044448170f) * x);  // exp(-x²/2)
-  const float h = (0.5f * x) * ((p * t) * e);
-  return x >= 0.f ? x - h : h;
+  const float e = __builtin_amdgcn_exp2f(u * (-2.88539008177792680f * u));  // exp(-x²/2)
+  return fmaf(-au, (p * t) * e, u + au);
 }
 
 // bf16 round-to-nearest-even of an f32 (NaN-preserving cast lowered to v_cvt_pk_bf16_f32).
