@@ -17,6 +17,7 @@
 //   * S^T = K·Q^T and O^T += V^T·P^T on v_mfma_f32_32x32x16_bf16, 3 products per term pair for
 //     NP = 2 (x_hi·y_hi + x_hi·y_lo + x_lo·y_hi), P split into hi/lo from the S accumulator.
 #include <cfloat>
+#include <type_traits>
 
 #include "common.h"
 
@@ -95,7 +96,12 @@ __global__ __launch_bounds__(256, PIPE == 5 ? 3 : 2) void attn_pp_kernel(const u
                                                          int mask_L) {
   using P = PPL<NP>;
   constexpr int TERMS = NP == 2 ? 3 : 1;
-  __shared__ __attribute__((aligned(16))) unsigned char lds[P::LDS];
+  static_assert(!(HAS_MASK && PIPE == 6), "PIPE 6 has no mask path (its loop keeps no ordinary "
+                                          "global load, so the mask launches run PIPE 4)");
+  // PIPE 6: three K and three V slots (the O staging of the epilogue fits inside)
+  constexpr int LDS_BYTES =
+      PIPE == 6 ? (6 * P::TILE > 4 * 32 * 66 * 4 ? 6 * P::TILE : 4 * 32 * 66 * 4) : P::LDS;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
   const int seq = blockIdx.z, head = blockIdx.y, qb = blockIdx.x;
   const int start = cu[seq];
   const int len = cu[seq + 1] - start;
@@ -277,7 +283,116 @@ __global__ __launch_bounds__(256, PIPE == 5 ? 3 : 2) void attn_pp_kernel(const u
   };
 
   const int nkt = (len + KT - 1) / KT;
-  if (PIPE == 0) {
+  if constexpr (PIPE == 6) {
+    // 3-slot rings: K_j in slot j % 3, V_j in slot 3 + j % 3.  Iteration kt issues V_{kt+2} and
+    // K_{kt+3} and, at its end, waits only for what iteration kt+1 reads (V_{kt+1}, K_{kt+2},
+    // issued one iteration earlier): a counted vmcnt leaves this iteration's DMA in flight across
+    // the raw s_barrier, so every transfer has two tiles of compute to land in.
+    auto kslot = [&](int j) { return (uint32_t)(j * P::TILE); };        // prologue tiles 0..2
+    auto vslot = [&](int j) { return (uint32_t)((3 + j) * P::TILE); };
+    auto wait_vm = [](int n) {  // n = DMA instructions allowed to stay outstanding
+      if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    auto barrier = []() {
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    constexpr int DM = P::DMA_PER_WAVE;  // DMA instructions per wave per matrix tile
+    // prologue: K0 V0 K1 V1 K2 (as many as exist)
+    int groups = 1;
+    issue1(0, AE_HIDDEN, lds0 + kslot(0), false);
+    issue1(0, 2 * AE_HIDDEN, lds0 + vslot(0), true);
+    ++groups;
+    if (nkt > 1) {
+      issue1(1, AE_HIDDEN, lds0 + kslot(1), false);
+      issue1(1, 2 * AE_HIDDEN, lds0 + vslot(1), true);
+      groups += 2;
+    }
+    if (nkt > 2) {
+      issue1(2, AE_HIDDEN, lds0 + kslot(2), false);
+      ++groups;
+    }
+    wait_vm(DM * (groups - 1));  // K0 landed
+    barrier();
+    floatx16 sA, sB;  // S of the current / next tile, alternating by tile parity
+    s_mfma(lds + kslot(0), sA);
+    wait_vm(nkt > 1 ? DM * (groups - 3) : 0);  // V0 (and K1) landed
+    barrier();  // every wave has read K0 (its slot takes K3) and sees V0, K1
+    // one tile; R = kt % 6 fixes the slots (R % 3) and the S buffers (R % 2) at compile time, so
+    // every LDS address of the body is a constant offset from a per-lane base
+    auto body = [&](auto rc, int kt, floatx16& s_cur, floatx16& s_next) {
+      constexpr int R = decltype(rc)::value;
+      constexpr uint32_t KS_NEXT = ((R + 1) % 3) * P::TILE, VS_CUR = (3 + R % 3) * P::TILE;
+      constexpr uint32_t VS_ISS = (3 + (R + 2) % 3) * P::TILE, KS_ISS = (R % 3) * P::TILE;
+      int n_iss = 0;
+      if (kt + 2 < nkt) {
+        issue1(kt + 2, 2 * AE_HIDDEN, lds0 + VS_ISS, true);
+        n_iss += DM;
+      }
+      if (kt + 3 < nkt) {
+        issue1(kt + 3, AE_HIDDEN, lds0 + KS_ISS, false);
+        n_iss += DM;
+      }
+      // deferred rescale (cdna_hip_programming.md T13): keep the running max unless some row's
+      // tile max exceeds it by more than 8 (log2 domain), so P <= 2^8 and the O rescale runs only
+      // on the tiles that move a max by that much — the same softmax with another reference max
+      float mt = -INFINITY;
+      if ((kt + 1) * KT <= len) {
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) mt = fmaxf(mt, fmaxf(s_cur[r], s_cur[r + 1]));
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const bool in = kt * KT + mfma32_row(r, lh) < len;
+          s_cur[r] = in ? s_cur[r] : -INFINITY;
+          mt = fmaxf(mt, s_cur[r]);
+        }
+      }
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const bool grow = __any(mt > m_run + 8.f);
+      const float m_new = grow ? fmaxf(m_run, mt) : m_run;
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);  // 1 when m_new == m_run; 0 from -inf
+      bf16x8 ph[2], pl[2];
+      __builtin_amdgcn_sched_barrier(0);
+      const float psum = exp_split(s_cur, m_new, ph, pl);
+      s_mfma(lds + KS_NEXT, s_next);
+      __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+      for (int i = 0; i < 12; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      l_run = l_run * alpha + psum;
+      m_run = m_new;
+      if (grow) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+      }
+      pv_mfma(lds + VS_CUR, ph, pl);
+      wait_vm(n_iss);  // V_{kt+1}, K_{kt+2} landed; this iteration's DMA stays in flight
+      barrier();
+    };
+    for (int kt = 0; kt < nkt; kt += 6) {
+      body(std::integral_constant<int, 0>(), kt, sA, sB);
+      if (kt + 1 >= nkt) break;
+      body(std::integral_constant<int, 1>(), kt + 1, sB, sA);
+      if (kt + 2 >= nkt) break;
+      body(std::integral_constant<int, 2>(), kt + 2, sA, sB);
+      if (kt + 3 >= nkt) break;
+      body(std::integral_constant<int, 3>(), kt + 3, sB, sA);
+      if (kt + 4 >= nkt) break;
+      body(std::integral_constant<int, 4>(), kt + 4, sA, sB);
+      if (kt + 5 >= nkt) break;
+      body(std::integral_constant<int, 5>(), kt + 5, sB, sA);
+    }
+  } else if (PIPE == 0) {
     // stage b = [K | V] of one tile, two stages
     issue1(0, AE_HIDDEN, lds0, false);
     issue1(0, 2 * AE_HIDDEN, lds0 + P::TILE, true);
@@ -366,6 +481,55 @@ __global__ __launch_bounds__(256, PIPE == 5 ? 3 : 2) void attn_pp_kernel(const u
 
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  if constexpr (PIPE == 6) {
+    // O through LDS (rows of 66 floats: 8-B aligned, 2-way on the column writes), then 16-B
+    // stores of whole output chunks: 8 (planes) or 8 (f32) store instructions per wave instead of
+    // one 2-B store per row and plane
+    constexpr int S6 = 66;
+    float* os6 = reinterpret_cast<float*>(lds) + wave * 32 * S6;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int d = mfma32_row(r, lh);
+      os6[li * S6 + d] = o0[r] * inv;
+      os6[li * S6 + 32 + d] = o1[r] * inv;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own rows: no barrier
+    constexpr int CPR = PLANES ? 8 * NP : 16;             // 16-B chunks per output row
+    constexpr int RPI = 64 / CPR;                         // rows per store instruction
+    const int c = lane % CPR;
+#pragma unroll
+    for (int it = 0; it < 32 / RPI; ++it) {
+      const int rr = it * RPI + lane / CPR;
+      const int qq = qb * QPB + wave * 32 + rr;
+      const float* src = os6 + rr * S6;
+      if (PLANES) {
+        // chunk c: block c / (4 NP), plane (c / 4) % NP, d = 32 block + 8 (c % 4) .. + 7
+        const int d0 = 32 * (c / (4 * NP)) + 8 * (c % 4);
+        const bool lo_plane = NP == 2 && ((c >> 2) & 1);
+        uint32_t w[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const floatx2 v = *reinterpret_cast<const floatx2*>(src + d0 + 2 * e);
+          const __bf16 hx = (__bf16)v.x, hy = (__bf16)v.y;
+          bf16x2 pr;
+          if (lo_plane) pr = bf16x2{(__bf16)(v.x - (float)hx), (__bf16)(v.y - (float)hy)};
+          else pr = bf16x2{hx, hy};
+          w[e] = __builtin_bit_cast(uint32_t, pr);
+        }
+        if (qq < nq) {
+          unsigned short* dst = op + (size_t)(start + qq) * NP * AE_HIDDEN + head * 64 * NP + c * 8;
+          *reinterpret_cast<u32x4*>(dst) = u32x4{w[0], w[1], w[2], w[3]};
+        }
+      } else {
+        const floatx2 a = *reinterpret_cast<const floatx2*>(src + 4 * c);
+        const floatx2 b = *reinterpret_cast<const floatx2*>(src + 4 * c + 2);
+        if (qq < nq)
+          *reinterpret_cast<floatx4*>(out + (size_t)(start + qq) * AE_HIDDEN + head * AE_HEAD_DIM + 4 * c) =
+              floatx4{a.x, a.y, b.x, b.y};
+      }
+    }
+    return;
+  }
   float* os = reinterpret_cast<float*>(lds) + wave * 32 * OSTRIDE;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -402,7 +566,8 @@ hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op
   if (np != 1 && np != 2) return hipErrorInvalidValue;
   dim3 grid((max_q + QPB - 1) / QPB, heads, n), block(256);
 #define APP_LAUNCH(N, M, PL)                                                                 \
-  hipLaunchKernelGGL((attn_pp_kernel<N, M, PL, PIPE>), grid, block, 0, stream, qkvp, out, op, cu, \
+  hipLaunchKernelGGL((attn_pp_kernel<N, M, PL, (M && PIPE == 6) ? 4 : PIPE>), grid, block, 0,      \
+                     stream, qkvp, out, op, cu,                                                 \
                      q_rows, mask, mask_L)
 #define APP_MP(N)                                                      \
   if (op) {                                                            \
@@ -419,10 +584,11 @@ hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op
 #undef APP_LAUNCH
   return hipGetLastError();
 }
-// production loop: PIPE 4 (tools/attn_bench.py, B=64 x L=512, same box, interleaved rounds:
-// pp1 197.0 / pp4 192.6 us median, ragged 129.1 / 126.5; profiles/r3i_attn_ab.jsonl).  PIPE 2-3
+// production loop: PIPE 6 (tools/attn_bench.py, B=64 x L=512, same box, interleaved rounds:
+// pp4 198.3 / pp6 190.8 us median, profiles/r3n_attn_ab.jsonl; before it pp1 197.0 / pp4 192.6,
+// ragged 129.1 / 126.5, profiles/r3i_attn_ab.jsonl); the masked launches keep PIPE 4.  PIPE 2-3
 // (packed split) and 5 (3 workgroups per CU) measured no better than 4.
-constexpr int APP_PIPE = 4;
+constexpr int APP_PIPE = 6;
 }  // namespace
 
 extern "C" hipError_t ae_launch_attention_pp(const unsigned short* qkvp, float* out,
@@ -443,6 +609,8 @@ extern "C" hipError_t ae_bench_attention_pp(const unsigned short* qkvp, float* o
                                             unsigned short* op, const int* cu, const int* q_rows,
                                             int max_q, int n, int heads, const uint32_t* mask,
                                             int mask_L, int np, int variant, hipStream_t stream) {
+  if (variant == 6)
+    return app_launch<6>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
   if (variant == 5)
     return app_launch<5>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
   if (variant == 4)

@@ -65,7 +65,8 @@ struct LnArgs {
   int mode;          // 0 = production; timing experiments (results WRONG for 1): 1 = no exchange
                      // (each tile normalises with its own 192 columns' statistics), 2 = the
                      // grouped XCD tile order of the other epilogues (partners may straddle two
-                     // XCDs when tiles_m % 32 != 0), 3 = row blocks interleaved over the XCDs
+                     // XCDs when tiles_m % 32 != 0), 3 = row blocks interleaved over the XCDs,
+                     // 4 = the previous 8-B plane stores (results exact)
 };
 
 namespace {
@@ -1089,24 +1090,55 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
           *reinterpret_cast<floatx4*>(reg + li * RS + (tn * 8 + 2 * j + lh) * 16) = o;
         }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (ln.mode == 4) {  // timing A/B only: the previous 4-column form (8-B plane stores)
 #pragma unroll
-      for (int k = 0; k < 12; ++k) {
-        const int idx = k * 64 + lane, lr = idx / 24, c = idx % 24;
+        for (int k = 0; k < 12; ++k) {
+          const int idx = k * 64 + lane, lr = idx / 24, c = idx % 24;
+          const int row = prow0 + tm * 32 + lr;
+          const floatx4 o = *reinterpret_cast<const floatx4*>(reg + lr * RS + c * 16);
+          if (row < M) {
+            const int col = cb0 + 4 * c;
+            *reinterpret_cast<floatx4*>(C + (size_t)row * N + col) = o;
+            ushortx4 h, l;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              h[i] = f2bf(o[i]);
+              l[i] = f2bf(o[i] - __builtin_bit_cast(float, (uint32_t)h[i] << 16));
+            }
+            unsigned short* dst = reinterpret_cast<unsigned short*>(ln.xp) + (size_t)row * NP * N +
+                                  (size_t)(col >> 5) * 32 * NP + (col & 31);
+            *reinterpret_cast<ushortx4*>(dst) = h;
+            if (NP == 2) *reinterpret_cast<ushortx4*>(dst + 32) = l;
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        continue;
+      }
+      // 8 consecutive columns per lane: x as two 16-B stores, each plane as one 16-B store (24
+      // store instructions per pass, all 16 B per lane; was 36, two thirds of them 8 B)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const int idx = k * 64 + lane, lr = idx / 12, c8 = idx % 12;
         const int row = prow0 + tm * 32 + lr;
-        const floatx4 o = *reinterpret_cast<const floatx4*>(reg + lr * RS + c * 16);
+        const floatx4 o0 = *reinterpret_cast<const floatx4*>(reg + lr * RS + c8 * 32);
+        const floatx4 o1 = *reinterpret_cast<const floatx4*>(reg + lr * RS + c8 * 32 + 16);
         if (row < M) {
-          const int col = cb0 + 4 * c;
-          *reinterpret_cast<floatx4*>(C + (size_t)row * N + col) = o;
-          ushortx4 h, l;
+          const int col = cb0 + 8 * c8;
+          *reinterpret_cast<floatx4*>(C + (size_t)row * N + col) = o0;
+          *reinterpret_cast<floatx4*>(C + (size_t)row * N + col + 4) = o1;
+          uint32_t h[4], l[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            h[i] = f2bf(o[i]);
-            l[i] = f2bf(o[i] - __builtin_bit_cast(float, (uint32_t)h[i] << 16));
+            const float a = i < 2 ? o0[2 * i] : o1[2 * i - 4], b = i < 2 ? o0[2 * i + 1] : o1[2 * i - 3];
+            const uint32_t ha = f2bf(a), hb = f2bf(b);
+            h[i] = ha | (hb << 16);
+            l[i] = (uint32_t)f2bf(a - __builtin_bit_cast(float, ha << 16)) |
+                   ((uint32_t)f2bf(b - __builtin_bit_cast(float, hb << 16)) << 16);
           }
           unsigned short* dst = reinterpret_cast<unsigned short*>(ln.xp) + (size_t)row * NP * N +
                                 (size_t)(col >> 5) * 32 * NP + (col & 31);
-          *reinterpret_cast<ushortx4*>(dst) = h;
-          if (NP == 2) *reinterpret_cast<ushortx4*>(dst + 32) = l;
+          *reinterpret_cast<uint4*>(dst) = uint4{h[0], h[1], h[2], h[3]};
+          if (NP == 2) *reinterpret_cast<uint4*>(dst + 32) = uint4{l[0], l[1], l[2], l[3]};
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1380,7 +1412,7 @@ extern "C" hipError_t ae_bench_gemm_packed_ln(const unsigned short* A, const uns
                                               const float* gamma, const float* beta, float eps,
                                               uint64_t* stats, int* ctr, int* err, int mode,
                                               hipStream_t st) {
-  if (mode < 0 || mode > 3) return hipErrorInvalidValue;
+  if (mode < 0 || mode > 4) return hipErrorInvalidValue;
   return packed_ln(A, W, bias, R, C, Cp, M, N, K, np, gamma, beta, eps, stats, ctr, err, mode, st);
 }
 

@@ -16,7 +16,8 @@ Prints ONE JSON line (rank 0).  `roofline` is the dominant kernel (the FFN1 GEMM
 [T,768]x[768,3072] + bias + GELU) timed live with HIP events on the launch stream (events created
 before the timed region); `cpu_baseline` is oracle/roberta_cpu.py (PyTorch-CPU fp32 eager
 restatement of the reference's scoring) on the host cores this job may use.  Sub-objects: the
-exact-fp32 mode of the same step (`fp32_mode`), the end-to-end config-2 GA attack over all of
+exact-fp32 mode of the same step (`fp32_mode`), the bf16 mode as a bound diagnostic
+(`bf16_mode`: one bf16 MFMA per product instead of three), the end-to-end config-2 GA attack over all of
 test_subs_0_400 (`attack`), config 1 (greedy, 16 functions) on GPU and CPU (`config1`), masked-LM
 substitute generation (`substitutes`), the MHM-NS baseline (`mhm`) and config 5 (`authorship`:
 CodeBERT GA vs MHM-NS, GraphCodeBERT GA).
@@ -57,8 +58,8 @@ def parse_args():
                     help="CPU scoring microbenchmark budget (cpu_baseline)")
     ap.add_argument("--cpu-e2e-seconds", type=float, default=60.0,
                     help="cap (s) of the CPU config-1 greedy attack (config1.cpu); all 16 "
-                         "functions take ~10 min on the box's cores (run once with a larger cap: "
-                         "profiles/r3d_config1_cpu_complete.jsonl)")
+                         "functions take ~15 min (tools/config1_cpu_full.py ran them once: "
+                         "profiles/r3_config1_cpu_full.json, compared as config1.cpu_full_run)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--attack-examples", type=int, default=400,
                     help="examples of test_subs_0_400 in the config-2 GA attack leg (0 disables)")
@@ -611,7 +612,7 @@ def main():
     # 3 bf16 MFMAs per product, so its ceiling in algorithmic FLOP/s is the bf16 peak / 3
     peak = {"fp32": FP32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS,
             "f32x3": BF16_MFMA_PEAK_TFLOPS / 3}[args.precision]
-    fp32_mode = None
+    fp32_mode = bf16_mode = None
     if args.precision != "fp32" and not args.no_fp32_mode:
         # the exact-fp32 mode of the same step, and the split / bf16 parity on this very batch
         ref_eng = Engine(sd, head="sigmoid1", num_labels=1, precision="fp32", device=dev.index)
@@ -628,6 +629,24 @@ def main():
                      "max_abs_dprob_vs_this_mode": float(np.abs(ref_out.cpu().numpy()[:, 0]
                                                                 - probs).max())}
         ref_eng.close()
+        if args.precision == "f32x3":
+            # bound diagnostic: the same step with one bf16 MFMA per product (hi planes only) —
+            # what the split products cost; not a parity mode (stated tolerance 2e-2)
+            b_eng = Engine(sd, head="sigmoid1", num_labels=1, precision="bf16", device=dev.index)
+            b_out = torch.empty_like(out)
+            el16, _ = time_steps(b_eng, ids_dev, lens, b_out, n32, args.warmup, dev, dist,
+                                 profile=False)
+            if dist is not None:
+                t = torch.tensor([el16], dtype=torch.float64, device=dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                el16 = float(t.item())
+            bf16_mode = {
+                "value": round(world * n32 * B / el16, 3), "unit": "victim queries/s", "steps": n32,
+                "ms_per_step": round(1e3 * el16 / n32, 4),
+                "max_abs_dprob_vs_fp32_mode": float(np.abs(ref_out.cpu().numpy()[:, 0]
+                                                           - b_out.cpu().numpy()[:, 0]).max()),
+                "note": "diagnostic only: 1 bf16 MFMA per product instead of 3"}
+            b_eng.close()
     executed = executed_flops_per_query(L) * total_q / elapsed / 1e12
     res = {
         "metric": METRIC,
@@ -671,6 +690,8 @@ def main():
     }
     if fp32_mode:
         res["fp32_mode"] = fp32_mode
+    if bf16_mode:
+        res["bf16_mode"] = bf16_mode
     eng.close()
     threads, cpu_facts = host_cores()
     log(f"scoring step: {value:.1f} q/s")

@@ -219,25 +219,38 @@ def _qkv_planes(qkv, np_):
     return _pack(hi, lo, np_)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("np_", [2, 1])
-@pytest.mark.parametrize("case", ["ragged", "mask", "cls", "planes"])
+@pytest.mark.parametrize("case", ["ragged", "mask", "cls", "planes", "grow"])
 def test_attention_pp_matches_f64(gpu, np_, case, variant):
     """attn_pp_kernel (packed-plane Q/K/V moved by LDS-DMA, swizzled K/V images, transposed V
     reads) against the float64 reference, for both plane counts (np 1 = bf16 mode: stated
-    tolerance 2e-2), both loops (variant 1: software-pipelined) and the ragged / mask /
-    CLS-only / packed-output launches."""
+    tolerance 2e-2), every loop (1: software-pipelined, 6: 3-slot rings + deferred rescale) and
+    the ragged / mask / CLS-only / packed-output launches.  "grow": spike keys whose scores
+    rise along the sequence, so every row max jumps past the deferred-rescale threshold (2^8)
+    several times — the rare branch of variant 6."""
     lib = _lib()
     vp, i32 = ctypes.c_void_p, ctypes.c_int32
     lib.ae_bench_attention_pp.argtypes = [vp] * 5 + [i32] * 3 + [vp, i32, i32, i32, vp]
     lib.ae_bench_attention_pp.restype = ctypes.c_int
     g = torch.Generator().manual_seed(11 + np_)
-    lens = [1, 31, 32, 33, 129, 300, 64] if case != "mask" else [40, 97, 128]
+    lens = {"mask": [40, 97, 128], "grow": [300, 517, 64]}.get(case, [1, 31, 32, 33, 129, 300, 64])
     n = len(lens)
     cu = torch.zeros(n + 1, dtype=torch.int32)
     cu[1:] = torch.cumsum(torch.tensor(lens), 0)
     T = int(cu[-1])
     qkv = torch.randn(T, 3 * 768, generator=g)
+    if case == "grow":
+        # every query ~ the all-ones direction; keys at 40, 100, 200, 400 of a sequence are c x ones,
+        # so a row's max jumps 0.5 -> 6 -> 13 -> 20 -> 27 (natural units; > 8 in log2 each time)
+        qkv *= 0.25
+        qkv[:, :768] += 1.0
+        start = 0
+        for x in lens:
+            for p_, c in ((40, 0.75), (100, 1.625), (200, 2.5), (400, 3.375)):
+                if p_ < x:
+                    qkv[start + p_, 768:1536] = c
+            start += x
     L, mask, dmask = 0, None, None
     if case == "mask":
         L = 128
