@@ -555,6 +555,333 @@ __global__ __launch_bounds__(256, PIPE == 5 ? 3 : 2) void attn_pp_kernel(const u
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// attn_pp8_kernel (variant 7): the same attention as attn_pp_kernel on 8 waves that share each
+// SIMD in a fixed ping-pong (MI355X_MICROARCH.md "Two waves per SIMD";
+// cdna_hip_programming.md T16).  Both 4-wave groups own the same 128 queries (wave w and w + 4
+// share a SIMD and a 32-query slice) but split the KEYS: group g takes key tiles g, g + 2, g + 4,
+// ... from its own 4-slot K and V rings, and the two partial softmaxes (m, l, O) are merged at the
+// end (flash-decoding inside the workgroup).  A group's work alternates two segment kinds:
+//   V(i): softmax of S(i) -> P(i) (deferred rescale as PIPE 6), the O rescale, the LDS reads of
+//         the next C segment's operands (K(i+1), V(i)) and the DMA of K(i+3), V(i+3);
+//   C(i): MFMAs only — S(i+1) = K(i+1)·Q^T and O += V(i)^T·P(i)^T — then the counted vmcnt that
+//         lands K(i+2), V(i+1);
+// group 1 runs one segment behind group 0, and an s_barrier separates segments, so on every SIMD
+// one wave feeds the matrix pipe while its partner runs the softmax VALU and the LDS traffic.
+// Measured SLOWER than PIPE 6 (B=64 x L=512, same box: 286.8 vs 173.3 us,
+// profiles/r3q_attn_pp7_ab.jsonl), correct (tests/test_kernels_gpu.py variant 7): a V segment
+// (softmax VALU + 24 LDS reads + 4 LDS-DMA issues) runs about twice a C segment's 24 MFMAs, so
+// the matrix pipe idles at every barrier, and with one workgroup per CU each workgroup's
+// prologue (Q, first tiles) and merge / store epilogue are no longer hidden by a co-resident
+// one.  Kept as an experiment (ae_bench_attention_pp variant 7), not used by the engine.
+template <int NP, bool PLANES>
+__global__ __launch_bounds__(512, 1) void attn_pp8_kernel(const unsigned short* __restrict__ qkvp,
+                                                          float* __restrict__ out,
+                                                          unsigned short* __restrict__ op,
+                                                          const int* __restrict__ cu,
+                                                          const int* __restrict__ q_rows) {
+  using P = PPL<NP>;
+  constexpr int TERMS = NP == 2 ? 3 : 1;
+  constexpr int NSL = 4;                      // ring slots per matrix per group
+  constexpr int GRING = 2 * NSL * P::TILE;    // a group's K then V slots
+  constexpr int MERGE_BYTES = 4 * 34 * 64 * 4;  // group 1's (O, m, l) per lane, after the loop
+  constexpr int STAGE_BYTES = 4 * 32 * 66 * 4;  // group 0's context staging, after the merge
+  constexpr int MERGE_OFF = GRING > STAGE_BYTES ? GRING : (STAGE_BYTES + 1023) / 1024 * 1024;
+  constexpr int LDS_BYTES = 2 * GRING > MERGE_OFF + MERGE_BYTES ? 2 * GRING : MERGE_OFF + MERGE_BYTES;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
+  const int seq = blockIdx.z, head = blockIdx.y, qb = blockIdx.x;
+  const int start = cu[seq];
+  const int len = cu[seq + 1] - start;
+  const int nq = q_rows ? min(len, q_rows[0]) : len;
+  if (qb * QPB >= nq) return;  // the whole workgroup: no barrier is skipped by part of it
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2, gw = wave & 3;
+  const int li = lane & 31, lh = lane >> 5;
+  constexpr size_t LDR = (size_t)NP * QKV_COLS;
+
+  const int q = qb * QPB + gw * 32 + li;
+  const int qr = q < nq ? q : nq - 1;
+  bf16x8 qh[4], ql[4];
+  {
+    const unsigned short* qp = qkvp + (size_t)(start + qr) * LDR + (size_t)head * 64 * NP;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int d = 16 * s + 8 * lh;
+      const int off = (d >> 5) * 32 * NP + (d & 31);
+      qh[s] = *reinterpret_cast<const bf16x8*>(qp + off);
+      if (TERMS == 3) ql[s] = *reinterpret_cast<const bf16x8*>(qp + off + 32);
+    }
+  }
+
+  const int nkt = (len + KT - 1) / KT;
+  const int n = (nkt - grp + 1) >> 1;  // this group's key tiles: t = 2 i + grp, i < n
+  const int nA = (nkt + 1) >> 1;       // group 0's count (>= group 1's)
+  const uint32_t ring = (uint32_t)(uintptr_t)lds + grp * GRING;
+  const unsigned char* gl = lds + grp * GRING;
+  constexpr int DM = P::DMA_PER_WAVE;
+  const int dr = lane / P::CR, dc = lane % P::CR;
+  // DMA of this group's i-th K (moff = AE_HIDDEN) or V (2 AE_HIDDEN) tile into its slot
+  auto issue = [&](int i, bool is_v) {
+    const int t = 2 * i + grp;
+    const uint32_t dst = ring + ((is_v ? NSL : 0) + (i & (NSL - 1))) * P::TILE;
+#pragma unroll
+    for (int j = 0; j < DM; ++j) {
+      const int pi = gw * DM + j;
+      const int r = pi * P::ROWS_PER_DMA + dr;
+      int key = t * KT + r;
+      key = key < len ? key : len - 1;
+      const unsigned short* row = qkvp + (size_t)(start + key) * LDR;
+      const int moff = is_v ? 2 * AE_HIDDEN : AE_HIDDEN;
+      dma16(row + (size_t)(moff + head * 64) * NP + (is_v ? vpos<NP>(r, dc) : kpos<NP>(r, dc)) * 8,
+            dst + pi * 1024);
+    }
+  };
+  auto wait_vm = [](int k) {  // k = DMA instructions allowed to stay outstanding
+    if (k >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (k >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (k >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if (k >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if (k >= 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  auto barrier = []() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // operand fragments of the next C segment (read in the V segment before it)
+  bf16x8 kfh[4], kfl[4];       // K(i+1): per 16-d step, hi / lo planes of this lane's key row
+  bf16x8 vfh[2][2], vfl[2][2];  // V(i): [key step t][d tile]
+  auto read_k = [&](int i) {
+    const unsigned char* kr = gl + (i & (NSL - 1)) * P::TILE + li * P::RB;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int d0 = 16 * ks + 8 * lh;
+      kfh[ks] = *reinterpret_cast<const bf16x8*>(kr + kpos<NP>(li, chunk_of<NP>(0, d0)) * 16);
+      if (TERMS == 3)
+        kfl[ks] = *reinterpret_cast<const bf16x8*>(kr + kpos<NP>(li, chunk_of<NP>(1, d0)) * 16);
+    }
+  };
+  auto read_v = [&](int i) {
+    const unsigned char* stv = gl + (NSL + (i & (NSL - 1))) * P::TILE;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int kq = 16 * t + 4 * lh + ((lane >> 2) & 3);
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int col = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+        const int cb = (col & 7) * 2;
+        const unsigned char* va = stv + kq * P::RB + cb;
+        const unsigned char* vb = stv + (kq + 8) * P::RB + cb;
+        const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (lds_bf16x4*)(va + vpos<NP>(kq, chunk_of<NP>(0, col)) * 16));
+        const bf16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (lds_bf16x4*)(vb + vpos<NP>(kq + 8, chunk_of<NP>(0, col)) * 16));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { vfh[t][dt][e] = a[e]; vfh[t][dt][4 + e] = b[e]; }
+        if (TERMS == 3) {
+          const bf16x4 c = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)(va + vpos<NP>(kq, chunk_of<NP>(1, col)) * 16));
+          const bf16x4 d = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)(vb + vpos<NP>(kq + 8, chunk_of<NP>(1, col)) * 16));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { vfl[t][dt][e] = c[e]; vfl[t][dt][4 + e] = d[e]; }
+        }
+      }
+    }
+  };
+
+  floatx16 s, o0, o1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; }
+  float m_run = -INFINITY, l_run = 0.f;
+  bf16x8 ph[2], pl[2];
+
+  // C(i): S(i+1) (if it exists) and O += V(i)^T P(i)^T (i >= 0); then land K(i+2), V(i+1)
+  auto seg_c = [&](int i) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (i + 1 < n) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        if (TERMS == 3) {
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfl[ks], qh[ks], s, 0, 0, 0);
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfh[ks], ql[ks], s, 0, 0, 0);
+        }
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfh[ks], qh[ks], s, 0, 0, 0);
+      }
+    }
+    if (i >= 0 && i < n) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          floatx16& o = dt == 0 ? o0 : o1;
+          if (TERMS == 3) {
+            o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfl[t][dt], ph[t], o, 0, 0, 0);
+            o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfh[t][dt], pl[t], o, 0, 0, 0);
+          }
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfh[t][dt], ph[t], o, 0, 0, 0);
+        }
+    }
+    // DMA issue order K0 V0 K1 V1 ...: after K(i+2) come V(i+2), K(i+3), V(i+3)
+    if (i + 2 < n) wait_vm(DM * (1 + (i + 3 < n ? 2 : 0)));
+    else wait_vm(0);
+  };
+  // V(i): softmax of S(i), O rescale, the next C segment's operand reads, DMA of tile i+3
+  auto seg_v = [&](int i) {
+    if (i < 0 || i >= n) return;
+    const int t = 2 * i + grp;
+    float mt = -INFINITY;
+    if ((t + 1) * KT <= len) {
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) mt = fmaxf(mt, fmaxf(s[r], s[r + 1]));
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const bool in = t * KT + mfma32_row(r, lh) < len;
+        s[r] = in ? s[r] : -INFINITY;
+        mt = fmaxf(mt, s[r]);
+      }
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const bool grow = __any(mt > m_run + 8.f);
+    const float m_new = grow ? fmaxf(m_run, mt) : m_run;
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+    float psum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = __builtin_amdgcn_exp2f(s[r] - m_new);
+      psum += p;
+      const __bf16 h = (__bf16)p;
+      ph[r >> 3][r & 7] = h;
+      pl[r >> 3][r & 7] = (__bf16)(p - (float)h);
+    }
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+    if (grow) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+    }
+    if (i + 1 < n) read_k(i + 1);
+    read_v(i);
+    if (i + 3 < n) {
+      issue(i + 3, false);
+      issue(i + 3, true);
+    }
+  };
+
+  // prologue: K0 V0 K1 V1 K2 V2 of this group (as many as exist); K0 landed -> its fragments
+  int issued = 0;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    if (i < n) {
+      issue(i, false);
+      issue(i, true);
+      issued += 2;
+    }
+  wait_vm(n > 0 ? DM * (issued - 1) : 0);
+  // Q through an empty asm: its uses in the loop then depend on the asm, not on the loads, so
+  // hipcc places its wait for them here (once, with the prologue DMA) instead of inside every
+  // C segment, where it drained the tile DMA in flight (measured: 296 vs 175 us)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    asm volatile("" : "+v"(qh[k]));
+    if (TERMS == 3) asm volatile("" : "+v"(ql[k]));
+  }
+  barrier();
+  if (n > 0) read_k(0);
+  // C(-1) lands K(1) (and V(0)); the segment loop's barriers make them visible to the group
+
+  // both groups run the same loop [C(j-1) | V(j)], a barrier after each segment; group 1 first
+  // passes one extra barrier (and group 0 one after the loop), so it runs one segment behind:
+  // group 0's C segments meet group 1's V segments and vice versa
+  if (grp == 1) barrier();
+  for (int j = 0; j <= nA; ++j) {
+    seg_c(j - 1);
+    barrier();
+    seg_v(j);
+    barrier();
+  }
+  if (grp == 0) barrier();
+
+  // merge: group 1 publishes (O, m, l) per lane, group 0 combines and writes the context
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  float* mg = reinterpret_cast<float*>(lds + MERGE_OFF) + gw * 34 * 64;
+  if (grp == 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      mg[r * 64 + lane] = o0[r];
+      mg[(16 + r) * 64 + lane] = o1[r];
+    }
+    mg[32 * 64 + lane] = m_run;
+    mg[33 * 64 + lane] = l_tot;
+  }
+  barrier();
+  if (grp == 1) return;
+  const float mb = mg[32 * 64 + lane], lb = mg[33 * 64 + lane];
+  const float mm = fmaxf(m_run, mb);
+  // -inf - -inf cannot occur: group 0 always has a tile, so m_run is finite
+  const float fa = __builtin_amdgcn_exp2f(m_run - mm), fb = __builtin_amdgcn_exp2f(mb - mm);
+  const float lt = l_tot * fa + lb * fb;
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  const float ca = fa * inv, cbf = fb * inv;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    o0[r] = o0[r] * ca + mg[r * 64 + lane] * cbf;
+    o1[r] = o1[r] * ca + mg[(16 + r) * 64 + lane] * cbf;
+  }
+  // context through LDS (PIPE 6's epilogue; the staging area is group 0's ring, nothing reads
+  // it any more), 16-B stores of whole output chunks
+  constexpr int S6 = 66;
+  float* os6 = reinterpret_cast<float*>(lds) + gw * 32 * S6;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int d = mfma32_row(r, lh);
+    os6[li * S6 + d] = o0[r];
+    os6[li * S6 + 32 + d] = o1[r];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  constexpr int CPR = PLANES ? 8 * NP : 16;
+  constexpr int RPI = 64 / CPR;
+  const int c = lane % CPR;
+#pragma unroll
+  for (int it = 0; it < 32 / RPI; ++it) {
+    const int rr = it * RPI + lane / CPR;
+    const int qq = qb * QPB + gw * 32 + rr;
+    const float* src = os6 + rr * S6;
+    if (PLANES) {
+      const int d0 = 32 * (c / (4 * NP)) + 8 * (c % 4);
+      const bool lo_plane = NP == 2 && ((c >> 2) & 1);
+      uint32_t w[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const floatx2 v = *reinterpret_cast<const floatx2*>(src + d0 + 2 * e);
+        const __bf16 hx = (__bf16)v.x, hy = (__bf16)v.y;
+        bf16x2 pr;
+        if (lo_plane) pr = bf16x2{(__bf16)(v.x - (float)hx), (__bf16)(v.y - (float)hy)};
+        else pr = bf16x2{hx, hy};
+        w[e] = __builtin_bit_cast(uint32_t, pr);
+      }
+      if (qq < nq) {
+        unsigned short* dst = op + (size_t)(start + qq) * NP * AE_HIDDEN + head * 64 * NP + c * 8;
+        *reinterpret_cast<u32x4*>(dst) = u32x4{w[0], w[1], w[2], w[3]};
+      }
+    } else {
+      const floatx2 a = *reinterpret_cast<const floatx2*>(src + 4 * c);
+      const floatx2 b = *reinterpret_cast<const floatx2*>(src + 4 * c + 2);
+      if (qq < nq)
+        *reinterpret_cast<floatx4*>(out + (size_t)(start + qq) * AE_HIDDEN + head * AE_HEAD_DIM + 4 * c) =
+            floatx4{a.x, a.y, b.x, b.y};
+    }
+  }
+}
+
 // qkvp: packed planes [T][np·2304] with Q pre-scaled by log2(e)/8; context to op (packed planes)
 // or out (f32 [T, 768]).  q_rows / max_q: the CLS-only launch of the last layer.
 namespace {
@@ -566,7 +893,7 @@ hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op
   if (np != 1 && np != 2) return hipErrorInvalidValue;
   dim3 grid((max_q + QPB - 1) / QPB, heads, n), block(256);
 #define APP_LAUNCH(N, M, PL)                                                                 \
-  hipLaunchKernelGGL((attn_pp_kernel<N, M, PL, (M && PIPE == 6) ? 4 : PIPE>), grid, block, 0,      \
+  hipLaunchKernelGGL((attn_pp_kernel<N, M, PL, (M && PIPE >= 6) ? 4 : (PIPE == 7 ? 6 : PIPE)>), grid, block, 0,      \
                      stream, qkvp, out, op, cu,                                                 \
                      q_rows, mask, mask_L)
 #define APP_MP(N)                                                      \
@@ -574,6 +901,17 @@ hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op
     if (mask) APP_LAUNCH(N, true, true); else APP_LAUNCH(N, false, true);   \
   } else {                                                             \
     if (mask) APP_LAUNCH(N, true, false); else APP_LAUNCH(N, false, false); \
+  }
+  if (PIPE == 7 && !mask) {  // the 8-wave ping-pong kernel (no mask path: masks run PIPE 4)
+    dim3 block8(512);
+    if (np == 2) {
+      if (op) hipLaunchKernelGGL((attn_pp8_kernel<2, true>), grid, block8, 0, stream, qkvp, out, op, cu, q_rows);
+      else hipLaunchKernelGGL((attn_pp8_kernel<2, false>), grid, block8, 0, stream, qkvp, out, op, cu, q_rows);
+    } else {
+      if (op) hipLaunchKernelGGL((attn_pp8_kernel<1, true>), grid, block8, 0, stream, qkvp, out, op, cu, q_rows);
+      else hipLaunchKernelGGL((attn_pp8_kernel<1, false>), grid, block8, 0, stream, qkvp, out, op, cu, q_rows);
+    }
+    return hipGetLastError();
   }
   if (np == 2) {
     APP_MP(2)
@@ -601,14 +939,17 @@ extern "C" hipError_t ae_launch_attention_pp(const unsigned short* qkvp, float* 
 
 // Kernel experiments (tools/attn_bench.py, tests): variant 0 = two-stage loop, 1 = pipelined,
 // 2 = pipelined with the packed / branch-free tile (PIPE 2 above), 3 = 2 without the
-// interleave hints, 4 = the production loop (rounded split, branch-free rescale, interleave
-// hints), 5 = 4 at three workgroups per CU.
+// interleave hints, 4 = the previous production loop (rounded split, branch-free rescale,
+// interleave hints), 5 = 4 at three workgroups per CU, 6 = the production loop (3-slot rings,
+// deferred rescale), 7 = attn_pp8_kernel (8-wave ping-pong, keys split over two groups).
 // (An XCD-aware workgroup order — the q-blocks of one (sequence, head) on one XCD — measured 2-3 %
 // slower, profiles/r2i_attn_pp_ab.jsonl: the K/V re-reads are Infinity-Cache hits, not the bound.)
 extern "C" hipError_t ae_bench_attention_pp(const unsigned short* qkvp, float* out,
                                             unsigned short* op, const int* cu, const int* q_rows,
                                             int max_q, int n, int heads, const uint32_t* mask,
                                             int mask_L, int np, int variant, hipStream_t stream) {
+  if (variant == 7)
+    return app_launch<7>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
   if (variant == 6)
     return app_launch<6>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
   if (variant == 5)

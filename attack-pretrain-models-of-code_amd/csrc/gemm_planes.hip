@@ -456,7 +456,10 @@ __device__ __forceinline__ void pp_wait_vm() {
 // the prologue, 2 = no MFMAs, 3 = no fragment reads after K-tile 0, 4 = no epilogue, 5 = no
 // vmcnt waits in the loop, 6 = MFMAs + barriers only (no DMA / reads / waits after K-tile 0),
 // 7 = MFMAs only (6 without barriers); 8 = plain (not non-temporal) epilogue stores, results
-// exact.  Production instantiations have DIAG = 0.
+// exact; 9 (PP_PERSIST) = the production kernel on a persistent grid, results exact (measured
+// FFN1 392.5 -> 397.9 us, QKV 295.8 -> 291.1 us, profiles/r3q_gemm_persistent_ab.jsonl: workgroup
+// turnover is not what the epilogue costs, so the production grid stays one workgroup per
+// tile).  Production instantiations have DIAG = 0.
 template <int NP, int EPI, int DIAG>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
     const __bf16* __restrict__ A, const __bf16* __restrict__ W, const float* __restrict__ bias,
@@ -471,7 +474,12 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
 
   const int tiles_n = (N + BN - 1) / BN;
   const int tiles_m = (M + BM - 1) / BM;
-  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  // persistent when the grid is smaller than the tile count (pp_launch): workgroup w takes the
+  // virtual blocks w, w + grid, ... — the same tiles, XCD and order as one block per tile — so a
+  // CU goes from one tile's epilogue straight into the next tile's prologue, with no workgroup
+  // retire / dispatch between them
+  for (int vb = blockIdx.x; vb < tiles_m * tiles_n; vb += gridDim.x) {
+  const int t = xcd_remap(vb, tiles_m * tiles_n);
   const int per_group = group_m * tiles_n;
   const int g = t / per_group, first_m = g * group_m;
   const int gsize = min(tiles_m - first_m, group_m);
@@ -645,7 +653,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
     mfma_quad(1, 0, std::integral_constant<int, 1>(), next2, kt + 2);
     sync_load();
   }
-  if (DIAG != 0 && DIAG != 8) pp_wait_vm<0>();
+  if (DIAG != 0 && DIAG != 8 && DIAG != 9) pp_wait_vm<0>();
   if (wm == 0) sync_load();
   if (DIAG == 7) __builtin_amdgcn_s_barrier();  // same barrier count in both groups; every LDS read and DMA done
   if (DIAG == 4) {
@@ -655,7 +663,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
       for (int b = 0; b < 2; ++b)
 #pragma unroll
         for (int r = 0; r < 16; ++r) keep_f32(acc[a][b][r]);
-    return;
+    continue;
   }
 
   // ---- epilogue.  acc[tm][tn] register 4 j + i of lane l = output row wm*128 + tm*32 + (l & 31),
@@ -748,6 +756,13 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // region reads done before it is rewritten
   }
+  // every wave's staging reads done before the next tile's prologue DMA rewrites the stages
+  // (raw barrier: the epilogue's stores stay in flight)
+  if constexpr (DIAG != 9) break;  // one tile per workgroup: no loop-carried state
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  }  // tile loop
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1188,6 +1203,10 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
 }
 
 namespace {
+int cu_count();
+// DIAG value of the persistent launch (exact results): one workgroup per CU looping over tiles
+constexpr int PP_PERSIST = 9;
+
 template <int NP, int EPI, int DIAG>
 hipError_t pp_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R, float* C,
                      __bf16* Cp, int M, int N, int K, int group_m, hipStream_t st) {
@@ -1195,7 +1214,9 @@ hipError_t pp_launch(const __bf16* A, const __bf16* W, const float* bias, const 
   if (hipError_t e = ensure_dynamic_lds((const void*)gemm_pp_kernel<NP, EPI, DIAG>, lds); e != hipSuccess)
     return e;
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
-  hipLaunchKernelGGL((gemm_pp_kernel<NP, EPI, DIAG>), dim3(tiles), dim3(512), lds, st, A, W, bias,
+  // persistent grid (one workgroup per CU looping over the tiles) or one workgroup per tile
+  const int grid = DIAG == PP_PERSIST ? std::min(tiles, cu_count()) : tiles;
+  hipLaunchKernelGGL((gemm_pp_kernel<NP, EPI, DIAG>), dim3(grid), dim3(512), lds, st, A, W, bias,
                      R, C, Cp, M, N, K, group_m);
   return hipGetLastError();
 }
@@ -1203,22 +1224,23 @@ hipError_t pp_launch(const __bf16* A, const __bf16* W, const float* bias, const 
 template <int NP, int DIAG>
 hipError_t pp_epi(int epi, const __bf16* A, const __bf16* W, const float* bias, const float* R,
                   float* C, __bf16* Cp, int M, int N, int K, int group_m, hipStream_t st) {
-  if constexpr (DIAG != 0) {  // diagnostic builds: split-bf16, bias / GELU epilogues only
+  if constexpr (DIAG != 0 && DIAG != PP_PERSIST) {  // diagnostic builds: split-bf16, bias / GELU only
     if (NP != 2 || (epi != PK_EPI_BIAS && epi != PK_EPI_GELU_PACKED)) return hipErrorInvalidValue;
     if (epi == PK_EPI_BIAS)
       return pp_launch<2, PK_EPI_BIAS, DIAG>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
     return pp_launch<2, PK_EPI_GELU_PACKED, DIAG>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
-  }
-  switch (epi) {
-    case PK_EPI_BIAS:
-      return pp_launch<NP, PK_EPI_BIAS, 0>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
-    case PK_EPI_GELU_PACKED:
-      return pp_launch<NP, PK_EPI_GELU_PACKED, 0>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
-    case PK_EPI_BIAS_PACKED:
-      return pp_launch<NP, PK_EPI_BIAS_PACKED, 0>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
-    case PK_EPI_RES:
-      return pp_launch<NP, PK_EPI_RES, 0>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
-    default: return pp_launch<NP, PK_EPI_TANH, 0>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
+  } else {
+    switch (epi) {
+      case PK_EPI_BIAS:
+        return pp_launch<NP, PK_EPI_BIAS, DIAG>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
+      case PK_EPI_GELU_PACKED:
+        return pp_launch<NP, PK_EPI_GELU_PACKED, DIAG>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
+      case PK_EPI_BIAS_PACKED:
+        return pp_launch<NP, PK_EPI_BIAS_PACKED, DIAG>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
+      case PK_EPI_RES:
+        return pp_launch<NP, PK_EPI_RES, DIAG>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
+      default: return pp_launch<NP, PK_EPI_TANH, DIAG>(A, W, bias, R, C, Cp, M, N, K, group_m, st);
+    }
   }
 }
 
@@ -1442,6 +1464,7 @@ extern "C" hipError_t ae_bench_gemm_packed(const unsigned short* A, const unsign
       case 6: return pp_dispatch<6>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
       case 7: return pp_dispatch<7>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
       case 8: return pp_dispatch<8>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
+      case 9: return pp_dispatch<9>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
       default: return hipErrorInvalidValue;
     }
   }

@@ -202,11 +202,11 @@ def run_sharded_mhm(model, codes, subs, labels, args, n_candi=30, max_iter=100, 
 
 
 def run_sharded_substitutes(gen, in_path, out_path, start=0, end=None, device=None,
-                            deadline: float | None = None):
+                            deadline: float | None = None, log=None):
     """get_substitutes.py over all ranks (examples across ranks, jsonl merged by
     index): every rank pulls item indices from the shared queue and writes its shard
     `<out_path>.rank<r>`; rank 0 merges the shards into `out_path` in input order.  Returns the
-    job totals (all-gathered)."""
+    job totals (all-gathered).  log(idx, item): called after each item this rank finishes."""
     import torch.distributed as dist
 
     from .substitutes import generate_file, merge_shards
@@ -221,7 +221,7 @@ def run_sharded_substitutes(gen, in_path, out_path, start=0, end=None, device=No
     q = DynamicQueue(n_items, key=call_key("apmc_subs_queue"), deadline=deadline)
     shard = f"{out_path}.rank{rank}"
     t0 = time.time()
-    out = generate_file(gen, in_path, shard, start, end, queue=q)
+    out = generate_file(gen, in_path, shard, start, end, queue=q, log=log)
     wall = time.time() - t0
     st = gather_stats([out["items"], out["occurrences"], out["encoded_seqs"],
                        out["encoded_tokens"], wall], device=device)

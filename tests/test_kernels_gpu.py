@@ -67,6 +67,10 @@ def _p(t):
     (700, 256, 256, 1, 1, "512"),
     (64, 2304, 768, 2, 3, "512"),
     (600, 3072, 768, 2, 1, "512"),
+    # the same kernel on a persistent grid (one workgroup per CU looping over > 256 tiles)
+    (8192, 2304, 256, 2, 0, "512p"),
+    (8200, 3072, 128, 2, 1, "512p"),
+    (2000, 768, 192, 1, 2, "512p"),
     # ping-pong 256 x 192 kernel (f32 epilogues): ragged M / N, short and long K
     (300, 768, 128, 2, 0, "192"),
     (512, 768, 768, 2, 2, "192"),
@@ -115,9 +119,10 @@ def test_gemm_packed_matches_split_products(gpu, M, N, K, np_, epi, bn):
         lib.ae_launch_gemm_w2.restype = ctypes.c_int
         rc = lib.ae_launch_gemm_w2(_p(dA), _p(dW), _p(db), _p(dR), _p(C), _p(Cp), M, N, K, epi,
                                    np_, 4, st)
-    elif bn:  # explicit tile width through the experiment entry point (production kernel, diag 0)
+    elif bn:  # explicit tile width through the experiment entry point (production kernel, diag 0;
+        # "512p": diag 9, the persistent grid)
         rc = lib.ae_bench_gemm_packed(_p(dA), _p(dW), _p(db), _p(dR), _p(C), _p(Cp), M, N, K, epi,
-                                      np_, int(bn), 0, st)
+                                      np_, int(bn.rstrip("p")), 9 if bn.endswith("p") else 0, st)
     else:
         rc = lib.ae_launch_gemm_packed(_p(dA), _p(dW), _p(db), _p(dR), _p(C), _p(Cp), M, N, K,
                                        epi, np_, st)
@@ -219,13 +224,14 @@ def _qkv_planes(qkv, np_):
     return _pack(hi, lo, np_)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("np_", [2, 1])
 @pytest.mark.parametrize("case", ["ragged", "mask", "cls", "planes", "grow"])
 def test_attention_pp_matches_f64(gpu, np_, case, variant):
     """attn_pp_kernel (packed-plane Q/K/V moved by LDS-DMA, swizzled K/V images, transposed V
     reads) against the float64 reference, for both plane counts (np 1 = bf16 mode: stated
-    tolerance 2e-2), every loop (1: software-pipelined, 6: 3-slot rings + deferred rescale) and
+    tolerance 2e-2), every loop (1: software-pipelined, 6: 3-slot rings + deferred rescale, 7: the
+    8-wave ping-pong kernel with the keys split between its two groups and merged) and
     the ragged / mask / CLS-only / packed-output launches.  "grow": spike keys whose scores
     rise along the sequence, so every row max jumps past the deferred-rescale threshold (2^8)
     several times — the rare branch of variant 6."""

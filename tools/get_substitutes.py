@@ -53,9 +53,17 @@ def main():
     gen = SubstituteGenerator(eng, tok, block_size=args.block_size, lang=args.lang,
                               cosine=not args.no_cosine)
     t0 = time.time()
+    done = [0]
+
+    def progress(idx, item):  # a line a minute or so: long runs stay visibly alive
+        done[0] += 1
+        if done[0] % 50 == 0:
+            print(f"[get_substitutes] {done[0]} items ({idx}) in {time.time() - t0:.0f} s",
+                  file=sys.stderr, flush=True)
+
     tot = run_sharded_substitutes(gen, args.eval_data_file, args.store_path,
                                   int(args.index[0]), int(args.index[1]),
-                                  device=torch.device(f"cuda:{local}"))
+                                  device=torch.device(f"cuda:{local}"), log=progress)
     if dist is None or dist.get_rank() == 0:
         print(f"{tot['items']} items, {tot['occurrences']} occurrences, "
               f"{tot['encoded_seqs']} re-encoded sequences in {time.time() - t0:.1f} s")
