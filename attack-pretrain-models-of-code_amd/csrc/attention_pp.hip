@@ -882,6 +882,318 @@ __global__ __launch_bounds__(512, 1) void attn_pp8_kernel(const unsigned short* 
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// attn_pw64_kernel (variant 8): one wave per SIMD, 64 queries per wave (two 32-query blocks),
+// 4 waves = 256 queries per workgroup, one workgroup per CU (cdna_hip_programming.md's
+// "pwg4x64" structure): each K fragment read from LDS serves both query blocks' S MFMAs and each
+// V fragment both blocks' PV MFMAs (half the LDS reads per query), and a wave's 48 MFMAs per key
+// tile are independent chains of two blocks whose issue gaps take the other block's softmax VALU
+// — latency is hidden inside the wave instead of by a second, uncoordinated wave on the SIMD.
+// Rings, waits and the deferred rescale are PIPE 6's; registers: up to 512 per wave.
+template <int NP, bool PLANES>
+__global__ __launch_bounds__(256, 1) void attn_pw64_kernel(const unsigned short* __restrict__ qkvp,
+                                                           float* __restrict__ out,
+                                                           unsigned short* __restrict__ op,
+                                                           const int* __restrict__ cu,
+                                                           const int* __restrict__ q_rows) {
+  using P = PPL<NP>;
+  constexpr int TERMS = NP == 2 ? 3 : 1;
+  constexpr int QW = 256;  // queries per workgroup
+  constexpr int LDS_BYTES = 6 * P::TILE > 4 * 32 * 66 * 4 ? 6 * P::TILE : 4 * 32 * 66 * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
+  const int seq = blockIdx.z, head = blockIdx.y, qb = blockIdx.x;
+  const int start = cu[seq];
+  const int len = cu[seq + 1] - start;
+  const int nq = q_rows ? min(len, q_rows[0]) : len;
+  if (qb * QW >= nq) return;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 31, lh = lane >> 5;
+  constexpr size_t LDR = (size_t)NP * QKV_COLS;
+
+  // Q fragments of the two blocks (b = 0, 1: queries qb*256 + wave*64 + 32 b + li)
+  bf16x8 qh[2][4], ql[2][4];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int q = qb * QW + wave * 64 + 32 * b + li;
+    const int qr = q < nq ? q : nq - 1;
+    const unsigned short* qp = qkvp + (size_t)(start + qr) * LDR + (size_t)head * 64 * NP;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int d = 16 * s + 8 * lh;
+      const int off = (d >> 5) * 32 * NP + (d & 31);
+      qh[b][s] = *reinterpret_cast<const bf16x8*>(qp + off);
+      if (TERMS == 3) ql[b][s] = *reinterpret_cast<const bf16x8*>(qp + off + 32);
+    }
+  }
+
+  const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
+  const int dr = lane / P::CR, dc = lane % P::CR;
+  auto issue1 = [&](int kt, int moff, uint32_t dst, bool vimg) {
+#pragma unroll
+    for (int j = 0; j < P::DMA_PER_WAVE; ++j) {
+      const int i = wave * P::DMA_PER_WAVE + j;
+      const int r = i * P::ROWS_PER_DMA + dr;
+      int key = kt * KT + r;
+      key = key < len ? key : len - 1;
+      const unsigned short* row = qkvp + (size_t)(start + key) * LDR;
+      dma16(row + (size_t)(moff + head * 64) * NP + (vimg ? vpos<NP>(r, dc) : kpos<NP>(r, dc)) * 8,
+            dst + i * 1024);
+    }
+  };
+  auto wait_vm = [](int n) {
+    if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  auto barrier = []() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  constexpr int DM = P::DMA_PER_WAVE;
+
+  floatx16 o[2][2];  // [block][d tile]
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { o[b][0][r] = 0.f; o[b][1][r] = 0.f; }
+  float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
+
+  // S^T of both blocks from one read of the K fragments
+  auto s_mfma = [&](const unsigned char* stk, floatx16 (&s)[2]) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[b][r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int d0 = 16 * ks + 8 * lh;
+      const unsigned char* kr = stk + li * P::RB;
+      const bf16x8 kh = *reinterpret_cast<const bf16x8*>(kr + kpos<NP>(li, chunk_of<NP>(0, d0)) * 16);
+      bf16x8 kl;
+      if (TERMS == 3) kl = *reinterpret_cast<const bf16x8*>(kr + kpos<NP>(li, chunk_of<NP>(1, d0)) * 16);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        if (TERMS == 3) {
+          s[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl, qh[b][ks], s[b], 0, 0, 0);
+          s[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, ql[b][ks], s[b], 0, 0, 0);
+        }
+        s[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, qh[b][ks], s[b], 0, 0, 0);
+      }
+    }
+  };
+  // O^T += V^T P^T for both blocks from one read of each V fragment
+  auto pv_mfma = [&](const unsigned char* stv, const bf16x8 (&ph)[2][2], const bf16x8 (&pl)[2][2]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int kq = 16 * t + 4 * lh + ((lane >> 2) & 3);
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int col = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+        const int cb = (col & 7) * 2;
+        const unsigned char* va = stv + kq * P::RB + cb;
+        const unsigned char* vb = stv + (kq + 8) * P::RB + cb;
+        bf16x8 vh, vl;
+        {
+          const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)(va + vpos<NP>(kq, chunk_of<NP>(0, col)) * 16));
+          const bf16x4 c = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)(vb + vpos<NP>(kq + 8, chunk_of<NP>(0, col)) * 16));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { vh[e] = a[e]; vh[4 + e] = c[e]; }
+        }
+        if (TERMS == 3) {
+          const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)(va + vpos<NP>(kq, chunk_of<NP>(1, col)) * 16));
+          const bf16x4 c = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)(vb + vpos<NP>(kq + 8, chunk_of<NP>(1, col)) * 16));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { vl[e] = a[e]; vl[4 + e] = c[e]; }
+        }
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          if (TERMS == 3) {
+            o[b][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl, ph[b][t], o[b][dt], 0, 0, 0);
+            o[b][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, pl[b][t], o[b][dt], 0, 0, 0);
+          }
+          o[b][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, ph[b][t], o[b][dt], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  const int nkt = (len + KT - 1) / KT;
+  auto kslot = [&](int j) { return (uint32_t)(j * P::TILE); };
+  auto vslot = [&](int j) { return (uint32_t)((3 + j) * P::TILE); };
+  int groups = 2;
+  issue1(0, AE_HIDDEN, lds0 + kslot(0), false);
+  issue1(0, 2 * AE_HIDDEN, lds0 + vslot(0), true);
+  if (nkt > 1) {
+    issue1(1, AE_HIDDEN, lds0 + kslot(1), false);
+    issue1(1, 2 * AE_HIDDEN, lds0 + vslot(1), true);
+    groups += 2;
+  }
+  if (nkt > 2) {
+    issue1(2, AE_HIDDEN, lds0 + kslot(2), false);
+    ++groups;
+  }
+  wait_vm(DM * (groups - 1));
+  // Q through an empty asm: hipcc waits for its loads here once, not inside the loop
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      asm volatile("" : "+v"(qh[b][k]));
+      if (TERMS == 3) asm volatile("" : "+v"(ql[b][k]));
+    }
+  barrier();
+  floatx16 sA[2], sB[2];
+  s_mfma(lds + kslot(0), sA);
+  wait_vm(nkt > 1 ? DM * (groups - 3) : 0);
+  barrier();
+
+  auto body = [&](auto rc, int kt, floatx16 (&s_cur)[2], floatx16 (&s_next)[2]) {
+    constexpr int R = decltype(rc)::value;
+    constexpr uint32_t KS_NEXT = ((R + 1) % 3) * P::TILE, VS_CUR = (3 + R % 3) * P::TILE;
+    constexpr uint32_t VS_ISS = (3 + (R + 2) % 3) * P::TILE, KS_ISS = (R % 3) * P::TILE;
+    int n_iss = 0;
+    if (kt + 2 < nkt) {
+      issue1(kt + 2, 2 * AE_HIDDEN, lds0 + VS_ISS, true);
+      n_iss += DM;
+    }
+    if (kt + 3 < nkt) {
+      issue1(kt + 3, AE_HIDDEN, lds0 + KS_ISS, false);
+      n_iss += DM;
+    }
+    const bool full = (kt + 1) * KT <= len;
+    float m_new[2], alpha[2];
+    bool grow[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      float mt = -INFINITY;
+      if (full) {
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) mt = fmaxf(mt, fmaxf(s_cur[b][r], s_cur[b][r + 1]));
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const bool in = kt * KT + mfma32_row(r, lh) < len;
+          s_cur[b][r] = in ? s_cur[b][r] : -INFINITY;
+          mt = fmaxf(mt, s_cur[b][r]);
+        }
+      }
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      grow[b] = __any(mt > m_run[b] + 8.f);
+      m_new[b] = grow[b] ? fmaxf(m_run[b], mt) : m_run[b];
+      alpha[b] = __builtin_amdgcn_exp2f(m_run[b] - m_new[b]);
+    }
+    bf16x8 ph[2][2], pl[2][2];
+    float psum[2] = {0.f, 0.f};
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(s_cur[b][r] - m_new[b]);
+        psum[b] += p;
+        const __bf16 h = (__bf16)p;
+        ph[b][r >> 3][r & 7] = h;
+        pl[b][r >> 3][r & 7] = (__bf16)(p - (float)h);
+      }
+    s_mfma(lds + KS_NEXT, s_next);
+    // K fragment reads first, then one S MFMA per ~7 vector instructions
+    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+    for (int i = 0; i < 24; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      l_run[b] = l_run[b] * alpha[b] + psum[b];
+      m_run[b] = m_new[b];
+    }
+    if (grow[0] || grow[1]) {
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { o[b][0][r] *= alpha[b]; o[b][1][r] *= alpha[b]; }
+    }
+    pv_mfma(lds + VS_CUR, ph, pl);
+    wait_vm(n_iss);
+    barrier();
+  };
+  for (int kt = 0; kt < nkt; kt += 6) {
+    body(std::integral_constant<int, 0>(), kt, sA, sB);
+    if (kt + 1 >= nkt) break;
+    body(std::integral_constant<int, 1>(), kt + 1, sB, sA);
+    if (kt + 2 >= nkt) break;
+    body(std::integral_constant<int, 2>(), kt + 2, sA, sB);
+    if (kt + 3 >= nkt) break;
+    body(std::integral_constant<int, 3>(), kt + 3, sB, sA);
+    if (kt + 4 >= nkt) break;
+    body(std::integral_constant<int, 4>(), kt + 4, sA, sB);
+    if (kt + 5 >= nkt) break;
+    body(std::integral_constant<int, 5>(), kt + 5, sB, sA);
+  }
+
+  // context: per block through the wave's LDS rows (66 floats), 16-B stores of whole chunks
+  constexpr int S6 = 66;
+  float* os6 = reinterpret_cast<float*>(lds) + wave * 32 * S6;
+  constexpr int CPR = PLANES ? 8 * NP : 16;
+  constexpr int RPI = 64 / CPR;
+  const int c = lane % CPR;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const float l_tot = l_run[b] + __shfl_xor(l_run[b], 32, 64);
+    const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int d = mfma32_row(r, lh);
+      os6[li * S6 + d] = o[b][0][r] * inv;
+      os6[li * S6 + 32 + d] = o[b][1][r] * inv;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int it = 0; it < 32 / RPI; ++it) {
+      const int rr = it * RPI + lane / CPR;
+      const int qq = qb * QW + wave * 64 + 32 * b + rr;
+      const float* src = os6 + rr * S6;
+      if (PLANES) {
+        const int d0 = 32 * (c / (4 * NP)) + 8 * (c % 4);
+        const bool lo_plane = NP == 2 && ((c >> 2) & 1);
+        uint32_t w[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const floatx2 v = *reinterpret_cast<const floatx2*>(src + d0 + 2 * e);
+          const __bf16 hx = (__bf16)v.x, hy = (__bf16)v.y;
+          bf16x2 pr;
+          if (lo_plane) pr = bf16x2{(__bf16)(v.x - (float)hx), (__bf16)(v.y - (float)hy)};
+          else pr = bf16x2{hx, hy};
+          w[e] = __builtin_bit_cast(uint32_t, pr);
+        }
+        if (qq < nq) {
+          unsigned short* dst = op + (size_t)(start + qq) * NP * AE_HIDDEN + head * 64 * NP + c * 8;
+          *reinterpret_cast<u32x4*>(dst) = u32x4{w[0], w[1], w[2], w[3]};
+        }
+      } else {
+        const floatx2 a = *reinterpret_cast<const floatx2*>(src + 4 * c);
+        const floatx2 b2 = *reinterpret_cast<const floatx2*>(src + 4 * c + 2);
+        if (qq < nq)
+          *reinterpret_cast<floatx4*>(out + (size_t)(start + qq) * AE_HIDDEN + head * AE_HEAD_DIM + 4 * c) =
+              floatx4{a.x, a.y, b2.x, b2.y};
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // block 0's rows read before block 1's land
+  }
+}
+
 // qkvp: packed planes [T][np·2304] with Q pre-scaled by log2(e)/8; context to op (packed planes)
 // or out (f32 [T, 768]).  q_rows / max_q: the CLS-only launch of the last layer.
 namespace {
@@ -893,7 +1205,7 @@ hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op
   if (np != 1 && np != 2) return hipErrorInvalidValue;
   dim3 grid((max_q + QPB - 1) / QPB, heads, n), block(256);
 #define APP_LAUNCH(N, M, PL)                                                                 \
-  hipLaunchKernelGGL((attn_pp_kernel<N, M, PL, (M && PIPE >= 6) ? 4 : (PIPE == 7 ? 6 : PIPE)>), grid, block, 0,      \
+  hipLaunchKernelGGL((attn_pp_kernel<N, M, PL, (M && PIPE >= 6) ? 4 : (PIPE >= 7 ? 6 : PIPE)>), grid, block, 0,      \
                      stream, qkvp, out, op, cu,                                                 \
                      q_rows, mask, mask_L)
 #define APP_MP(N)                                                      \
@@ -901,6 +1213,17 @@ hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op
     if (mask) APP_LAUNCH(N, true, true); else APP_LAUNCH(N, false, true);   \
   } else {                                                             \
     if (mask) APP_LAUNCH(N, true, false); else APP_LAUNCH(N, false, false); \
+  }
+  if (PIPE == 8 && !mask) {  // 4 waves x 64 queries (no mask path: masks run PIPE 4)
+    dim3 grid8((max_q + 255) / 256, heads, n);
+    if (np == 2) {
+      if (op) hipLaunchKernelGGL((attn_pw64_kernel<2, true>), grid8, block, 0, stream, qkvp, out, op, cu, q_rows);
+      else hipLaunchKernelGGL((attn_pw64_kernel<2, false>), grid8, block, 0, stream, qkvp, out, op, cu, q_rows);
+    } else {
+      if (op) hipLaunchKernelGGL((attn_pw64_kernel<1, true>), grid8, block, 0, stream, qkvp, out, op, cu, q_rows);
+      else hipLaunchKernelGGL((attn_pw64_kernel<1, false>), grid8, block, 0, stream, qkvp, out, op, cu, q_rows);
+    }
+    return hipGetLastError();
   }
   if (PIPE == 7 && !mask) {  // the 8-wave ping-pong kernel (no mask path: masks run PIPE 4)
     dim3 block8(512);
@@ -948,6 +1271,8 @@ extern "C" hipError_t ae_bench_attention_pp(const unsigned short* qkvp, float* o
                                             unsigned short* op, const int* cu, const int* q_rows,
                                             int max_q, int n, int heads, const uint32_t* mask,
                                             int mask_L, int np, int variant, hipStream_t stream) {
+  if (variant == 8)
+    return app_launch<8>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
   if (variant == 7)
     return app_launch<7>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
   if (variant == 6)

@@ -124,6 +124,14 @@ struct ae_engine {
   int* pinned_cu = nullptr;
   size_t cap_pinned = 0;
   hipEvent_t pinned_ready = nullptr;
+  // two-stream encoder (split-precision modes; AE_SPLIT_STREAMS=0 at engine creation turns it
+  // off): the batch's sequences in two halves, each half's layers on its own stream, the second
+  // half one kernel behind, so one half's memory-bound phases (GEMM epilogues, LayerNorm) and
+  // tile-quantisation tails can run beside the other half's MFMA-bound main loops; LayerNorm as
+  // its own kernel (no cross-workgroup exchange, whose partners must be co-resident)
+  bool split = false;
+  hipStream_t st2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_lag = nullptr, ev_join = nullptr;
   // profiling: event pairs are created when profiling is switched on (never inside the timed
   // launches) and recycled by ae_kernel_time
   int prof_kind = -1;
@@ -352,11 +360,46 @@ int gemm_pk_ln(ae_engine* e, const unsigned short* A, const unsigned short* Wp, 
   return AE_OK;
 }
 
+// One full encoder layer of the split-precision path over the token rows [t0, t0 + M) of the
+// sequences [s0, s0 + ns) on stream st, with the residual + LayerNorm as their own kernels (the
+// two-stream encoder; results equal the fused path's to LayerNorm rounding).
+int layer_rows(ae_engine* e, const LayerW& w, int64_t t0, int M, int s0, int ns, int max_len,
+               const uint32_t* mask_bits, int L, hipStream_t st, hipEvent_t after_qkv = nullptr) {
+  const int H = e->cfg.hidden, F = e->cfg.ffn, np = e->np;
+  unsigned short* qkvp = reinterpret_cast<unsigned short*>(e->qkv);
+  unsigned short* xp = e->xp + t0 * H * np;
+  float* x = e->x + t0 * H;
+  float* tmp = e->tmp + t0 * H;
+  int rc;
+  if ((rc = gemm_pk(e, xp, w.wqkv_p, w.bqkv, nullptr, nullptr, qkvp + t0 * 3 * H * np, M, 3 * H, H,
+                    EPI_BIAS_PACKED, st, false)))
+    return rc;
+  if (after_qkv) HIPC(hipEventRecord(after_qkv, st));
+  {
+    Prof p(e, st, e->prof_kind == AE_KIND_ATTENTION, 0.0);
+    HIPC(ae_launch_attention_pp(qkvp, e->ctx, e->cp, e->cu + s0, nullptr, max_len, ns,
+                                e->cfg.heads, mask_bits ? mask_bits + (size_t)s0 * L * (L / 32) : nullptr,
+                                L, np, st));
+  }
+  if ((rc = gemm_pk(e, e->cp + t0 * H * np, w.wo_p, w.bo, x, tmp, nullptr, M, H, H,
+                    EPI_BIAS_RESIDUAL, st, false)))
+    return rc;
+  HIPC(ae_launch_layernorm(tmp, w.ln1g, w.ln1b, e->cfg.ln_eps, M, x, xp, np, st));
+  if ((rc = gemm_pk(e, xp, w.w1_p, w.b1, nullptr, nullptr, e->hp + t0 * F * np, M, F, H,
+                    EPI_BIAS_GELU, st, true)))
+    return rc;
+  if ((rc = gemm_pk(e, e->hp + t0 * F * np, w.w2_p, w.b2, x, tmp, nullptr, M, H, F,
+                    EPI_BIAS_RESIDUAL, st, false)))
+    return rc;
+  HIPC(ae_launch_layernorm(tmp, w.ln2g, w.ln2b, e->cfg.ln_eps, M, x, xp, np, st));
+  return AE_OK;
+}
+
 // Runs the encoder over compacted tokens; on return the last-layer CLS rows are in e->xc
-// (cls_only) or all rows in e->x.
+// (cls_only) or all rows in e->x.  lens: the host copy of the sequence lengths (two-stream mode).
 int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint32_t* mask_bits,
                 int n, int L, int64_t T, int max_len, bool cls_only, hipStream_t st,
-                int keep_all = 0, bool node_avg = false) {
+                int keep_all = 0, bool node_avg = false, const int32_t* lens = nullptr) {
   const int H = e->cfg.hidden, F = e->cfg.ffn, NL = e->cfg.layers, heads = e->cfg.heads;
   const float eps = e->cfg.ln_eps;
   HIPC(hipMemsetAsync(e->err, 0, sizeof(int), st));
@@ -367,7 +410,42 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
                           (int)T, e->cfg.max_pos, e->x, pl ? e->xp : nullptr, e->np,
                           node_avg ? mask_bits : nullptr, L, e->cu, n, st));
   unsigned short* qkvp = reinterpret_cast<unsigned short*>(e->qkv);  // planes mode: [T][np·3H]
-  for (int li = 0; li < NL; ++li) {
+  int first = 0;  // first layer the single-stream loop below runs
+  if (pl && e->split && lens) {
+    // full layers in two halves of the batch on two streams (one half when n == 1, so that every
+    // batch size runs the same per-row arithmetic)
+    const int NLs = cls_only ? NL - 1 : NL;
+    const int n0 = n >= 2 ? n / 2 : n;
+    const int64_t T0 = e->pinned_cu[n0];  // host prefix sums of the uploaded lens
+    int ml0 = 0, ml1 = 0;
+    for (int i = 0; i < n; ++i) {
+      if (i < n0) ml0 = lens[i] > ml0 ? lens[i] : ml0;
+      else ml1 = lens[i] > ml1 ? lens[i] : ml1;
+    }
+    const bool two = n0 < n;
+    if (two) {
+      HIPC(hipEventRecord(e->ev_fork, st));
+      HIPC(hipStreamWaitEvent(e->st2, e->ev_fork, 0));
+    }
+    for (int li = 0; li < NLs; ++li) {
+      const LayerW& w = e->layers[li];
+      int rc;
+      if ((rc = layer_rows(e, w, 0, (int)T0, 0, n0, ml0, mask_bits, L, st,
+                           two && li == 0 ? e->ev_lag : nullptr)))
+        return rc;
+      if (two) {
+        if (li == 0) HIPC(hipStreamWaitEvent(e->st2, e->ev_lag, 0));  // one kernel behind
+        if ((rc = layer_rows(e, w, T0, (int)(T - T0), n0, n - n0, ml1, mask_bits, L, e->st2)))
+          return rc;
+      }
+    }
+    if (two) {
+      HIPC(hipEventRecord(e->ev_join, e->st2));
+      HIPC(hipStreamWaitEvent(st, e->ev_join, 0));
+    }
+    first = NLs;
+  }
+  for (int li = first; li < NL; ++li) {
     const LayerW& w = e->layers[li];
     const bool last_cls = cls_only && li == NL - 1;
     int rc;
@@ -588,6 +666,18 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
   HIPC(hipMemcpy(e->one, one_host, 16, hipMemcpyHostToDevice));
   HIPC(hipEventCreateWithFlags(&e->pinned_ready, hipEventDisableTiming));
   HIPC(hipEventRecord(e->pinned_ready, nullptr));
+  if (e->planes) {
+    // on unless AE_SPLIT_STREAMS=0 (tools/split_ab.py, profiles/r3s_split_streams_ab.json:
+    // B=64 x L=512 16.58 -> 16.35 ms per step, ragged lens 40..512 11.36 -> 9.53 ms)
+    const char* sp = std::getenv("AE_SPLIT_STREAMS");
+    e->split = !(sp && sp[0] == '0');
+    if (e->split) {
+      HIPC(hipStreamCreateWithFlags(&e->st2, hipStreamNonBlocking));
+      HIPC(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
+      HIPC(hipEventCreateWithFlags(&e->ev_lag, hipEventDisableTiming));
+      HIPC(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
+    }
+  }
   HIPC(hipDeviceSynchronize());
   *out = e;
   return AE_OK;
@@ -601,6 +691,9 @@ int ae_destroy(ae_engine* e) {
     if (p) (void)hipFree(p);
   if (e->pinned_cu) (void)hipHostFree(e->pinned_cu);
   if (e->pinned_ready) (void)hipEventDestroy(e->pinned_ready);
+  for (hipEvent_t ev : {e->ev_fork, e->ev_lag, e->ev_join})
+    if (ev) (void)hipEventDestroy(ev);
+  if (e->st2) (void)hipStreamDestroy(e->st2);
   for (auto* v : {&e->prof, &e->prof_pool})
     for (auto& r : *v) {
       (void)hipEventDestroy(r.a);
@@ -644,7 +737,7 @@ static int score_impl(ae_engine* e, const int32_t* ids, const int32_t* lens, con
   int max_len = 0;
   for (int i = 0; i < n; ++i) max_len = lens[i] > max_len ? lens[i] : max_len;
   if ((rc = run_encoder(e, ids, pos, mask_bits, n, L, T, max_len, true, st, node_avg ? 1 : 0,
-                        node_avg)))
+                        node_avg, lens)))
     return rc;
   const int kind = e->cfg.head_kind == AE_HEAD_SIGMOID1 ? 0 : (e->cfg.head_kind == AE_HEAD_PAIR2 ? 2 : 1);
   const int n_out = kind == 2 ? n / 2 : n;
@@ -675,7 +768,7 @@ int ae_encode_ex(ae_engine* e, const int32_t* ids, const int32_t* lens, int32_t 
   int max_len = 0;
   for (int i = 0; i < n; ++i) max_len = lens[i] > max_len ? lens[i] : max_len;
   if ((rc = run_encoder(e, ids, nullptr, nullptr, n, L, T, max_len, false, st,
-                        (flags & AE_ENC_ATTEND_PAD) ? 1 : 0)))
+                        (flags & AE_ENC_ATTEND_PAD) ? 1 : 0, false, lens)))
     return rc;
   HIPC(ae_launch_scatter_rows(e->x, e->cu, e->src_col, n, row0, nrows, (int)T, hidden_out, e->err,
                               st));
