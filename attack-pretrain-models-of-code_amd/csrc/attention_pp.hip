@@ -890,6 +890,10 @@ __global__ __launch_bounds__(512, 1) void attn_pp8_kernel(const unsigned short* 
 // tile are independent chains of two blocks whose issue gaps take the other block's softmax VALU
 // — latency is hidden inside the wave instead of by a second, uncoordinated wave on the SIMD.
 // Rings, waits and the deferred rescale are PIPE 6's; registers: up to 512 per wave.
+// Measured SLOWER than PIPE 6 (B=64 x L=512, same box: 273.0 vs 175.1 us,
+// profiles/r3r_attn_pw64_ab.jsonl), correct (tests/test_kernels_gpu.py variant 8): the body needs
+// 355 registers, 160 AGPR <-> VGPR moves per tile come with them, and a lone wave per SIMD
+// exposes every dependency the interleave cannot cover.  Kept as an experiment (variant 8).
 template <int NP, bool PLANES>
 __global__ __launch_bounds__(256, 1) void attn_pw64_kernel(const unsigned short* __restrict__ qkvp,
                                                            float* __restrict__ out,
