@@ -130,6 +130,7 @@ struct ae_engine {
   // tile-quantisation tails can run beside the other half's MFMA-bound main loops; LayerNorm as
   // its own kernel (no cross-workgroup exchange, whose partners must be co-resident)
   bool split = false;
+  int split_lag = 1;  // the second half starts after this many of the first half's layer-0 kernels
   hipStream_t st2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_lag = nullptr, ev_join = nullptr;
   // profiling: event pairs are created when profiling is switched on (never inside the timed
@@ -364,35 +365,42 @@ int gemm_pk_ln(ae_engine* e, const unsigned short* A, const unsigned short* Wp, 
 // sequences [s0, s0 + ns) on stream st, with the residual + LayerNorm as their own kernels (the
 // two-stream encoder; results equal the fused path's to LayerNorm rounding).
 int layer_rows(ae_engine* e, const LayerW& w, int64_t t0, int M, int s0, int ns, int max_len,
-               const uint32_t* mask_bits, int L, hipStream_t st, hipEvent_t after_qkv = nullptr) {
+               const uint32_t* mask_bits, int L, hipStream_t st, hipEvent_t mark = nullptr,
+               int mark_after = 1) {
   const int H = e->cfg.hidden, F = e->cfg.ffn, np = e->np;
   unsigned short* qkvp = reinterpret_cast<unsigned short*>(e->qkv);
   unsigned short* xp = e->xp + t0 * H * np;
   float* x = e->x + t0 * H;
   float* tmp = e->tmp + t0 * H;
-  int rc;
+  int rc, k = 0;
+  // records `mark` on st after the mark_after-th kernel of the layer (the second stream's lag)
+  auto done = [&]() -> int {
+    if (mark && ++k == mark_after) HIPC(hipEventRecord(mark, st));
+    return AE_OK;
+  };
   if ((rc = gemm_pk(e, xp, w.wqkv_p, w.bqkv, nullptr, nullptr, qkvp + t0 * 3 * H * np, M, 3 * H, H,
-                    EPI_BIAS_PACKED, st, false)))
+                    EPI_BIAS_PACKED, st, false)) || (rc = done()))
     return rc;
-  if (after_qkv) HIPC(hipEventRecord(after_qkv, st));
   {
     Prof p(e, st, e->prof_kind == AE_KIND_ATTENTION, 0.0);
     HIPC(ae_launch_attention_pp(qkvp, e->ctx, e->cp, e->cu + s0, nullptr, max_len, ns,
                                 e->cfg.heads, mask_bits ? mask_bits + (size_t)s0 * L * (L / 32) : nullptr,
                                 L, np, st));
   }
+  if ((rc = done())) return rc;
   if ((rc = gemm_pk(e, e->cp + t0 * H * np, w.wo_p, w.bo, x, tmp, nullptr, M, H, H,
-                    EPI_BIAS_RESIDUAL, st, false)))
+                    EPI_BIAS_RESIDUAL, st, false)) || (rc = done()))
     return rc;
   HIPC(ae_launch_layernorm(tmp, w.ln1g, w.ln1b, e->cfg.ln_eps, M, x, xp, np, st));
+  if ((rc = done())) return rc;
   if ((rc = gemm_pk(e, xp, w.w1_p, w.b1, nullptr, nullptr, e->hp + t0 * F * np, M, F, H,
-                    EPI_BIAS_GELU, st, true)))
+                    EPI_BIAS_GELU, st, true)) || (rc = done()))
     return rc;
   if ((rc = gemm_pk(e, e->hp + t0 * F * np, w.w2_p, w.b2, x, tmp, nullptr, M, H, F,
-                    EPI_BIAS_RESIDUAL, st, false)))
+                    EPI_BIAS_RESIDUAL, st, false)) || (rc = done()))
     return rc;
   HIPC(ae_launch_layernorm(tmp, w.ln2g, w.ln2b, e->cfg.ln_eps, M, x, xp, np, st));
-  return AE_OK;
+  return done();
 }
 
 // Runs the encoder over compacted tokens; on return the last-layer CLS rows are in e->xc
@@ -431,7 +439,7 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
       const LayerW& w = e->layers[li];
       int rc;
       if ((rc = layer_rows(e, w, 0, (int)T0, 0, n0, ml0, mask_bits, L, st,
-                           two && li == 0 ? e->ev_lag : nullptr)))
+                           two && li == 0 ? e->ev_lag : nullptr, e->split_lag)))
         return rc;
       if (two) {
         if (li == 0) HIPC(hipStreamWaitEvent(e->st2, e->ev_lag, 0));  // one kernel behind
@@ -671,6 +679,8 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
     // B=64 x L=512 16.58 -> 16.35 ms per step, ragged lens 40..512 11.36 -> 9.53 ms)
     const char* sp = std::getenv("AE_SPLIT_STREAMS");
     e->split = !(sp && sp[0] == '0');
+    const char* lag = std::getenv("AE_SPLIT_LAG");  // experiments: 1 (QKV) .. 7 (whole layer 0)
+    if (lag && lag[0] >= '1' && lag[0] <= '7') e->split_lag = lag[0] - '0';
     if (e->split) {
       HIPC(hipStreamCreateWithFlags(&e->st2, hipStreamNonBlocking));
       HIPC(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));

@@ -1,8 +1,9 @@
-"""A/B of the two-stream encoder (AE_SPLIT_STREAMS=1) against the single-stream fused path on the
-bench's scoring step (GPU): interleaved rounds of `--steps` steps each, in one process, and the
-max |dp| between the two engines' probabilities (full-length and ragged batches).
+"""A/B of the two-stream encoder (AE_SPLIT_STREAMS=1, second stream lagging by AE_SPLIT_LAG
+kernels) against the single-stream fused path on the bench's scoring step (GPU): interleaved
+rounds of `--steps` steps each, in one process, and the max |dp| between the engines'
+probabilities (full-length and ragged batches).
 
-  python tools/split_ab.py [--steps 10] [--rounds 5]
+  python tools/split_ab.py [--steps 10] [--rounds 5] [--lags 1,2,5]
 """
 import argparse
 import json
@@ -21,6 +22,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--precision", default="f32x3")
+    ap.add_argument("--lags", default="1",
+                    help="AE_SPLIT_LAG values of the two-stream engines (comma-separated)")
     args = ap.parse_args()
 
     import numpy as np
@@ -33,11 +36,15 @@ def main():
     dev = torch.device("cuda:0")
     sd = synthetic_state_dict(seed=0, head="sigmoid1")
     engines = {}
-    for mode in ("0", "1"):
-        os.environ["AE_SPLIT_STREAMS"] = mode
-        engines[mode] = Engine(sd, head="sigmoid1", num_labels=1, precision=args.precision,
-                               device=0)
+    os.environ["AE_SPLIT_STREAMS"] = "0"
+    engines["single"] = Engine(sd, head="sigmoid1", num_labels=1, precision=args.precision, device=0)
+    os.environ["AE_SPLIT_STREAMS"] = "1"
+    for lag in args.lags.split(","):
+        os.environ["AE_SPLIT_LAG"] = lag
+        engines[f"lag{lag}"] = Engine(sd, head="sigmoid1", num_labels=1, precision=args.precision,
+                                      device=0)
     os.environ.pop("AE_SPLIT_STREAMS")
+    os.environ.pop("AE_SPLIT_LAG")
     B, L = 64, 512
     rng = np.random.default_rng(0)
     ids = rng.integers(4, 50264, size=(B, L)).astype(np.int32)
@@ -66,10 +73,11 @@ def main():
                     eng.score(xd, lens, out=outs[m], stream=stream)
                 torch.cuda.synchronize()
                 times[m].append((time.perf_counter() - t0) * 1e3 / args.steps)
-        d = float((outs["0"] - outs["1"]).abs().max())
-        res[name] = {"ms_per_step_single": round(statistics.median(times["0"]), 3),
-                     "ms_per_step_split": round(statistics.median(times["1"]), 3),
-                     "tokens": int(lens.sum()), "max_abs_dprob_split_vs_single": d}
+        res[name] = {"tokens": int(lens.sum())}
+        for m in engines:
+            res[name][f"ms_per_step_{m}"] = round(statistics.median(times[m]), 3)
+            if m != "single":
+                res[name][f"max_abs_dprob_{m}_vs_single"] = float((outs[m] - outs["single"]).abs().max())
         print(json.dumps({name: res[name]}), flush=True)
     for eng in engines.values():
         eng.close()
