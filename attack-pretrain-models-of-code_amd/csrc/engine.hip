@@ -129,10 +129,12 @@ struct ae_engine {
   // half one kernel behind, so one half's memory-bound phases (GEMM epilogues, LayerNorm) and
   // tile-quantisation tails can run beside the other half's MFMA-bound main loops; LayerNorm as
   // its own kernel (no cross-workgroup exchange, whose partners must be co-resident)
+  static constexpr int kMaxParts = 4;
   bool split = false;
-  int split_lag = 1;  // the second half starts after this many of the first half's layer-0 kernels
-  hipStream_t st2 = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_lag = nullptr, ev_join = nullptr;
+  int split_parts = 2;  // parts of the batch, each on its own stream (AE_SPLIT_PARTS, 2..4)
+  int split_lag = 1;    // a part starts after this many of the previous part's layer-0 kernels
+  hipStream_t sts[kMaxParts] = {};  // sts[0] unused: part 0 runs on the caller's stream
+  hipEvent_t ev_fork = nullptr, ev_lag[kMaxParts] = {}, ev_join[kMaxParts] = {};
   // profiling: event pairs are created when profiling is switched on (never inside the timed
   // launches) and recycled by ae_kernel_time
   int prof_kind = -1;
@@ -420,36 +422,38 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
   unsigned short* qkvp = reinterpret_cast<unsigned short*>(e->qkv);  // planes mode: [T][np·3H]
   int first = 0;  // first layer the single-stream loop below runs
   if (pl && e->split && lens) {
-    // full layers in two halves of the batch on two streams (one half when n == 1, so that every
-    // batch size runs the same per-row arithmetic)
+    // full layers in P parts of the batch (sequence ranges, each on its own stream, every part
+    // one lag behind the previous); one part when n == 1, so every batch size runs the same
+    // per-row arithmetic
     const int NLs = cls_only ? NL - 1 : NL;
-    const int n0 = n >= 2 ? n / 2 : n;
-    const int64_t T0 = e->pinned_cu[n0];  // host prefix sums of the uploaded lens
-    int ml0 = 0, ml1 = 0;
-    for (int i = 0; i < n; ++i) {
-      if (i < n0) ml0 = lens[i] > ml0 ? lens[i] : ml0;
-      else ml1 = lens[i] > ml1 ? lens[i] : ml1;
+    const int P = n < e->split_parts ? n : e->split_parts;
+    int s_beg[ae_engine::kMaxParts + 1], ml[ae_engine::kMaxParts];
+    for (int p = 0; p <= P; ++p) s_beg[p] = (int)((int64_t)n * p / P);
+    for (int p = 0; p < P; ++p) {
+      ml[p] = 0;
+      for (int i = s_beg[p]; i < s_beg[p + 1]; ++i) ml[p] = lens[i] > ml[p] ? lens[i] : ml[p];
     }
-    const bool two = n0 < n;
-    if (two) {
+    auto stream_of = [&](int p) { return p == 0 ? st : e->sts[p]; };
+    if (P > 1) {
       HIPC(hipEventRecord(e->ev_fork, st));
-      HIPC(hipStreamWaitEvent(e->st2, e->ev_fork, 0));
+      for (int p = 1; p < P; ++p) HIPC(hipStreamWaitEvent(e->sts[p], e->ev_fork, 0));
     }
     for (int li = 0; li < NLs; ++li) {
       const LayerW& w = e->layers[li];
-      int rc;
-      if ((rc = layer_rows(e, w, 0, (int)T0, 0, n0, ml0, mask_bits, L, st,
-                           two && li == 0 ? e->ev_lag : nullptr, e->split_lag)))
-        return rc;
-      if (two) {
-        if (li == 0) HIPC(hipStreamWaitEvent(e->st2, e->ev_lag, 0));  // one kernel behind
-        if ((rc = layer_rows(e, w, T0, (int)(T - T0), n0, n - n0, ml1, mask_bits, L, e->st2)))
+      for (int p = 0; p < P; ++p) {
+        if (li == 0 && p > 0) HIPC(hipStreamWaitEvent(e->sts[p], e->ev_lag[p - 1], 0));
+        const int64_t t0 = e->pinned_cu[s_beg[p]];  // host prefix sums of the uploaded lens
+        const int M = (int)(e->pinned_cu[s_beg[p + 1]] - t0);
+        int rc;
+        if ((rc = layer_rows(e, w, t0, M, s_beg[p], s_beg[p + 1] - s_beg[p], ml[p], mask_bits, L,
+                             stream_of(p), li == 0 && p + 1 < P ? e->ev_lag[p] : nullptr,
+                             e->split_lag)))
           return rc;
       }
     }
-    if (two) {
-      HIPC(hipEventRecord(e->ev_join, e->st2));
-      HIPC(hipStreamWaitEvent(st, e->ev_join, 0));
+    for (int p = 1; p < P; ++p) {
+      HIPC(hipEventRecord(e->ev_join[p], e->sts[p]));
+      HIPC(hipStreamWaitEvent(st, e->ev_join[p], 0));
     }
     first = NLs;
   }
@@ -681,11 +685,15 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
     e->split = !(sp && sp[0] == '0');
     const char* lag = std::getenv("AE_SPLIT_LAG");  // experiments: 1 (QKV) .. 7 (whole layer 0)
     if (lag && lag[0] >= '1' && lag[0] <= '7') e->split_lag = lag[0] - '0';
+    const char* parts = std::getenv("AE_SPLIT_PARTS");  // experiments: 2 (default) .. 4
+    if (parts && parts[0] >= '2' && parts[0] <= '4') e->split_parts = parts[0] - '0';
     if (e->split) {
-      HIPC(hipStreamCreateWithFlags(&e->st2, hipStreamNonBlocking));
       HIPC(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
-      HIPC(hipEventCreateWithFlags(&e->ev_lag, hipEventDisableTiming));
-      HIPC(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
+      for (int p = 0; p < ae_engine::kMaxParts; ++p) {
+        if (p > 0) HIPC(hipStreamCreateWithFlags(&e->sts[p], hipStreamNonBlocking));
+        HIPC(hipEventCreateWithFlags(&e->ev_lag[p], hipEventDisableTiming));
+        HIPC(hipEventCreateWithFlags(&e->ev_join[p], hipEventDisableTiming));
+      }
     }
   }
   HIPC(hipDeviceSynchronize());
@@ -701,9 +709,12 @@ int ae_destroy(ae_engine* e) {
     if (p) (void)hipFree(p);
   if (e->pinned_cu) (void)hipHostFree(e->pinned_cu);
   if (e->pinned_ready) (void)hipEventDestroy(e->pinned_ready);
-  for (hipEvent_t ev : {e->ev_fork, e->ev_lag, e->ev_join})
-    if (ev) (void)hipEventDestroy(ev);
-  if (e->st2) (void)hipStreamDestroy(e->st2);
+  if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+  for (int p = 0; p < ae_engine::kMaxParts; ++p) {
+    if (e->ev_lag[p]) (void)hipEventDestroy(e->ev_lag[p]);
+    if (e->ev_join[p]) (void)hipEventDestroy(e->ev_join[p]);
+    if (e->sts[p]) (void)hipStreamDestroy(e->sts[p]);
+  }
   for (auto* v : {&e->prof, &e->prof_pool})
     for (auto& r : *v) {
       (void)hipEventDestroy(r.a);

@@ -1,9 +1,9 @@
-"""A/B of the two-stream encoder (AE_SPLIT_STREAMS=1, second stream lagging by AE_SPLIT_LAG
-kernels) against the single-stream fused path on the bench's scoring step (GPU): interleaved
+"""A/B of the split encoder (AE_SPLIT_STREAMS=1: AE_SPLIT_PARTS parts of the batch on as many
+streams, each lagging the previous by AE_SPLIT_LAG kernels) against the single-stream fused path on the bench's scoring step (GPU): interleaved
 rounds of `--steps` steps each, in one process, and the max |dp| between the engines'
 probabilities (full-length and ragged batches).
 
-  python tools/split_ab.py [--steps 10] [--rounds 5] [--lags 1,2,5]
+  python tools/split_ab.py [--steps 10] [--rounds 5] [--lags 1,2,5] [--parts 2,3,4]
 """
 import argparse
 import json
@@ -23,7 +23,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--precision", default="f32x3")
     ap.add_argument("--lags", default="1",
-                    help="AE_SPLIT_LAG values of the two-stream engines (comma-separated)")
+                    help="AE_SPLIT_LAG values of the split engines (comma-separated)")
+    ap.add_argument("--parts", default="2",
+                    help="AE_SPLIT_PARTS values of the split engines (comma-separated)")
     args = ap.parse_args()
 
     import numpy as np
@@ -39,12 +41,14 @@ def main():
     os.environ["AE_SPLIT_STREAMS"] = "0"
     engines["single"] = Engine(sd, head="sigmoid1", num_labels=1, precision=args.precision, device=0)
     os.environ["AE_SPLIT_STREAMS"] = "1"
-    for lag in args.lags.split(","):
-        os.environ["AE_SPLIT_LAG"] = lag
-        engines[f"lag{lag}"] = Engine(sd, head="sigmoid1", num_labels=1, precision=args.precision,
-                                      device=0)
-    os.environ.pop("AE_SPLIT_STREAMS")
-    os.environ.pop("AE_SPLIT_LAG")
+    for parts in args.parts.split(","):
+        for lag in args.lags.split(","):
+            os.environ["AE_SPLIT_LAG"] = lag
+            os.environ["AE_SPLIT_PARTS"] = parts
+            engines[f"p{parts}lag{lag}"] = Engine(sd, head="sigmoid1", num_labels=1,
+                                                  precision=args.precision, device=0)
+    for k in ("AE_SPLIT_STREAMS", "AE_SPLIT_LAG", "AE_SPLIT_PARTS"):
+        os.environ.pop(k)
     B, L = 64, 512
     rng = np.random.default_rng(0)
     ids = rng.integers(4, 50264, size=(B, L)).astype(np.int32)
