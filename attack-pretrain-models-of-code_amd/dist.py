@@ -86,7 +86,9 @@ def gather_stats(stats, device=None):
     v = np.asarray(stats, dtype=np.float64)
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return v[None]
-    if device is None and dist.get_backend() == "nccl":
+    if dist.get_backend() != "nccl":
+        device = torch.device("cpu")  # gloo: host tensors
+    elif device is None:
         device = torch.device("cuda", torch.cuda.current_device())
     t = torch.tensor(v, dtype=torch.float64, device=device)
     out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
@@ -151,6 +153,16 @@ def _job_totals(st, names, nsum):
     return tot
 
 
+def _inflight(max_inflight, n, world):
+    """Examples a rank keeps in flight: on one rank all it may; on several, at most half an even
+    share of the queue, so the other half is handed out as ranks free up (per-example cost is
+    skewed; the ranks fill their first batches at the same instant after the barrier, and an
+    uncapped fill would hand the whole queue out statically)."""
+    if world <= 1:
+        return max_inflight
+    return max(1, min(max_inflight, max(8, -(-n // (2 * world)))))
+
+
 GI_STATS = ["examples", "total_cnt", "success", "queries", "ga_runs", "ga_successes", "wall_s"]
 MHM_STATS = ["examples", "total_cnt", "success", "queries", "wall_s"]
 
@@ -168,7 +180,7 @@ def run_sharded_gi_batched(model, codes, subs, labels, args, max_inflight=64, de
     if dist is not None:
         dist.barrier()
     out = run_gi_attack_batched(model, codes, subs, labels, args, queue=q,
-                                max_inflight=max_inflight)
+                                max_inflight=_inflight(max_inflight, len(codes), world))
     recs = out["records"]
     ga = [r for r in recs if r["attack_type"] == "GA"]
     st = gather_stats([out["examples"], out["total_cnt"], out["success"], out["queries"],
@@ -188,12 +200,13 @@ def run_sharded_mhm(model, codes, subs, labels, args, n_candi=30, max_iter=100, 
     from .drivers import run_mhm_attack
 
     dist, _, world = _rank_world()
-    q = DynamicQueue(len(codes) if n is None else n, key=call_key(key))
+    n_ex = len(codes) if n is None else n
+    q = DynamicQueue(n_ex, key=call_key(key))
     if dist is not None:
         dist.barrier()
     out = run_mhm_attack(model, codes, subs, labels, args, n_candi=n_candi, max_iter=max_iter,
                          prob_threshold=prob_threshold, original=original,
-                         max_inflight=max_inflight, queue=q)
+                         max_inflight=_inflight(max_inflight, n_ex, world), queue=q)
     st = gather_stats([out["examples"], out["total_cnt"], out["success"], out["queries"],
                        out["wall_s"]], device=device)
     tot = _job_totals(st, MHM_STATS, 4)

@@ -46,6 +46,7 @@ CLONE_FIXTURE = ROOT / "data" / "clone" / "test_subs_0_500.jsonl"
 # attack-sensitive synthetic victim (the attack parity tests' weights): a larger classifier
 # out_proj spreads probabilities so that substitutions can flip predictions
 VICTIM_SEED, VICTIM_OUT_STD = 5, 8.0
+COLL_DEV = None  # device of the collectives' tensors (main sets it: the rank's GPU, or host for gloo)
 
 
 def parse_args():
@@ -534,7 +535,7 @@ def subs_leg(dev, seconds, rank, world, precision):
                   st["encoder_flop"], wall], dtype=np.float64)
     if world > 1:
         import torch.distributed as dist
-        t = torch.tensor(v, device=dev)
+        t = torch.tensor(v, device=COLL_DEV)
         g = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(g, t)
         allv = torch.stack(g).cpu().numpy()
@@ -569,18 +570,28 @@ def main():
 
     import _apmc  # noqa: F401
 
+    # APMC_BENCH_REHEARSE=1: rehearsal of the N-rank path on a one-GPU box — every rank on cuda:0,
+    # collectives over gloo (host tensors); the numbers of such a run are not a measurement
+    rehearse = os.environ.get("APMC_BENCH_REHEARSE") == "1"
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-        seen = torch.ones(1, device=f"cuda:{local}")
+        gpu = 0 if rehearse else local
+        torch.cuda.set_device(gpu)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{gpu}"))
+        seen = torch.ones(1, device="cpu" if rehearse else f"cuda:{gpu}")
         dist.all_reduce(seen)
         if int(seen.item()) != args.gpus:
-            raise SystemExit(f"RCCL all-reduce saw {int(seen.item())} ranks, expected {args.gpus}")
+            raise SystemExit(f"all-reduce saw {int(seen.item())} ranks, expected {args.gpus}")
     else:
+        gpu = 0
         torch.cuda.set_device(0)
-    dev = torch.device(f"cuda:{local if world > 1 else 0}")
+    dev = torch.device(f"cuda:{gpu}")
+    global COLL_DEV
+    COLL_DEV = torch.device("cpu") if rehearse else dev  # where collective tensors live
 
     from apmc_amd.engine import Engine
     from apmc_amd.weights import synthetic_state_dict
@@ -610,11 +621,11 @@ def main():
                                           profile=True)
     eng1.close()
     if dist is not None:
-        t = torch.tensor([elapsed, el1], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, el1], dtype=torch.float64, device=COLL_DEV)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, el1 = float(t[0]), float(t[1])
         kt = torch.tensor([k_ms, float(k_n), k_flop, s_ms, float(s_n)], dtype=torch.float64,
-                          device=dev)
+                          device=COLL_DEV)
         dist.all_reduce(kt, op=dist.ReduceOp.SUM)
         k_ms, k_n, k_flop, s_ms, s_n = float(kt[0]), int(kt[1]), float(kt[2]), float(kt[3]), int(kt[4])
 
@@ -635,7 +646,7 @@ def main():
         el32, _ = time_steps(ref_eng, ids_dev, lens, ref_out, max(3, args.steps // 2),
                              args.warmup, dev, dist, profile=False)
         if dist is not None:
-            t = torch.tensor([el32], dtype=torch.float64, device=dev)
+            t = torch.tensor([el32], dtype=torch.float64, device=COLL_DEV)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el32 = float(t.item())
         n32 = max(3, args.steps // 2)
@@ -652,7 +663,7 @@ def main():
             el16, _ = time_steps(b_eng, ids_dev, lens, b_out, n32, args.warmup, dev, dist,
                                  profile=False)
             if dist is not None:
-                t = torch.tensor([el16], dtype=torch.float64, device=dev)
+                t = torch.tensor([el16], dtype=torch.float64, device=COLL_DEV)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
                 el16 = float(t.item())
             bf16_mode = {

@@ -190,5 +190,8 @@ def test_two_ranks_batched_drivers_match_single_process(tmp_path):
     assert got["mhm_tot"]["queries"] == mhm["queries"]
     assert {r["is_success"] for r in mhm["records"]} & {1, -1}
     for tot in (got["gi_tot"], got["mhm_tot"]):
-        assert len(tot["per_rank"]) == 2 and all(r["examples"] >= 1 for r in tot["per_rank"])
+        # one row per rank, summing to the job; which rank takes how many examples is scheduling
+        # (with this instant victim one rank can drain the queue before the other's first pull)
+        assert len(tot["per_rank"]) == 2
+        assert sum(r["examples"] for r in tot["per_rank"]) == N_EX
         assert sum(r["examples"] for r in tot["per_rank"]) == N_EX

@@ -256,3 +256,26 @@ def test_scores_batch_invariant_across_split_k(gpu, precision, head, num_labels)
     small = _score(eng, ids[:8])  # 8 sequences = 4 pair rows for the pair head
     k = small.shape[0]
     assert np.array_equal(big[:k], small), np.abs(big[:k] - small).max()
+
+
+@pytest.mark.parametrize("precision", ["f32x3", "bf16"])
+@pytest.mark.parametrize("n", [1, 3, 64])
+def test_two_stream_encoder_matches_single_stream(gpu, monkeypatch, precision, n):
+    """The split-precision engine's default two-stream encoder (two half-batch streams, residual +
+    LayerNorm as its own kernel) against the same engine built with AE_SPLIT_STREAMS=0 (one
+    stream, fused residual + LayerNorm epilogue): odd and single-row batches, ragged lengths
+    across a 256-row tile boundary; the two differ only by LayerNorm rounding."""
+    from apmc_amd.engine import Engine
+    sd = synthetic_sd(6, "softmaxN", 5)
+    engines = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("AE_SPLIT_STREAMS", mode)
+        engines[mode] = Engine(sd, head="softmaxN", num_labels=5, precision=precision)
+    rng = np.random.default_rng(30 + n)
+    L = 384
+    ids = _rand_ids(rng, n, L, rng.integers(3, L + 1, n))
+    a, b = _score(engines["1"], ids), _score(engines["0"], ids)
+    tol = 1e-4 if precision == "f32x3" else 2e-2
+    np.testing.assert_allclose(a, b, atol=tol, rtol=0)
+    for e in engines.values():
+        e.close()
