@@ -1198,6 +1198,281 @@ __global__ __launch_bounds__(256, 1) void attn_pw64_kernel(const unsigned short*
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// attn_kt64_kernel (variant 9): PIPE 6 with 64-key tiles — the per-tile fixed work (row-max
+// exchange, rescale decision, DMA issue, counted wait, barrier) is paid once per 64 keys, and the
+// S of a tile is two independent 12-MFMA chains.  K and V tiles of 64 keys (16 KiB each for
+// NP = 2) in 2-slot rings: iteration kt issues V(kt+1) and K(kt+2) and waits for them at its end.
+// Measured and not kept: correct (tests/test_kernels_gpu.py variant 9) but 217.1 vs 186.2 µs
+// full-length, 136.3 vs 126.6 µs ragged against PIPE 6 (profiles/r3x_attn_kt64_ab.log): the
+// per-key VALU falls only ~3 % and the 2-slot rings prefetch one tile less deep.
+template <int NP, bool PLANES>
+__global__ __launch_bounds__(256, 2) void attn_kt64_kernel(const unsigned short* __restrict__ qkvp,
+                                                           float* __restrict__ out,
+                                                           unsigned short* __restrict__ op,
+                                                           const int* __restrict__ cu,
+                                                           const int* __restrict__ q_rows) {
+  using P = PPL<NP>;
+  constexpr int TERMS = NP == 2 ? 3 : 1;
+  constexpr int KT2 = 64;
+  constexpr int TILE2 = KT2 * P::RB;  // one 64-key K (or V) tile
+  constexpr int DM = KT2 / P::ROWS_PER_DMA / 4;  // DMA instructions per wave per matrix tile
+  constexpr int LDS_BYTES = 4 * TILE2 > 4 * 32 * 66 * 4 ? 4 * TILE2 : 4 * 32 * 66 * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
+  const int seq = blockIdx.z, head = blockIdx.y, qb = blockIdx.x;
+  const int start = cu[seq];
+  const int len = cu[seq + 1] - start;
+  const int nq = q_rows ? min(len, q_rows[0]) : len;
+  if (qb * QPB >= nq) return;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 31, lh = lane >> 5;
+  constexpr size_t LDR = (size_t)NP * QKV_COLS;
+
+  const int q = qb * QPB + wave * 32 + li;
+  const int qr = q < nq ? q : nq - 1;
+  bf16x8 qh[4], ql[4];
+  {
+    const unsigned short* qp = qkvp + (size_t)(start + qr) * LDR + (size_t)head * 64 * NP;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int d = 16 * s + 8 * lh;
+      const int off = (d >> 5) * 32 * NP + (d & 31);
+      qh[s] = *reinterpret_cast<const bf16x8*>(qp + off);
+      if (TERMS == 3) ql[s] = *reinterpret_cast<const bf16x8*>(qp + off + 32);
+    }
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
+  const int dr = lane / P::CR, dc = lane % P::CR;
+  // DMA of a 64-key K (moff AE_HIDDEN) or V (2 AE_HIDDEN) tile; row r of the tile keeps the
+  // 32-key tiles' swizzles (they depend on r's low bits only)
+  auto issue = [&](int kt, int moff, uint32_t dst, bool vimg) {
+#pragma unroll
+    for (int j = 0; j < DM; ++j) {
+      const int i = wave * DM + j;
+      const int r = i * P::ROWS_PER_DMA + dr;
+      int key = kt * KT2 + r;
+      key = key < len ? key : len - 1;
+      const unsigned short* row = qkvp + (size_t)(start + key) * LDR;
+      dma16(row + (size_t)(moff + head * 64) * NP + (vimg ? vpos<NP>(r, dc) : kpos<NP>(r, dc)) * 8,
+            dst + i * 1024);
+    }
+  };
+  auto wait_vm = [](int n) {
+    if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  auto barrier = []() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  floatx16 o0, o1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; }
+  float m_run = -INFINITY, l_run = 0.f;
+
+  // S^T of both 32-key halves of a 64-key K image
+  auto s_mfma = [&](const unsigned char* stk, floatx16 (&s)[2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[h][r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int d0 = 16 * ks + 8 * lh;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int row = 32 * h + li;
+        const unsigned char* kr = stk + row * P::RB;
+        const bf16x8 kh = *reinterpret_cast<const bf16x8*>(kr + kpos<NP>(row, chunk_of<NP>(0, d0)) * 16);
+        if (TERMS == 3) {
+          const bf16x8 kl =
+              *reinterpret_cast<const bf16x8*>(kr + kpos<NP>(row, chunk_of<NP>(1, d0)) * 16);
+          s[h] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl, qh[ks], s[h], 0, 0, 0);
+          s[h] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, ql[ks], s[h], 0, 0, 0);
+        }
+        s[h] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, qh[ks], s[h], 0, 0, 0);
+      }
+    }
+  };
+  // O^T += V^T P^T over 64 keys (4 k-steps of 16)
+  auto pv_mfma = [&](const unsigned char* stv, const bf16x8 (&ph)[4], const bf16x8 (&pl)[4]) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int kq = 16 * t + 4 * lh + ((lane >> 2) & 3);
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int col = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+        const int cb = (col & 7) * 2;
+        const unsigned char* va = stv + kq * P::RB + cb;
+        const unsigned char* vb = stv + (kq + 8) * P::RB + cb;
+        bf16x8 vh, vl;
+        {
+          const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)(va + vpos<NP>(kq, chunk_of<NP>(0, col)) * 16));
+          const bf16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)(vb + vpos<NP>(kq + 8, chunk_of<NP>(0, col)) * 16));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { vh[e] = a[e]; vh[4 + e] = b[e]; }
+        }
+        if (TERMS == 3) {
+          const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)(va + vpos<NP>(kq, chunk_of<NP>(1, col)) * 16));
+          const bf16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)(vb + vpos<NP>(kq + 8, chunk_of<NP>(1, col)) * 16));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { vl[e] = a[e]; vl[4 + e] = b[e]; }
+        }
+        floatx16& o = dt == 0 ? o0 : o1;
+        if (TERMS == 3) {
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl, ph[t], o, 0, 0, 0);
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, pl[t], o, 0, 0, 0);
+        }
+        o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, ph[t], o, 0, 0, 0);
+      }
+    }
+  };
+
+  const int nkt = (len + KT2 - 1) / KT2;
+  // prologue: K0, V0, K1 (slots: K_j in j & 1, V_j in 2 + (j & 1))
+  issue(0, AE_HIDDEN, lds0, false);
+  issue(0, 2 * AE_HIDDEN, lds0 + 2 * TILE2, true);
+  if (nkt > 1) issue(1, AE_HIDDEN, lds0 + TILE2, false);
+  wait_vm(nkt > 1 ? 2 * DM : DM);  // K0 landed
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {  // Q through an empty asm: hipcc waits for it here, once
+    asm volatile("" : "+v"(qh[k]));
+    if (TERMS == 3) asm volatile("" : "+v"(ql[k]));
+  }
+  barrier();
+  floatx16 sA[2], sB[2];
+  s_mfma(lds, sA);
+  wait_vm(0);  // V0, K1 landed
+  barrier();  // every wave has read K0 (its slot takes K2) and sees V0, K1
+
+  auto body = [&](auto rc, int kt, floatx16 (&s_cur)[2], floatx16 (&s_next)[2]) {
+    constexpr int R = decltype(rc)::value;  // kt & 1
+    constexpr uint32_t KS_NEXT = (1 - R) * TILE2, VS_CUR = (2 + R) * TILE2;
+    constexpr uint32_t VS_ISS = (2 + (1 - R)) * TILE2, KS_ISS = R * TILE2;
+    int n_iss = 0;
+    if (kt + 1 < nkt) {
+      issue(kt + 1, 2 * AE_HIDDEN, lds0 + VS_ISS, true);  // V(kt+1) into V(kt-1)'s slot
+      n_iss += DM;
+    }
+    if (kt + 2 < nkt) {
+      issue(kt + 2, AE_HIDDEN, lds0 + KS_ISS, false);  // K(kt+2) into K(kt)'s slot
+      n_iss += DM;
+    }
+    float mt = -INFINITY;
+    if ((kt + 1) * KT2 <= len) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) mt = fmaxf(mt, fmaxf(s_cur[h][r], s_cur[h][r + 1]));
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const bool in = kt * KT2 + 32 * h + mfma32_row(r, lh) < len;
+          s_cur[h][r] = in ? s_cur[h][r] : -INFINITY;
+          mt = fmaxf(mt, s_cur[h][r]);
+        }
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const bool grow = __any(mt > m_run + 8.f);
+    const float m_new = grow ? fmaxf(m_run, mt) : m_run;
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+    bf16x8 ph[4], pl[4];
+    float psum = 0.f;
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(s_cur[h][r] - m_new);
+        psum += p;
+        const __bf16 hv = (__bf16)p;
+        ph[2 * h + (r >> 3)][r & 7] = hv;
+        pl[2 * h + (r >> 3)][r & 7] = (__bf16)(p - (float)hv);
+      }
+    s_mfma(lds + KS_NEXT, s_next);  // unconditional: the last tile's reads a stale slot, unused
+    __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+#pragma unroll
+    for (int i = 0; i < 24; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+    if (grow) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+    }
+    pv_mfma(lds + VS_CUR, ph, pl);
+    (void)n_iss;
+    wait_vm(0);  // V(kt+1), K(kt+2): iteration kt+1 reads both
+    barrier();
+  };
+  for (int kt = 0; kt < nkt; kt += 2) {
+    body(std::integral_constant<int, 0>(), kt, sA, sB);
+    if (kt + 1 >= nkt) break;
+    body(std::integral_constant<int, 1>(), kt + 1, sB, sA);
+  }
+
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  constexpr int S6 = 66;
+  float* os6 = reinterpret_cast<float*>(lds) + wave * 32 * S6;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int d = mfma32_row(r, lh);
+    os6[li * S6 + d] = o0[r] * inv;
+    os6[li * S6 + 32 + d] = o1[r] * inv;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  constexpr int CPR = PLANES ? 8 * NP : 16;
+  constexpr int RPI = 64 / CPR;
+  const int c = lane % CPR;
+#pragma unroll
+  for (int it = 0; it < 32 / RPI; ++it) {
+    const int rr = it * RPI + lane / CPR;
+    const int qq = qb * QPB + wave * 32 + rr;
+    const float* src = os6 + rr * S6;
+    if (PLANES) {
+      const int d0 = 32 * (c / (4 * NP)) + 8 * (c % 4);
+      const bool lo_plane = NP == 2 && ((c >> 2) & 1);
+      uint32_t w[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const floatx2 v = *reinterpret_cast<const floatx2*>(src + d0 + 2 * e);
+        const __bf16 hx = (__bf16)v.x, hy = (__bf16)v.y;
+        bf16x2 pr;
+        if (lo_plane) pr = bf16x2{(__bf16)(v.x - (float)hx), (__bf16)(v.y - (float)hy)};
+        else pr = bf16x2{hx, hy};
+        w[e] = __builtin_bit_cast(uint32_t, pr);
+      }
+      if (qq < nq) {
+        unsigned short* dst = op + (size_t)(start + qq) * NP * AE_HIDDEN + head * 64 * NP + c * 8;
+        *reinterpret_cast<u32x4*>(dst) = u32x4{w[0], w[1], w[2], w[3]};
+      }
+    } else {
+      const floatx2 a = *reinterpret_cast<const floatx2*>(src + 4 * c);
+      const floatx2 b = *reinterpret_cast<const floatx2*>(src + 4 * c + 2);
+      if (qq < nq)
+        *reinterpret_cast<floatx4*>(out + (size_t)(start + qq) * AE_HIDDEN + head * AE_HEAD_DIM + 4 * c) =
+            floatx4{a.x, a.y, b.x, b.y};
+    }
+  }
+}
+
 // qkvp: packed planes [T][np·2304] with Q pre-scaled by log2(e)/8; context to op (packed planes)
 // or out (f32 [T, 768]).  q_rows / max_q: the CLS-only launch of the last layer.
 namespace {
@@ -1217,6 +1492,16 @@ hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op
     if (mask) APP_LAUNCH(N, true, true); else APP_LAUNCH(N, false, true);   \
   } else {                                                             \
     if (mask) APP_LAUNCH(N, true, false); else APP_LAUNCH(N, false, false); \
+  }
+  if (PIPE == 9 && !mask) {  // 64-key tiles (no mask path: masks run PIPE 4)
+    if (np == 2) {
+      if (op) hipLaunchKernelGGL((attn_kt64_kernel<2, true>), grid, block, 0, stream, qkvp, out, op, cu, q_rows);
+      else hipLaunchKernelGGL((attn_kt64_kernel<2, false>), grid, block, 0, stream, qkvp, out, op, cu, q_rows);
+    } else {
+      if (op) hipLaunchKernelGGL((attn_kt64_kernel<1, true>), grid, block, 0, stream, qkvp, out, op, cu, q_rows);
+      else hipLaunchKernelGGL((attn_kt64_kernel<1, false>), grid, block, 0, stream, qkvp, out, op, cu, q_rows);
+    }
+    return hipGetLastError();
   }
   if (PIPE == 8 && !mask) {  // 4 waves x 64 queries (no mask path: masks run PIPE 4)
     dim3 grid8((max_q + 255) / 256, heads, n);
@@ -1275,6 +1560,8 @@ extern "C" hipError_t ae_bench_attention_pp(const unsigned short* qkvp, float* o
                                             unsigned short* op, const int* cu, const int* q_rows,
                                             int max_q, int n, int heads, const uint32_t* mask,
                                             int mask_L, int np, int variant, hipStream_t stream) {
+  if (variant == 9)
+    return app_launch<9>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
   if (variant == 8)
     return app_launch<8>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
   if (variant == 7)

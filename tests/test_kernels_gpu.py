@@ -224,7 +224,7 @@ def _qkv_planes(qkv, np_):
     return _pack(hi, lo, np_)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("np_", [2, 1])
 @pytest.mark.parametrize("case", ["ragged", "mask", "cls", "planes", "grow"])
 def test_attention_pp_matches_f64(gpu, np_, case, variant):
@@ -232,7 +232,7 @@ def test_attention_pp_matches_f64(gpu, np_, case, variant):
     reads) against the float64 reference, for both plane counts (np 1 = bf16 mode: stated
     tolerance 2e-2), every loop (1: software-pipelined, 6: 3-slot rings + deferred rescale, 7: the
     8-wave ping-pong kernel with the keys split between its two groups and merged, 8: 4 waves x
-    64 queries, one wave per SIMD) and
+    64 queries, one wave per SIMD, 9: 64-key tiles) and
     the ragged / mask / CLS-only / packed-output launches.  "grow": spike keys whose scores
     rise along the sequence, so every row max jumps past the deferred-rescale threshold (2^8)
     several times — the rare branch of variant 6."""
