@@ -46,6 +46,17 @@ __device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_base) {
       : "v"(gsrc), "s"(lds_base)
       : "memory", "m0");
 }
+// The same with a uniform 64-bit base in SGPRs and a per-lane 32-bit byte offset (saddr form):
+// advancing a tile is two scalar adds instead of per-lane 64-bit address arithmetic.
+__device__ __forceinline__ void dma16s(uint32_t voff, const void* sbase, uint32_t lds_base) {
+  asm volatile(
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %0, %1"
+      :
+      : "v"(voff), "s"(sbase), "s"(lds_base)
+      : "memory", "m0");
+}
 
 template <int NP>
 struct PPL {
@@ -87,7 +98,7 @@ __device__ __forceinline__ int vpos(int r, int x) {
 // upper 16 bits, one shift-or per pair) and lo = bf16(p - hi), exact to 2^-16 of p as the
 // rounded split.
 template <int NP, bool HAS_MASK, bool PLANES, int PIPE>
-__global__ __launch_bounds__(256, PIPE == 5 ? 3 : 2) void attn_pp_kernel(const unsigned short* __restrict__ qkvp,
+__global__ __launch_bounds__(256, (PIPE == 5 || (PIPE >= 60 && PIPE != 64)) ? 3 : 2) void attn_pp_kernel(const unsigned short* __restrict__ qkvp,
                                                          float* __restrict__ out,
                                                          unsigned short* __restrict__ op,
                                                          const int* __restrict__ cu,
@@ -96,11 +107,19 @@ __global__ __launch_bounds__(256, PIPE == 5 ? 3 : 2) void attn_pp_kernel(const u
                                                          int mask_L) {
   using P = PPL<NP>;
   constexpr int TERMS = NP == 2 ? 3 : 1;
-  static_assert(!(HAS_MASK && PIPE == 6), "PIPE 6 has no mask path (its loop keeps no ordinary "
+  // PIPE 66: PIPE 6 with saddr DMA (per-lane offsets computed once, tiles advanced on the scalar
+  // unit) and the cross-half row max by v_permlane32_swap instead of an LDS permute.  PIPE 61-65:
+  // timing diagnostics of 66 (results WRONG; tools/attn_bench.py only): 1 = no exp / P split
+  // (P = bf16(S)), 2 = no tile max (fixed reference max 0), 3 = no barriers in the loop, 4 = no
+  // PV MFMAs (no V reads), 5 = no S MFMAs after the prologue (no K reads)
+  constexpr int PB = PIPE >= 60 ? 6 : PIPE;
+  constexpr int DG = (PIPE >= 61 && PIPE <= 65) ? PIPE - 60 : 0;
+  constexpr bool FAST = PIPE >= 60;
+  static_assert(!(HAS_MASK && PB == 6), "PIPE 6 has no mask path (its loop keeps no ordinary "
                                           "global load, so the mask launches run PIPE 4)");
   // PIPE 6: three K and three V slots (the O staging of the epilogue fits inside)
   constexpr int LDS_BYTES =
-      PIPE == 6 ? (6 * P::TILE > 4 * 32 * 66 * 4 ? 6 * P::TILE : 4 * 32 * 66 * 4) : P::LDS;
+      PB == 6 ? (6 * P::TILE > 4 * 32 * 66 * 4 ? 6 * P::TILE : 4 * 32 * 66 * 4) : P::LDS;
   __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
   const int seq = blockIdx.z, head = blockIdx.y, qb = blockIdx.x;
   const int start = cu[seq];
@@ -283,7 +302,7 @@ __global__ __launch_bounds__(256, PIPE == 5 ? 3 : 2) void attn_pp_kernel(const u
   };
 
   const int nkt = (len + KT - 1) / KT;
-  if constexpr (PIPE == 6) {
+  if constexpr (PB == 6) {
     // 3-slot rings: K_j in slot j % 3, V_j in slot 3 + j % 3.  Iteration kt issues V_{kt+2} and
     // K_{kt+3} and, at its end, waits only for what iteration kt+1 reads (V_{kt+1}, K_{kt+2},
     // issued one iteration earlier): a counted vmcnt leaves this iteration's DMA in flight across
@@ -300,28 +319,62 @@ __global__ __launch_bounds__(256, PIPE == 5 ? 3 : 2) void attn_pp_kernel(const u
     auto barrier = []() {
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
+      if constexpr (DG != 3) __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
     };
     constexpr int DM = P::DMA_PER_WAVE;  // DMA instructions per wave per matrix tile
+    // FAST: byte offsets of this lane's DMA chunks from the sequence's first token row (K and V,
+    // one per DMA instruction), fixed for the whole loop; a full tile kt adds kt·KT rows to the
+    // scalar base; the last, partial tile clamps its key rows the per-lane way (issue1)
+    uint32_t voff[2][FAST ? DM : 1];
+    const unsigned char* sbase =
+        reinterpret_cast<const unsigned char*>(qkvp + (size_t)start * LDR);
+    if constexpr (FAST) {
+#pragma unroll
+      for (int j = 0; j < DM; ++j) {
+        const int r = (wave * DM + j) * P::ROWS_PER_DMA + dr;
+        voff[0][j] = 2u * ((uint32_t)r * (uint32_t)LDR + (AE_HIDDEN + head * 64) * NP + kpos<NP>(r, dc) * 8);
+        voff[1][j] = 2u * ((uint32_t)r * (uint32_t)LDR + (2 * AE_HIDDEN + head * 64) * NP + vpos<NP>(r, dc) * 8);
+      }
+    }
+    auto issue = [&](int kt, bool isv, uint32_t dst) {
+      if constexpr (FAST) {
+        const unsigned char* sb = sbase + (size_t)kt * KT * LDR * 2;
+        if ((kt + 1) * KT <= len) {
+#pragma unroll
+          for (int j = 0; j < DM; ++j) dma16s(voff[isv][j], sb, dst + (wave * DM + j) * 1024);
+        } else {  // key rows past the sequence re-read its last row (finite, masked to -inf)
+          const int last = len - 1 - kt * KT;
+#pragma unroll
+          for (int j = 0; j < DM; ++j) {
+            const int over = (wave * DM + j) * P::ROWS_PER_DMA + dr - last;
+            const uint32_t v = voff[isv][j] - (over > 0 ? (uint32_t)over * (uint32_t)(LDR * 2) : 0u);
+            dma16s(v, sb, dst + (wave * DM + j) * 1024);
+          }
+        }
+      } else {
+        issue1(kt, isv ? 2 * AE_HIDDEN : AE_HIDDEN, dst, isv);
+      }
+    };
     // prologue: K0 V0 K1 V1 K2 (as many as exist)
     int groups = 1;
-    issue1(0, AE_HIDDEN, lds0 + kslot(0), false);
-    issue1(0, 2 * AE_HIDDEN, lds0 + vslot(0), true);
+    issue(0, false, lds0 + kslot(0));
+    issue(0, true, lds0 + vslot(0));
     ++groups;
     if (nkt > 1) {
-      issue1(1, AE_HIDDEN, lds0 + kslot(1), false);
-      issue1(1, 2 * AE_HIDDEN, lds0 + vslot(1), true);
+      issue(1, false, lds0 + kslot(1));
+      issue(1, true, lds0 + vslot(1));
       groups += 2;
     }
     if (nkt > 2) {
-      issue1(2, AE_HIDDEN, lds0 + kslot(2), false);
+      issue(2, false, lds0 + kslot(2));
       ++groups;
     }
     wait_vm(DM * (groups - 1));  // K0 landed
     barrier();
     floatx16 sA, sB;  // S of the current / next tile, alternating by tile parity
     s_mfma(lds + kslot(0), sA);
+    if constexpr (DG == 5) sB = sA;
     wait_vm(nkt > 1 ? DM * (groups - 3) : 0);  // V0 (and K1) landed
     barrier();  // every wave has read K0 (its slot takes K3) and sees V0, K1
     // one tile; R = kt % 6 fixes the slots (R % 3) and the S buffers (R % 2) at compile time, so
@@ -332,36 +385,56 @@ __global__ __launch_bounds__(256, PIPE == 5 ? 3 : 2) void attn_pp_kernel(const u
       constexpr uint32_t VS_ISS = (3 + (R + 2) % 3) * P::TILE, KS_ISS = (R % 3) * P::TILE;
       int n_iss = 0;
       if (kt + 2 < nkt) {
-        issue1(kt + 2, 2 * AE_HIDDEN, lds0 + VS_ISS, true);
+        issue(kt + 2, true, lds0 + VS_ISS);
         n_iss += DM;
       }
       if (kt + 3 < nkt) {
-        issue1(kt + 3, AE_HIDDEN, lds0 + KS_ISS, false);
+        issue(kt + 3, false, lds0 + KS_ISS);
         n_iss += DM;
       }
       // deferred rescale (cdna_hip_programming.md T13): keep the running max unless some row's
       // tile max exceeds it by more than 8 (log2 domain), so P <= 2^8 and the O rescale runs only
       // on the tiles that move a max by that much — the same softmax with another reference max
-      float mt = -INFINITY;
-      if ((kt + 1) * KT <= len) {
+      float m_new = 0.f, alpha = 1.f;
+      bool grow = false;
+      if constexpr (DG != 2) {
+        float mt = -INFINITY;
+        if ((kt + 1) * KT <= len) {
 #pragma unroll
-        for (int r = 0; r < 16; r += 2) mt = fmaxf(mt, fmaxf(s_cur[r], s_cur[r + 1]));
-      } else {
+          for (int r = 0; r < 16; r += 2) mt = fmaxf(mt, fmaxf(s_cur[r], s_cur[r + 1]));
+        } else {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const bool in = kt * KT + mfma32_row(r, lh) < len;
-          s_cur[r] = in ? s_cur[r] : -INFINITY;
-          mt = fmaxf(mt, s_cur[r]);
+          for (int r = 0; r < 16; ++r) {
+            const bool in = kt * KT + mfma32_row(r, lh) < len;
+            s_cur[r] = in ? s_cur[r] : -INFINITY;
+            mt = fmaxf(mt, s_cur[r]);
+          }
         }
+        if constexpr (FAST) {
+          // lanes l and l ^ 32 hold the two halves of a query's keys: swap the halves on the VALU
+          const auto sw = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(uint32_t, mt),
+                                                          __builtin_bit_cast(uint32_t, mt), false, false);
+          mt = fmaxf(__builtin_bit_cast(float, (uint32_t)sw[0]), __builtin_bit_cast(float, (uint32_t)sw[1]));
+        } else {
+          mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+        }
+        grow = __any(mt > m_run + 8.f);
+        m_new = grow ? fmaxf(m_run, mt) : m_run;
+        alpha = __builtin_amdgcn_exp2f(m_run - m_new);  // 1 when m_new == m_run; 0 from -inf
       }
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-      const bool grow = __any(mt > m_run + 8.f);
-      const float m_new = grow ? fmaxf(m_run, mt) : m_run;
-      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);  // 1 when m_new == m_run; 0 from -inf
       bf16x8 ph[2], pl[2];
       __builtin_amdgcn_sched_barrier(0);
-      const float psum = exp_split(s_cur, m_new, ph, pl);
-      s_mfma(lds + KS_NEXT, s_next);
+      float psum;
+      if constexpr (DG == 1) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) ph[r >> 3][r & 7] = (__bf16)s_cur[r];
+        pl[0] = ph[0];
+        pl[1] = ph[1];
+        psum = s_cur[0];
+      } else {
+        psum = exp_split(s_cur, m_new, ph, pl);
+      }
+      if constexpr (DG != 5) s_mfma(lds + KS_NEXT, s_next);
       __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
 #pragma unroll
       for (int i = 0; i < 12; ++i) {
@@ -375,7 +448,12 @@ __global__ __launch_bounds__(256, PIPE == 5 ? 3 : 2) void attn_pp_kernel(const u
 #pragma unroll
         for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
       }
-      pv_mfma(lds + VS_CUR, ph, pl);
+      if constexpr (DG == 4) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) { o0[r] += (float)ph[0][r]; o1[r] += (float)pl[1][r]; }
+      } else {
+        pv_mfma(lds + VS_CUR, ph, pl);
+      }
       wait_vm(n_iss);  // V_{kt+1}, K_{kt+2} landed; this iteration's DMA stays in flight
       barrier();
     };
@@ -481,7 +559,7 @@ __global__ __launch_bounds__(256, PIPE == 5 ? 3 : 2) void attn_pp_kernel(const u
 
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-  if constexpr (PIPE == 6) {
+  if constexpr (PB == 6) {
     // O through LDS (rows of 66 floats: 8-B aligned, 2-way on the column writes), then 16-B
     // stores of whole output chunks: 8 (planes) or 8 (f32) store instructions per wave instead of
     // one 2-B store per row and plane
@@ -1484,7 +1562,7 @@ hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op
   if (np != 1 && np != 2) return hipErrorInvalidValue;
   dim3 grid((max_q + QPB - 1) / QPB, heads, n), block(256);
 #define APP_LAUNCH(N, M, PL)                                                                 \
-  hipLaunchKernelGGL((attn_pp_kernel<N, M, PL, (M && PIPE >= 6) ? 4 : (PIPE >= 7 ? 6 : PIPE)>), grid, block, 0,      \
+  hipLaunchKernelGGL((attn_pp_kernel<N, M, PL, (M && PIPE >= 6) ? 4 : (PIPE >= 60 ? PIPE : PIPE >= 7 ? 6 : PIPE)>), grid, block, 0,      \
                      stream, qkvp, out, op, cu,                                                 \
                      q_rows, mask, mask_L)
 #define APP_MP(N)                                                      \
@@ -1534,11 +1612,20 @@ hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op
 #undef APP_LAUNCH
   return hipGetLastError();
 }
-// production loop: PIPE 6 (tools/attn_bench.py, B=64 x L=512, same box, interleaved rounds:
-// pp4 198.3 / pp6 190.8 us median, profiles/r3n_attn_ab.jsonl; before it pp1 197.0 / pp4 192.6,
-// ragged 129.1 / 126.5, profiles/r3i_attn_ab.jsonl); the masked launches keep PIPE 4.  PIPE 2-3
-// (packed split) and 5 (3 workgroups per CU) measured no better than 4.
-constexpr int APP_PIPE = 6;
+// production loop: PIPE 66 = PIPE 6 with saddr DMA and the permlane row max, at three
+// workgroups per CU (168 registers): packed-plane output (the engine's launch), B=64 x L=512, same
+// box, interleaved rounds: pp6 192.3 / pp66 172.2 us median, ragged 138.6 / 123.5
+// (profiles/r3y_attn_diag_ab.jsonl; again 207.7 / 178.3 and 130.6 / 125.3 on another box,
+// profiles/r3z_attn_spec_ab.jsonl).  Before it PIPE 6 over PIPE 4 (pp4 198.3 / pp6 190.8 us,
+// profiles/r3n_attn_ab.jsonl) and PIPE 4 over 1 (197.0 / 192.6, ragged 129.1 / 126.5,
+// profiles/r3i_attn_ab.jsonl); the masked launches keep PIPE 4.  PIPE 2-3 (packed split) and 5 (3
+// workgroups per CU of PIPE 4) measured no better than 4.  Measured and not kept: the tile's P
+// computed against the running max before the tile max is known (recomputed when the max
+// moves; bit-identical) 190.7 vs 178.3 us, and that on packed pairs 191.6
+// (profiles/r3z_attn_spec_ab.jsonl).  PIPE 61-65 timing diagnostics of 66 (r3y): without the
+// exp / split 160.5 us, without the tile max 161.5, without barriers 176.1, without the next
+// tile's S MFMAs 151.7 of 172.2 — no single stage bounds the loop.
+constexpr int APP_PIPE = 66;
 }  // namespace
 
 extern "C" hipError_t ae_launch_attention_pp(const unsigned short* qkvp, float* out,
@@ -1552,14 +1639,25 @@ extern "C" hipError_t ae_launch_attention_pp(const unsigned short* qkvp, float* 
 // Kernel experiments (tools/attn_bench.py, tests): variant 0 = two-stage loop, 1 = pipelined,
 // 2 = pipelined with the packed / branch-free tile (PIPE 2 above), 3 = 2 without the
 // interleave hints, 4 = the previous production loop (rounded split, branch-free rescale,
-// interleave hints), 5 = 4 at three workgroups per CU, 6 = the production loop (3-slot rings,
-// deferred rescale), 7 = attn_pp8_kernel (8-wave ping-pong, keys split over two groups).
+// interleave hints), 5 = 4 at three workgroups per CU, 6 = the round-3 loop (3-slot rings,
+// deferred rescale), 7 = attn_pp8_kernel (8-wave ping-pong, keys split over two groups), 8 =
+// attn_pw64_kernel, 9 = attn_kt64_kernel, 61-65 = timing diagnostics of 66 (WRONG results), 66 =
+// the production loop.
 // (An XCD-aware workgroup order — the q-blocks of one (sequence, head) on one XCD — measured 2-3 %
 // slower, profiles/r2i_attn_pp_ab.jsonl: the K/V re-reads are Infinity-Cache hits, not the bound.)
 extern "C" hipError_t ae_bench_attention_pp(const unsigned short* qkvp, float* out,
                                             unsigned short* op, const int* cu, const int* q_rows,
                                             int max_q, int n, int heads, const uint32_t* mask,
                                             int mask_L, int np, int variant, hipStream_t stream) {
+  switch (variant) {  // PIPE 6 diagnostics / the saddr + permlane form (see attn_pp_kernel)
+    case 61: return app_launch<61>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
+    case 62: return app_launch<62>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
+    case 63: return app_launch<63>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
+    case 64: return app_launch<64>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
+    case 65: return app_launch<65>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
+    case 66: return app_launch<66>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
+    default: break;
+  }
   if (variant == 9)
     return app_launch<9>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
   if (variant == 8)

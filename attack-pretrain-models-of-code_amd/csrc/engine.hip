@@ -29,6 +29,9 @@ hipError_t ae_launch_attention_f32(const float*, float*, const int*, const int*,
                                    const uint32_t*, int, hipStream_t);
 hipError_t ae_launch_attention_pp(const unsigned short*, float*, unsigned short*, const int*,
                                   const int*, int, int, int, const uint32_t*, int, int, hipStream_t);
+hipError_t ae_bench_attention_pp(const unsigned short*, float*, unsigned short*, const int*,
+                                 const int*, int, int, int, const uint32_t*, int, int, int,
+                                 hipStream_t);
 hipError_t ae_launch_attention_x3(const float*, float*, unsigned short*, const int*, const int*,
                                   int, int, int, const uint32_t*, int, int, hipStream_t);
 hipError_t ae_launch_gemm_packed(const unsigned short*, const unsigned short*, const float*,
@@ -133,6 +136,9 @@ struct ae_engine {
   bool split = false;
   int split_parts = 2;  // parts of the batch, each on its own stream (AE_SPLIT_PARTS, 2..4)
   int split_lag = 1;    // a part starts after this many of the previous part's layer-0 kernels
+  // experiments (AE_ATTN_VARIANT, tools/engine_ab.py): an attention_pp loop variant other than the
+  // production one for the unmasked launches (0 = production)
+  int attn_variant = 0;
   hipStream_t sts[kMaxParts] = {};  // sts[0] unused: part 0 runs on the caller's stream
   hipEvent_t ev_fork = nullptr, ev_lag[kMaxParts] = {}, ev_join[kMaxParts] = {};
   // profiling: event pairs are created when profiling is switched on (never inside the timed
@@ -363,6 +369,16 @@ int gemm_pk_ln(ae_engine* e, const unsigned short* A, const unsigned short* Wp, 
   return AE_OK;
 }
 
+// attention over packed planes: the production loop, or an experiment variant (unmasked launches)
+hipError_t attention_pp(ae_engine* e, const unsigned short* qkvp, float* out, unsigned short* op,
+                        const int* cu, const int* q_rows, int max_q, int n, int heads,
+                        const uint32_t* mask, int mask_L, int np, hipStream_t st) {
+  if (e->attn_variant && !mask)
+    return ae_bench_attention_pp(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np,
+                                 e->attn_variant, st);
+  return ae_launch_attention_pp(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, st);
+}
+
 // One full encoder layer of the split-precision path over the token rows [t0, t0 + M) of the
 // sequences [s0, s0 + ns) on stream st, with the residual + LayerNorm as their own kernels (the
 // two-stream encoder; results equal the fused path's to LayerNorm rounding).
@@ -385,9 +401,9 @@ int layer_rows(ae_engine* e, const LayerW& w, int64_t t0, int M, int s0, int ns,
     return rc;
   {
     Prof p(e, st, e->prof_kind == AE_KIND_ATTENTION, 0.0);
-    HIPC(ae_launch_attention_pp(qkvp, e->ctx, e->cp, e->cu + s0, nullptr, max_len, ns,
-                                e->cfg.heads, mask_bits ? mask_bits + (size_t)s0 * L * (L / 32) : nullptr,
-                                L, np, st));
+    HIPC(attention_pp(e, qkvp, e->ctx, e->cp, e->cu + s0, nullptr, max_len, ns,
+                      e->cfg.heads, mask_bits ? mask_bits + (size_t)s0 * L * (L / 32) : nullptr,
+                      L, np, st));
   }
   if ((rc = done())) return rc;
   if ((rc = gemm_pk(e, e->cp + t0 * H * np, w.wo_p, w.bo, x, tmp, nullptr, M, H, H,
@@ -477,9 +493,9 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
         HIPC(ae_launch_attention_f32(e->qkv, e->ctx, e->cu, last_cls ? e->one : nullptr,
                                      last_cls ? 1 : max_len, n, heads, mask_bits, L, st));
       else
-        HIPC(ae_launch_attention_pp(qkvp, e->ctx, last_cls ? nullptr : e->cp, e->cu,
-                                    last_cls ? e->one : nullptr, last_cls ? 1 : max_len, n, heads,
-                                    mask_bits, L, e->np, st));
+        HIPC(attention_pp(e, qkvp, e->ctx, last_cls ? nullptr : e->cp, e->cu,
+                          last_cls ? e->one : nullptr, last_cls ? 1 : max_len, n, heads,
+                          mask_bits, L, e->np, st));
     }
     if (!last_cls && pl) {
       // O-proj + residual + LN1 and FFN2 + residual + LN2 each one kernel (x updated in place)
@@ -685,6 +701,8 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
     e->split = !(sp && sp[0] == '0');
     const char* lag = std::getenv("AE_SPLIT_LAG");  // experiments: 1 (QKV) .. 7 (whole layer 0)
     if (lag && lag[0] >= '1' && lag[0] <= '7') e->split_lag = lag[0] - '0';
+    const char* av = std::getenv("AE_ATTN_VARIANT");  // experiments: e.g. 6 (the round-3 loop)
+    if (av) e->attn_variant = std::atoi(av);
     const char* parts = std::getenv("AE_SPLIT_PARTS");  // experiments: 2 (default) .. 4
     if (parts && parts[0] >= '2' && parts[0] <= '4') e->split_parts = parts[0] - '0';
     if (e->split) {

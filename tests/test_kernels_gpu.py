@@ -224,7 +224,7 @@ def _qkv_planes(qkv, np_):
     return _pack(hi, lo, np_)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 66])
 @pytest.mark.parametrize("np_", [2, 1])
 @pytest.mark.parametrize("case", ["ragged", "mask", "cls", "planes", "grow"])
 def test_attention_pp_matches_f64(gpu, np_, case, variant):
@@ -232,7 +232,7 @@ def test_attention_pp_matches_f64(gpu, np_, case, variant):
     reads) against the float64 reference, for both plane counts (np 1 = bf16 mode: stated
     tolerance 2e-2), every loop (1: software-pipelined, 6: 3-slot rings + deferred rescale, 7: the
     8-wave ping-pong kernel with the keys split between its two groups and merged, 8: 4 waves x
-    64 queries, one wave per SIMD, 9: 64-key tiles) and
+    64 queries, one wave per SIMD, 9: 64-key tiles, 66 (production): 6 with saddr DMA and a permlane row max) and
     the ragged / mask / CLS-only / packed-output launches.  "grow": spike keys whose scores
     rise along the sequence, so every row max jumps past the deferred-rescale threshold (2^8)
     several times — the rare branch of variant 6."""
@@ -289,6 +289,43 @@ def test_attention_pp_matches_f64(gpu, np_, case, variant):
     assert torch.isfinite(got).all()
     err = (got - ref).abs()
     assert (err <= tol).all(), float(err.max())
+
+
+@pytest.mark.parametrize("case", ["ragged", "grow"])
+def test_attention_pp_restructured_loops_bit_identical(gpu, case):
+    """Variant 66 (production: saddr DMA with clamped offsets in the last tile, permlane row max,
+    three workgroups per CU) restructures PIPE 6 without changing its arithmetic: its packed-plane
+    context must equal PIPE 6's bit for bit."""
+    lib = _lib()
+    vp, i32 = ctypes.c_void_p, ctypes.c_int32
+    lib.ae_bench_attention_pp.argtypes = [vp] * 5 + [i32] * 3 + [vp, i32, i32, i32, vp]
+    lib.ae_bench_attention_pp.restype = ctypes.c_int
+    g = torch.Generator().manual_seed(5)
+    lens = [1, 31, 32, 33, 129, 300, 512, 64] if case == "ragged" else [300, 517, 64]
+    n = len(lens)
+    cu = torch.zeros(n + 1, dtype=torch.int32)
+    cu[1:] = torch.cumsum(torch.tensor(lens), 0)
+    T = int(cu[-1])
+    qkv = torch.randn(T, 3 * 768, generator=g)
+    if case == "grow":  # row maxes jump past the deferred-rescale threshold several times
+        qkv *= 0.25
+        qkv[:, :768] += 1.0
+        start = 0
+        for x in lens:
+            for p_, c in ((40, 0.75), (100, 1.625), (200, 2.5), (400, 3.375)):
+                if p_ < x:
+                    qkv[start + p_, 768:1536] = c
+            start += x
+    dq, dcu = _qkv_planes(qkv, 2).cuda(), cu.cuda()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    outs = {}
+    for v in (6, 66):
+        op = torch.zeros((T, 2 * 768), dtype=torch.int16, device="cuda")
+        assert lib.ae_bench_attention_pp(_p(dq), None, _p(op), _p(dcu), None, max(lens), n, 12,
+                                         None, 0, 2, v, st) == 0
+        outs[v] = op
+    torch.cuda.synchronize()
+    assert torch.equal(outs[66], outs[6])
 
 
 @pytest.mark.parametrize("M,K,np_", [(300, 768, 2), (512, 3072, 2), (1000, 768, 1), (37, 768, 2),
