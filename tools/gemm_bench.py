@@ -45,10 +45,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--entry", default="ae_bench_gemm_packed")
+    ap.add_argument("--lib", default=None, help="engine library to load (A/B of build flags)")
     args = ap.parse_args()
 
     from apmc_amd.engine import load_library
-    lib = load_library()
+    lib = load_library(args.lib)
     vp, i32 = ctypes.c_void_p, ctypes.c_int32
     fn = getattr(lib, args.entry)
     fn.argtypes = [vp] * 6 + [i32] * 7 + [vp]
