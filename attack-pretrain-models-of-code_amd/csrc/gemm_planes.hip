@@ -721,36 +721,44 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own region: no barrier
     constexpr int RPI = 64 / CPR;  // rows per store instruction
+    // a lane keeps its 16-B column chunk c for the whole half and moves down RPI rows per store:
+    // 32-bit element offsets from the half's uniform base row, one multiply per lane instead of a
+    // 64-bit row x stride product per store (three quarter-rate integer ops each)
+    const int lr0 = lane / CPR, c = lane % CPR;
+    const int rbase = m0 + wm * 128 + half * 64;
+    const uint32_t ldc = (uint32_t)(PACKED ? NP * N : N);  // elements per output row
+    uint32_t off0 = (uint32_t)lr0 * ldc + (PACKED ? c * 8 : 4 * c);
+    asm("" : "+v"(off0));  // opaque: keeps the per-store offset an add (no re-derived multiply)
+    // 16 B of the packed row: column block (c*16 / (64 NP)), all within the wave's 64 columns
+    const int col = PACKED ? cb0 + (c * 16) / (2 * NP) : cb0 + 4 * c;
+    floatx4 bv = {0.f, 0.f, 0.f, 0.f};
+    if (!PACKED && col < N) bv = *reinterpret_cast<const floatx4*>(bias + col);
 #pragma unroll
     for (int k = 0; k < 64 / RPI; ++k) {
-      const int lr = k * RPI + lane / CPR, c = lane % CPR;
-      const int row = m0 + wm * 128 + half * 64 + lr;
-      const bool ok = row < M;
+      const int lr = k * RPI + lr0;
+      const bool ok = rbase + lr < M;
       const uint4 v = *reinterpret_cast<const uint4*>(reg + lr * RB + ((c ^ (lr & 15)) & (CPR - 1)) * 16);
+      const uint32_t o = off0 + (uint32_t)(k * RPI) * ldc;
       if (PACKED) {
-        // 16 B of the packed row: column block (c*16 / (64 NP)), all within the wave's 64 columns
-        const int col = cb0 + (c * 16) / (2 * NP);  // first column this chunk belongs to (>= block start)
         if (ok && col < N) {
-          __bf16* dstp = Cp + (size_t)row * NP * N + (size_t)(cb0 >> 5) * 32 * NP + c * 8;
+          __bf16* dstp = Cp + (size_t)rbase * NP * N + (size_t)(cb0 >> 5) * 32 * NP + o;
           if (DIAG != 8)
             __builtin_nontemporal_store(__builtin_bit_cast(floatx4, v), reinterpret_cast<floatx4*>(dstp));
           else
             *reinterpret_cast<uint4*>(dstp) = v;
         }
       } else {
-        const int col = cb0 + 4 * c;
         if (ok && col < N) {
-          const size_t o = (size_t)row * N + col;
-          floatx4 f = __builtin_bit_cast(floatx4, v);
-          f += *reinterpret_cast<const floatx4*>(bias + col);
+          floatx4 f = __builtin_bit_cast(floatx4, v) + bv;
           if (EPI == PK_EPI_TANH)
 #pragma unroll
             for (int i = 0; i < 4; ++i) f[i] = tanhf(f[i]);
-          if (EPI == PK_EPI_RES) f += *reinterpret_cast<const floatx4*>(R + o);
+          float* dst = C + (size_t)rbase * N + cb0 + o;
+          if (EPI == PK_EPI_RES) f += *reinterpret_cast<const floatx4*>(R + (size_t)rbase * N + cb0 + o);
           if (DIAG != 8)
-            __builtin_nontemporal_store(f, reinterpret_cast<floatx4*>(C + o));
+            __builtin_nontemporal_store(f, reinterpret_cast<floatx4*>(dst));
           else
-            *reinterpret_cast<floatx4*>(C + o) = f;
+            *reinterpret_cast<floatx4*>(dst) = f;
         }
       }
     }
@@ -1131,16 +1139,19 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
       }
       // 8 consecutive columns per lane: x as two 16-B stores, each plane as one 16-B store (24
       // store instructions per pass, all 16 B per lane; was 36, two thirds of them 8 B)
+      // round k = 3 g + kk: round kk's chunks 16 g rows further down (see the f32 epilogue)
 #pragma unroll
       for (int k = 0; k < 6; ++k) {
-        const int idx = k * 64 + lane, lr = idx / 12, c8 = idx % 12;
+        const int kk = k % 3, g = k / 3;
+        const int idx = kk * 64 + lane, lr = idx / 12 + 16 * g, c8 = idx % 12;
         const int row = prow0 + tm * 32 + lr;
         const floatx4 o0 = *reinterpret_cast<const floatx4*>(reg + lr * RS + c8 * 32);
         const floatx4 o1 = *reinterpret_cast<const floatx4*>(reg + lr * RS + c8 * 32 + 16);
         if (row < M) {
           const int col = cb0 + 8 * c8;
-          *reinterpret_cast<floatx4*>(C + (size_t)row * N + col) = o0;
-          *reinterpret_cast<floatx4*>(C + (size_t)row * N + col + 4) = o1;
+          float* const xrow = C + (size_t)prow0 * N + (uint32_t)(lr + tm * 32) * (uint32_t)N;
+          *reinterpret_cast<floatx4*>(xrow + col) = o0;
+          *reinterpret_cast<floatx4*>(xrow + col + 4) = o1;
           uint32_t h[4], l[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
@@ -1150,8 +1161,9 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
             l[i] = (uint32_t)f2bf(a - __builtin_bit_cast(float, ha << 16)) |
                    ((uint32_t)f2bf(b - __builtin_bit_cast(float, hb << 16)) << 16);
           }
-          unsigned short* dst = reinterpret_cast<unsigned short*>(ln.xp) + (size_t)row * NP * N +
-                                (size_t)(col >> 5) * 32 * NP + (col & 31);
+          unsigned short* dst = reinterpret_cast<unsigned short*>(ln.xp) + (size_t)prow0 * NP * N +
+                                (uint32_t)(lr + tm * 32) * (uint32_t)(NP * N) +
+                                (uint32_t)((col >> 5) * 32 * NP + (col & 31));
           *reinterpret_cast<uint4*>(dst) = uint4{h[0], h[1], h[2], h[3]};
           if (NP == 2) *reinterpret_cast<uint4*>(dst + 32) = uint4{l[0], l[1], l[2], l[3]};
         }
@@ -1167,6 +1179,21 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
   constexpr int RS = 400;
   unsigned char* reg = pk_smem + wave * 32 * RS;
   const int cb0 = n0 + sn * 96;
+  // store round k = 3 g + kk covers chunks 64 k + lane of the pass's 32 x 24 = round kk's chunks
+  // 8 g rows further down: the three rounds' (row, column) and 32-bit offsets from the wave's
+  // first row are computed once, every other round adds a uniform 8 g rows
+  const int rbase = m0 + wm * 128 + sm * 64;
+  int lrk[3], ck[3];
+  uint32_t offk[3];
+#pragma unroll
+  for (int kk = 0; kk < 3; ++kk) {
+    const int idx = kk * 64 + lane;
+    lrk[kk] = idx / 24;
+    ck[kk] = idx % 24;
+    offk[kk] = (uint32_t)lrk[kk] * (uint32_t)N + 4 * ck[kk];
+    asm("" : "+v"(offk[kk]));  // opaque: keeps the per-store offset an add
+  }
+  float* const cbase = C + (size_t)rbase * N + cb0;
 #pragma unroll
   for (int tm = 0; tm < 2; ++tm) {
 #pragma unroll
@@ -1181,21 +1208,22 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int k = 0; k < 12; ++k) {
-      const int idx = k * 64 + lane, lr = idx / 24, c = idx % 24;
-      const int row = m0 + wm * 128 + sm * 64 + tm * 32 + lr;
+      const int kk = k % 3, g = k / 3;
+      const int lr = lrk[kk] + 8 * g, c = ck[kk];
+      const int row = rbase + tm * 32 + lr;
       const int col = cb0 + 4 * c;
       floatx4 f = *reinterpret_cast<const floatx4*>(reg + lr * RS + c * 16);
       if (row < M && col < N) {
-        const size_t o = (size_t)row * N + col;
+        const uint32_t o = offk[kk] + (uint32_t)(tm * 32 + 8 * g) * (uint32_t)N;
         f += *reinterpret_cast<const floatx4*>(bias + col);
         if (EPI == PK_EPI_TANH)
 #pragma unroll
           for (int i = 0; i < 4; ++i) f[i] = tanhf(f[i]);
-        if (EPI == PK_EPI_RES) f += *reinterpret_cast<const floatx4*>(R + o);
+        if (EPI == PK_EPI_RES) f += *reinterpret_cast<const floatx4*>(R + (size_t)rbase * N + cb0 + o);
         if (NT)
-          __builtin_nontemporal_store(f, reinterpret_cast<floatx4*>(C + o));
+          __builtin_nontemporal_store(f, reinterpret_cast<floatx4*>(cbase + o));
         else
-          *reinterpret_cast<floatx4*>(C + o) = f;
+          *reinterpret_cast<floatx4*>(cbase + o) = f;
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

@@ -31,6 +31,10 @@ SHAPES = {  # name: (N, K, epilogue) with M = tokens (64 x 512 by default)
     "oproj": (768, 768, 0),
     "ffn1": (3072, 768, 1),
     "ffn2": (768, 3072, 0),
+    # the encoder's own epilogues: QKV -> packed planes, O-proj / FFN2 + residual (two-stream)
+    "qkvp": (2304, 768, 4),
+    "oproj_res": (768, 768, 2),
+    "ffn2_res": (768, 3072, 2),
     # fused residual + LayerNorm (ae_bench_gemm_packed_ln; the variant's diag is its mode)
     "oproj_ln": (768, 768, 5),
     "ffn2_ln": (768, 3072, 5),
@@ -92,8 +96,10 @@ def main():
         bias = torch.zeros(N, device=dev)
         C = torch.empty((M, N), device=dev)
         Cp = torch.empty((M, 2 * N), dtype=torch.bfloat16, device=dev)
-        if epi == 5:
+        R = None
+        if epi in (2, 5):
             R = torch.randn((M, N), generator=g, device=dev)
+        if epi == 5:
             gam, bet = torch.ones(N, device=dev), torch.zeros(N, device=dev)
             blocks = (M + 255) // 256
             stats = torch.zeros(blocks * 256 * 4, dtype=torch.int64, device=dev)
@@ -113,8 +119,8 @@ def main():
                                        np_, max(diag, 1), sp))
             else:
                 call = (lambda A=A, W=W, bias=bias, C=C, Cp=Cp, N=N, K=K, epi=epi, np_=np_, bn=bn,
-                        diag=diag: fn(p(A), p(W), p(bias), p(None), p(C), p(Cp), M, N, K, epi,
-                                      np_, bn, diag, sp))
+                        diag=diag, R=R: fn(p(A), p(W), p(bias), p(R), p(C), p(Cp), M, N, K, epi,
+                                           np_, bn, diag, sp))
             rc = call()
             if rc != 0:
                 print(json.dumps({"shape": name, "variant": [diag, bn, np_], "error": rc}))
