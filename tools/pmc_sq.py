@@ -42,14 +42,14 @@ for run in sorted(root.glob("pmc_p*")):
             key = (r["Kernel_Name"].split("(")[0], int(r["Grid_Size_X"]) * int(r.get("Grid_Size_Y", 1) or 1)
                    * int(r.get("Grid_Size_Z", 1) or 1))
             if any(p in key[0] for p in pats):
-                dur[key[0]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+                dur[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 
 out = []
 for (name, grid), cs in sorted(agg.items(), key=lambda kv: -len(kv[1])):
     m = {c: statistics.mean(v) for c, v in cs.items()}
     rec = {"kernel": name, "grid": grid, "dispatches": max(len(v) for v in cs.values()),
            "counters_mean": {c: round(v, 1) for c, v in sorted(m.items())}}
-    us = statistics.mean(dur[name]) if dur.get(name) else None
+    us = statistics.mean(dur[(name, grid)]) if dur.get((name, grid)) else None
     rec["avg_duration_us_profiled"] = round(us, 2) if us else None
     g = m.get("GRBM_GUI_ACTIVE")
     if g and us:
