@@ -774,6 +774,309 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
+// Role-split persistent ping-pong GEMM (gemm_pprs_kernel; experiment, packed-plane epilogues
+// only, reachable through ae_bench_gemm_packed diag 10 / 11).
+//
+// gemm_pp_kernel's main loop and tile order on a persistent grid, arranged so that a tile's
+// epilogue write burst drains behind the next tile's MFMAs.  vmcnt is per wave and counts stores
+// and loads in issue order, so a wave that stores cannot wait for a DMA issued after its stores
+// without waiting for the stores too.  Hence the roles alternate by tile: at the end of local tile
+// i only wave group (i & 1) issues the tile's global stores (its own 64-row blocks and its
+// partner's — wave w ^ 4 — through the LDS staging regions); for the prologue and the first H
+// K-tiles of tile i + 1 the other group issues every DMA piece (its own and its partner's, the
+// counted waits doubled) while the storing group issues and waits for nothing.  From K-tile H on
+// both groups run the production schedule; the storing group's first wait (for a piece it issued
+// itself, at K-tile H + 1) comes after its stores in the queue, by then H K-tiles of MFMAs later.
+// DMA sources as saddr offsets: per-lane 32-bit byte offsets from the tile's first A / W row,
+// the K-tile advance on the scalar base.
+namespace {
+__device__ __forceinline__ void dma16s_pk(uint32_t voff, const void* sbase, uint32_t lds_base) {
+  asm volatile(
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %0, %1"
+      :
+      : "v"(voff), "s"(sbase), "s"(lds_base)
+      : "memory", "m0");
+}
+// s_waitcnt vmcnt(x) with x the largest supported value <= n (waiting longer is always safe)
+__device__ __forceinline__ void pprs_wait(int n) {
+  if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (n >= 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+}  // namespace
+
+template <int NP, int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_pprs_kernel(
+    const __bf16* __restrict__ A, const __bf16* __restrict__ W, const float* __restrict__ bias,
+    __bf16* __restrict__ Cp, int M, int N, int K, int group_m, int H) {
+  static_assert(EPI == PK_EPI_GELU_PACKED || EPI == PK_EPI_BIAS_PACKED, "packed epilogues only");
+  extern __shared__ __attribute__((aligned(16))) unsigned char pk_smem[];
+  constexpr int BM = 256, BN = 256, ROWB = PK_ROWB;
+  constexpr int A_BYTES = BM * ROWB, STAGE = (BM + BN) * ROWB;
+  constexpr int KB = 64 / NP, NS = KB / 16, T = NP == 2 ? 3 : 1;
+  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM, tiles = tiles_m * tiles_n;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int lda = NP * K;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)pk_smem;
+  const int nk = K / KB;
+  const bool split_ok = nk >= H + 3;  // enough K-tiles for the hand-over (uniform)
+
+  int it = 0;
+  for (int vb = blockIdx.x; vb < tiles; vb += gridDim.x, ++it) {
+    // the lane id made opaque per tile: every lane-derived address is recomputed inside the tile
+    // instead of hoisted out of the tile loop (which spills)
+    int lane = tid & 63;
+    asm volatile("" : "+v"(lane));
+    const int li = lane & 31, lh = lane >> 5;
+    const int sw = (li >> 1) & 7;
+    const int a_row = (wm * 128 + li) * ROWB;
+    const int w_row = A_BYTES + (wn * 64 + li) * ROWB;
+    const int t = xcd_remap(vb, tiles);
+    const int per_group = group_m * tiles_n;
+    const int g = t / per_group, first_m = g * group_m;
+    const int gsize = min(tiles_m - first_m, group_m);
+    const int tm0 = first_m + (t - g * per_group) % gsize, tn0 = (t - g * per_group) / gsize;
+    const int m0 = tm0 * BM, n0 = tn0 * BN;
+    // roles of this tile's hand-over (tile it - 1 was stored by group (it - 1) & 1)
+    const bool hand = it > 0 && split_ok;
+    const bool idle = hand && wm != (it & 1);  // stored the previous tile: no DMA before K-tile H
+    const bool dbl = hand && wm == (it & 1);   // issues its partner's pieces too
+    const char* abase = reinterpret_cast<const char*>(A + (size_t)m0 * lda);
+    const char* wbase = reinterpret_cast<const char*>(W + (size_t)n0 * lda);
+    // DMA pieces (8 rows x 128 B), as gemm_pp_kernel: [0,1] A(mh 0), [2,3] W(nh 0), [4,5] W(nh 1),
+    // [6,7] A(mh 1); off[0] this wave's, off[1] its partner's (wave ^ 4)
+    uint32_t off[2][8];
+#pragma unroll
+    for (int w2 = 0; w2 < 2; ++w2) {
+      const int wv = w2 ? (wave ^ 4) : wave;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int pidx = 2 * wv + (j & 1);
+        const bool is_a = j < 2 || j >= 6;
+        const int r0 = is_a ? (pidx >> 3) * 128 + (pidx & 7) * 8 + (j >= 6 ? 64 : 0)
+                            : (pidx >> 2) * 64 + (pidx & 3) * 8 + (j >= 4 ? 32 : 0);
+        const int r = r0 + (lane >> 3);
+        const int cs = (lane & 7) ^ ((r >> 1) & 7);
+        const int gr = is_a ? min(m0 + r, M - 1) - m0 : min(n0 + r, N - 1) - n0;
+        off[w2][j] = (uint32_t)gr * (uint32_t)(lda * 2) + 16u * cs;
+      }
+    }
+    auto piece = [&](int w2, int j, int kd) {
+      const int wv = w2 ? (wave ^ 4) : wave;
+      const int pidx = 2 * wv + (j & 1);
+      const bool is_a = j < 2 || j >= 6;
+      const int r0 = is_a ? (pidx >> 3) * 128 + (pidx & 7) * 8 + (j >= 6 ? 64 : 0)
+                          : (pidx >> 2) * 64 + (pidx & 3) * 8 + (j >= 4 ? 32 : 0);
+      const uint32_t dst = (is_a ? 0u : (uint32_t)A_BYTES) + (uint32_t)r0 * ROWB;
+      dma16s_pk(off[w2][j], (is_a ? abase : wbase) + (size_t)kd * ROWB,
+                lds0 + (kd & 1) * STAGE + dst);
+    };
+    // quarter q of K-tile kd, by the roles in force at loop K-tile kt (kt = -1: the prologue)
+    auto issue_q = [&](int q, int kd, int kt) {
+      const bool early = kt < H;
+      if (!(idle && early)) {
+        piece(0, 2 * q, kd);
+        piece(0, 2 * q + 1, kd);
+      }
+      if (dbl && early) {
+        piece(1, 2 * q, kd);
+        piece(1, 2 * q + 1, kd);
+      }
+    };
+
+    floatx16 acc[4][2];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+    bf16x8 fa[2][NS][NP];
+    bf16x8 fw[2][NS][NP];
+    auto read_a = [&](const unsigned char* st, int mh) {
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+          for (int p = 0; p < NP; ++p)
+            fa[tt][s][p] = *reinterpret_cast<const bf16x8*>(
+                st + a_row + (2 * mh + tt) * 32 * ROWB + 16 * ((4 * p + 2 * s + lh) ^ sw));
+    };
+    auto read_w = [&](const unsigned char* st, int nh) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+          fw[nh][s][p] = *reinterpret_cast<const bf16x8*>(
+              st + w_row + nh * 32 * ROWB + 16 * ((4 * p + 2 * s + lh) ^ sw));
+    };
+    // a quadrant's MFMAs with DMA quarter q of K-tile kd in the issue gaps (both halves of the
+    // quarter's pieces after the first and second thirds of the MFMAs, as gemm_pp_kernel)
+    auto mfma_quad = [&](int mh, int nh, auto qc, bool dma, int kd, int kt) {
+      constexpr int q = decltype(qc)::value;
+      constexpr int NM = NS * 2 * T;
+      const bool own = dma && !(idle && kt < H), part = dma && dbl && kt < H;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < NM; ++i) {
+        const int s = i / (2 * T), tt = (i / T) % 2, term = i % T;
+        floatx16& c = acc[2 * mh + tt][nh];
+        const bf16x8& x = (T == 3 && term == 1) ? fw[nh][s][NP - 1] : fw[nh][s][0];
+        const bf16x8& y = (T == 3 && term == 0) ? fa[tt][s][NP - 1] : fa[tt][s][0];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, c, 0, 0, 0);
+        if (i == NM / 3 - 1 || i == 2 * NM / 3 - 1) {
+          const int j = 2 * q + (i == NM / 3 - 1 ? 0 : 1);
+          __builtin_amdgcn_sched_barrier(0);
+          if (own) piece(0, j, kd);
+          if (part) piece(1, j, kd);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      __builtin_amdgcn_s_setprio(0);
+    };
+    auto sync_compute = [&]() {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto sync_load = [&]() {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    // counted wait at phase ph of K-tile kt for this wave's own pieces (see the role comment):
+    // doubled counts while it issues its partner's pieces, none while it issues nothing
+    auto wait_q = [&](int ph, int kt, bool full) {
+      if (!full) pprs_wait(0);
+      else if (idle && kt <= H) {
+      } else if (dbl && kt < H) pprs_wait(12);
+      else if (dbl && kt == H) pprs_wait(ph == 0 ? 12 : ph == 1 ? 10 : 6);
+      else pprs_wait(6);
+    };
+
+    // prologue: K-tile 0 whole and K-tile 1's first two quarters
+#pragma unroll
+    for (int q = 0; q < 4; ++q) issue_q(q, 0, -1);
+    if (nk > 1) {
+      issue_q(0, 1, -1);
+      issue_q(1, 1, -1);
+      if (!idle) pprs_wait(dbl ? 16 : 8);  // K-tile 0's A(mh 0) + W(nh 0) of what this wave issued
+    } else {
+      pprs_wait(0);
+    }
+    __builtin_amdgcn_s_barrier();
+    if (wm == 1) sync_load();  // group 1 runs one phase behind
+
+    for (int kt = 0; kt < nk; ++kt) {
+      const unsigned char* st = pk_smem + (kt & 1) * STAGE;
+      const bool next1 = kt + 1 < nk, next2 = kt + 2 < nk;
+      wait_q(0, kt, next1);
+      read_a(st, 0);
+      read_w(st, 0);
+      sync_compute();
+      mfma_quad(0, 0, std::integral_constant<int, 2>(), next1, kt + 1, kt);
+      sync_load();
+      wait_q(1, kt, next1);
+      read_w(st, 1);
+      sync_compute();
+      mfma_quad(0, 1, std::integral_constant<int, 3>(), next1, kt + 1, kt);
+      sync_load();
+      read_a(st, 1);
+      sync_compute();
+      mfma_quad(1, 1, std::integral_constant<int, 0>(), next2, kt + 2, kt);
+      sync_load();
+      wait_q(3, kt, next2);
+      sync_compute();
+      mfma_quad(1, 0, std::integral_constant<int, 1>(), next2, kt + 2, kt);
+      sync_load();
+    }
+    pprs_wait(0);  // (nothing of this tile's DMA stays in flight into the epilogue)
+    if (wm == 0) sync_load();
+
+    // ---- epilogue: every wave stages its 64-row halves in its own 16-KiB region (as
+    // gemm_pp_kernel); with the role split, group (it & 1) stores its own and its partner's
+    // regions and the other group stores nothing
+    constexpr int RB = 64 * 2 * NP, CPR = RB / 16, RPI = 64 / CPR;
+    const bool rs = split_ok;
+    const bool storer = !rs || wm == (it & 1);
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      unsigned char* reg = pk_smem + wave * 16384;
+      const int cb0 = n0 + wn * 64;
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const int lr = tt * 32 + li;
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const floatx16& c = acc[2 * half + tt][tn];
+            const int cc = tn * 32 + 8 * j + 4 * lh;
+            const int col = cb0 + cc < N ? cb0 + cc : N - 4;
+            const floatx4 bv = *reinterpret_cast<const floatx4*>(bias + col);
+            ushortx4 h, l;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float y = EPI == PK_EPI_GELU_PACKED ? gelu_erfc_fast(c[4 * j + i] + bv[i])
+                                                        : c[4 * j + i] + bv[i];
+              const __bf16 hv = (__bf16)y;
+              h[i] = __builtin_bit_cast(unsigned short, hv);
+              l[i] = f2bf(y - (float)hv);
+            }
+            const int hb = tn * 64 * NP + 2 * (8 * j + 4 * lh);
+            const int ch = ((hb >> 4) ^ (lr & 15)) & (CPR - 1);
+            *reinterpret_cast<ushortx4*>(reg + lr * RB + ch * 16 + (hb & 15)) = h;
+            if (NP == 2) {
+              const int lb = hb + 64;
+              const int cl = ((lb >> 4) ^ (lr & 15)) & (CPR - 1);
+              *reinterpret_cast<ushortx4*>(reg + lr * RB + cl * 16 + (lb & 15)) = l;
+            }
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (rs) sync_load();  // every region written before the storing group reads its partner's
+      if (storer) {
+#pragma unroll
+        for (int w2 = 0; w2 < 2; ++w2) {
+          if (w2 == 1 && !rs) break;
+          const int sw2 = w2 ? (wave ^ 4) : wave;  // whose block
+          const unsigned char* rg = pk_smem + sw2 * 16384;
+          const int lr0 = lane / CPR, c = lane % CPR;
+          const int rbase = m0 + (sw2 >> 2) * 128 + half * 64;
+          const uint32_t ldc = (uint32_t)(NP * N);
+          uint32_t off0 = (uint32_t)lr0 * ldc + c * 8;
+          asm("" : "+v"(off0));
+          const int col = cb0 + (c * 16) / (2 * NP);
+          __bf16* const tb = Cp + (size_t)rbase * NP * N + (size_t)(cb0 >> 5) * 32 * NP;
+#pragma unroll
+          for (int k = 0; k < 64 / RPI; ++k) {
+            const int lr = k * RPI + lr0;
+            const uint4 v = *reinterpret_cast<const uint4*>(rg + lr * RB + ((c ^ (lr & 15)) & (CPR - 1)) * 16);
+            if (rbase + lr < M && col < N)
+              __builtin_nontemporal_store(__builtin_bit_cast(floatx4, v),
+                                          reinterpret_cast<floatx4*>(tb + off0 + (uint32_t)(k * RPI) * ldc));
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // region reads done before it is rewritten
+      if (rs) sync_load();
+    }
+    // every wave's staging reads done before the next tile's prologue DMA rewrites the stages
+    sync_load();
+  }  // tile loop
+}
+
+// ------------------------------------------------------------------------------------------
 // Ping-pong 256 x 192 packed GEMM (gemm_pp192_kernel): the N = 768 GEMMs (O-projection, FFN2)
 // tile as 128 x 4 = 512 tiles = 2 full rounds on 256 CUs instead of 384 256^2 tiles (1.5 rounds,
 // the second half idle).  gemm_pp_kernel's structure with a 64 x 96 block per wave: group g
@@ -1272,6 +1575,21 @@ hipError_t pp_epi(int epi, const __bf16* A, const __bf16* W, const float* bias, 
   }
 }
 
+// the role-split persistent kernel (experiment): grid = min(tiles, CUs / share), H K-tiles of
+// hand-over
+template <int NP, int EPI>
+hipError_t pprs_launch(const __bf16* A, const __bf16* W, const float* bias, __bf16* Cp, int M,
+                       int N, int K, int group_m, int share, int H, hipStream_t st) {
+  constexpr int lds = 2 * (256 + 256) * PK_ROWB;  // 128 KiB
+  if (hipError_t e = ensure_dynamic_lds((const void*)gemm_pprs_kernel<NP, EPI>, lds); e != hipSuccess)
+    return e;
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  const int grid = std::max(1, std::min(tiles, cu_count() / share));
+  hipLaunchKernelGGL((gemm_pprs_kernel<NP, EPI>), dim3(grid), dim3(512), lds, st, A, W, bias, Cp,
+                     M, N, K, group_m, H);
+  return hipGetLastError();
+}
+
 template <int NP, int EPI, bool NT = false>
 hipError_t pp192_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R,
                         float* C, int M, int N, int K, int group_m, hipStream_t st,
@@ -1481,6 +1799,23 @@ extern "C" hipError_t ae_bench_gemm_packed(const unsigned short* A, const unsign
       (bn != 0 && bn != 128 && bn != 192 && bn != 256 && bn != 512))
     return hipErrorInvalidValue;
   if (bn == 192) return pp192_dispatch(A, W, bias, R, C, M, N, K, epi, np, PK_GROUP_M, st, diag == 8);
+  if (bn == 512 && diag >= 10 && diag <= 14) {  // role-split persistent kernel (experiment)
+    // 10: whole chip, H = 8; 11: half the CUs (one of two streams), H = 8; 12 / 13: H = 4 / 12;
+    // 14: no hand-over (every wave stores its own blocks: the kernel's base cost)
+    if (!Cp || (epi != PK_EPI_GELU_PACKED && epi != PK_EPI_BIAS_PACKED)) return hipErrorInvalidValue;
+    const int share = diag == 11 ? 2 : 1, H = diag == 12 ? 4 : diag == 13 ? 12 : diag == 14 ? 1 << 20 : 8;
+    auto a = reinterpret_cast<const __bf16*>(A);
+    auto w = reinterpret_cast<const __bf16*>(W);
+    auto cp = reinterpret_cast<__bf16*>(Cp);
+#define PPRS(NPV, E) return pprs_launch<NPV, E>(a, w, bias, cp, M, N, K, PK_GROUP_M, share, H, st)
+    if (np == 2) {
+      if (epi == PK_EPI_GELU_PACKED) PPRS(2, PK_EPI_GELU_PACKED);
+      PPRS(2, PK_EPI_BIAS_PACKED);
+    }
+    if (epi == PK_EPI_GELU_PACKED) PPRS(1, PK_EPI_GELU_PACKED);
+    PPRS(1, PK_EPI_BIAS_PACKED);
+#undef PPRS
+  }
   if (bn == 512) {  // the ping-pong 256 x 256 kernel
     switch (diag) {
       case 0: return pp_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);

@@ -86,6 +86,14 @@ def _p(t):
     (700, 256, 256, 1, 1, "w2"),
     (600, 3072, 768, 2, 1, "w2"),
     (129, 2304, 3072, 2, 0, "w2"),
+    # role-split persistent kernel (gemm_pprs_kernel, packed epilogues): several tiles per
+    # workgroup so the hand-over runs, ragged M / N, H = 8 and 4, the short-K fallback
+    (8200, 3072, 768, 2, 1, "512rs2"),
+    (8192, 2304, 768, 2, 4, "512rs"),
+    (8192, 2304, 768, 2, 4, "512rs4"),
+    (4100, 2272, 768, 2, 4, "512rs2"),
+    (8192, 3072, 768, 1, 1, "512rs2"),
+    (8192, 1024, 128, 2, 1, "512rs2"),
 ])
 def test_gemm_packed_matches_split_products(gpu, M, N, K, np_, epi, bn):
     lib = _lib()
@@ -119,6 +127,11 @@ def test_gemm_packed_matches_split_products(gpu, M, N, K, np_, epi, bn):
         lib.ae_launch_gemm_w2.restype = ctypes.c_int
         rc = lib.ae_launch_gemm_w2(_p(dA), _p(dW), _p(db), _p(dR), _p(C), _p(Cp), M, N, K, epi,
                                    np_, 4, st)
+    elif bn.startswith("512rs"):  # role-split persistent kernel: diag 10 (whole chip), 11 (half
+        # the CUs, several tiles per workgroup), 12 (H = 4)
+        diag = {"512rs": 10, "512rs2": 11, "512rs4": 12}[bn]
+        rc = lib.ae_bench_gemm_packed(_p(dA), _p(dW), _p(db), _p(dR), _p(C), _p(Cp), M, N, K, epi,
+                                      np_, 512, diag, st)
     elif bn:  # explicit tile width through the experiment entry point (production kernel, diag 0;
         # "512p": diag 9, the persistent grid)
         rc = lib.ae_bench_gemm_packed(_p(dA), _p(dW), _p(db), _p(dR), _p(C), _p(Cp), M, N, K, epi,
@@ -128,9 +141,9 @@ def test_gemm_packed_matches_split_products(gpu, M, N, K, np_, epi, bn):
                                        epi, np_, st)
     assert rc == 0
     torch.cuda.synchronize()
-    if epi == 1:
+    if epi in (1, 4):
         got = _unpack(Cp.cpu(), np_, N)
-        # the packed planes hold the GELU output to ~2^-17 relative (np 2) / 2^-9 (np 1)
+        # the packed planes hold the GELU / biased output to ~2^-17 relative (np 2) / 2^-9 (np 1)
         rel = 2e-5 if np_ == 2 else 5e-3
         tol = 1e-5 * scale + rel * ref.abs() + 1e-6
     else:
