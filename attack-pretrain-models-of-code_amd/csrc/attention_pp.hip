@@ -58,6 +58,17 @@ __device__ __forceinline__ void dma16s(uint32_t voff, const void* sbase, uint32_
       : "memory", "m0");
 }
 
+// One 4-B-per-lane LDS-DMA (saddr form): lane l's dword lands at lds_base + 4 * l
+__device__ __forceinline__ void dma4s(uint32_t voff, const void* sbase, uint32_t lds_base) {
+  asm volatile(
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dword %0, %1"
+      :
+      : "v"(voff), "s"(sbase), "s"(lds_base)
+      : "memory", "m0");
+}
+
 template <int NP>
 struct PPL {
   static constexpr int RB = 128 * NP;             // bytes of one key's 64 d (NP planes)
@@ -98,7 +109,7 @@ __device__ __forceinline__ int vpos(int r, int x) {
 // upper 16 bits, one shift-or per pair) and lo = bf16(p - hi), exact to 2^-16 of p as the
 // rounded split.
 template <int NP, bool HAS_MASK, bool PLANES, int PIPE>
-__global__ __launch_bounds__(256, (PIPE == 5 || (PIPE >= 60 && PIPE != 64)) ? 3 : 2) void attn_pp_kernel(const unsigned short* __restrict__ qkvp,
+__global__ __launch_bounds__(256, (PIPE == 5 || (PIPE >= 60 && PIPE != 64 && !(HAS_MASK && NP == 2))) ? 3 : 2) void attn_pp_kernel(const unsigned short* __restrict__ qkvp,
                                                          float* __restrict__ out,
                                                          unsigned short* __restrict__ op,
                                                          const int* __restrict__ cu,
@@ -115,11 +126,16 @@ __global__ __launch_bounds__(256, (PIPE == 5 || (PIPE >= 60 && PIPE != 64)) ? 3 
   constexpr int PB = PIPE >= 60 ? 6 : PIPE;
   constexpr int DG = (PIPE >= 61 && PIPE <= 65) ? PIPE - 60 : 0;
   constexpr bool FAST = PIPE >= 60;
-  static_assert(!(HAS_MASK && PB == 6), "PIPE 6 has no mask path (its loop keeps no ordinary "
-                                          "global load, so the mask launches run PIPE 4)");
+  static_assert(!(HAS_MASK && PB == 6 && !FAST),
+                "PIPE 6 has no mask path (its loop keeps no ordinary global load, so its mask "
+                "launches run PIPE 4); PIPE 66 moves the mask words by LDS-DMA");
+  // PIPE 66 with a mask: the tile's mask words (one per query) ride the K / V DMA stream into a
+  // 3-slot LDS ring of 4 waves x 256 B (lanes 32-63 duplicate lanes 0-31), so the loop still has
+  // no compiler-visible global load and every wait stays a counted vmcnt
+  constexpr int MASK_RING = (HAS_MASK && PB == 6) ? 3 * 4 * 256 : 0;
   // PIPE 6: three K and three V slots (the O staging of the epilogue fits inside)
   constexpr int LDS_BYTES =
-      PB == 6 ? (6 * P::TILE > 4 * 32 * 66 * 4 ? 6 * P::TILE : 4 * 32 * 66 * 4) : P::LDS;
+      PB == 6 ? (6 * P::TILE > 4 * 32 * 66 * 4 ? 6 * P::TILE : 4 * 32 * 66 * 4) + MASK_RING : P::LDS;
   __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
   const int seq = blockIdx.z, head = blockIdx.y, qb = blockIdx.x;
   const int start = cu[seq];
@@ -310,10 +326,15 @@ __global__ __launch_bounds__(256, (PIPE == 5 || (PIPE >= 60 && PIPE != 64)) ? 3 
     auto kslot = [&](int j) { return (uint32_t)(j * P::TILE); };        // prologue tiles 0..2
     auto vslot = [&](int j) { return (uint32_t)((3 + j) * P::TILE); };
     auto wait_vm = [](int n) {  // n = DMA instructions allowed to stay outstanding
-      if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      if (n >= 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (HAS_MASK && n == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
       else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if (HAS_MASK && n == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
       else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if (HAS_MASK && n == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
       else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else if (HAS_MASK && n == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     };
     auto barrier = []() {
@@ -356,27 +377,39 @@ __global__ __launch_bounds__(256, (PIPE == 5 || (PIPE >= 60 && PIPE != 64)) ? 3 
         issue1(kt, isv ? 2 * AE_HIDDEN : AE_HIDDEN, dst, isv);
       }
     };
-    // prologue: K0 V0 K1 V1 K2 (as many as exist)
-    int groups = 1;
+    // mask words of tile j: query qr's word j, from the sequence's first mask row (scalar base)
+    constexpr int MW = HAS_MASK ? 1 : 0;  // DMA instructions per tile for the mask
+    constexpr uint32_t MASK_OFF = 6 * P::TILE > 4 * 32 * 66 * 4 ? 6 * P::TILE : 4 * 32 * 66 * 4;
+    const uint32_t* mbase = HAS_MASK ? mask + (size_t)seq * mask_L * (mask_L / 32) : nullptr;
+    const uint32_t moff = HAS_MASK ? (uint32_t)qr * (uint32_t)(mask_L / 32) * 4u : 0u;
+    auto issue_m = [&](int j) {
+      if constexpr (HAS_MASK)
+        dma4s(moff, mbase + j, lds0 + MASK_OFF + (uint32_t)((j % 3) * 1024 + wave * 256));
+    };
+    // prologue: K0 V0 M0 K1 V1 M1 K2 (as many as exist; M = mask words, masked launches only)
     issue(0, false, lds0 + kslot(0));
     issue(0, true, lds0 + vslot(0));
-    ++groups;
+    issue_m(0);
+    int after_k0 = DM + MW, after_k1 = 0;
     if (nkt > 1) {
       issue(1, false, lds0 + kslot(1));
       issue(1, true, lds0 + vslot(1));
-      groups += 2;
+      issue_m(1);
+      after_k0 += 2 * DM + MW;
+      after_k1 = DM + MW;
     }
     if (nkt > 2) {
       issue(2, false, lds0 + kslot(2));
-      ++groups;
+      after_k0 += DM;
+      after_k1 += DM;
     }
-    wait_vm(DM * (groups - 1));  // K0 landed
+    wait_vm(after_k0);  // K0 landed
     barrier();
     floatx16 sA, sB;  // S of the current / next tile, alternating by tile parity
     s_mfma(lds + kslot(0), sA);
     if constexpr (DG == 5) sB = sA;
-    wait_vm(nkt > 1 ? DM * (groups - 3) : 0);  // V0 (and K1) landed
-    barrier();  // every wave has read K0 (its slot takes K3) and sees V0, K1
+    wait_vm(after_k1);  // V0, M0 (and K1) landed
+    barrier();  // every wave has read K0 (its slot takes K3) and sees V0, M0, K1
     // one tile; R = kt % 6 fixes the slots (R % 3) and the S buffers (R % 2) at compile time, so
     // every LDS address of the body is a constant offset from a per-lane base
     auto body = [&](auto rc, int kt, floatx16& s_cur, floatx16& s_next) {
@@ -385,8 +418,9 @@ __global__ __launch_bounds__(256, (PIPE == 5 || (PIPE >= 60 && PIPE != 64)) ? 3 
       constexpr uint32_t VS_ISS = (3 + (R + 2) % 3) * P::TILE, KS_ISS = (R % 3) * P::TILE;
       int n_iss = 0;
       if (kt + 2 < nkt) {
+        issue_m(kt + 2);
         issue(kt + 2, true, lds0 + VS_ISS);
-        n_iss += DM;
+        n_iss += DM + MW;
       }
       if (kt + 3 < nkt) {
         issue(kt + 3, false, lds0 + KS_ISS);
@@ -399,14 +433,20 @@ __global__ __launch_bounds__(256, (PIPE == 5 || (PIPE >= 60 && PIPE != 64)) ? 3 
       bool grow = false;
       if constexpr (DG != 2) {
         float mt = -INFINITY;
-        if ((kt + 1) * KT <= len) {
+        if (!HAS_MASK && (kt + 1) * KT <= len) {
 #pragma unroll
           for (int r = 0; r < 16; r += 2) mt = fmaxf(mt, fmaxf(s_cur[r], s_cur[r + 1]));
         } else {
+          uint32_t mb = 0xffffffffu;
+          if constexpr (HAS_MASK)
+            mb = *reinterpret_cast<const uint32_t*>(lds + MASK_OFF + (R % 3) * 1024 + wave * 256 + 4 * li);
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const bool in = kt * KT + mfma32_row(r, lh) < len;
-            s_cur[r] = in ? s_cur[r] : -INFINITY;
+            const int kk = mfma32_row(r, lh);
+            // absent keys -inf; keys the mask excludes the most negative finite float (HF's
+            // additive finfo.min mask), as tile_max
+            const bool in = kt * KT + kk < len;
+            s_cur[r] = !in ? -INFINITY : (((mb >> kk) & 1u) ? s_cur[r] : -FLT_MAX);
             mt = fmaxf(mt, s_cur[r]);
           }
         }
@@ -1562,7 +1602,7 @@ hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op
   if (np != 1 && np != 2) return hipErrorInvalidValue;
   dim3 grid((max_q + QPB - 1) / QPB, heads, n), block(256);
 #define APP_LAUNCH(N, M, PL)                                                                 \
-  hipLaunchKernelGGL((attn_pp_kernel<N, M, PL, (M && PIPE >= 6) ? 4 : (PIPE >= 60 ? PIPE : PIPE >= 7 ? 6 : PIPE)>), grid, block, 0,      \
+  hipLaunchKernelGGL((attn_pp_kernel<N, M, PL, M ? (PIPE >= 60 ? 66 : PIPE >= 6 ? 4 : PIPE) : (PIPE >= 60 ? PIPE : PIPE >= 7 ? 6 : PIPE)>), grid, block, 0,      \
                      stream, qkvp, out, op, cu,                                                 \
                      q_rows, mask, mask_L)
 #define APP_MP(N)                                                      \

@@ -6,7 +6,10 @@ in one process, and checked against a float64 torch reference of the same attent
 Q·K^T/8 over each sequence's keys, times V).  One JSON line per variant: median / min µs per
 launch, the algorithmic TFLOP/s (4·len²·64 per (sequence, head)) and max |out - ref|.
 
-  python tools/attn_bench.py [--n 64] [--L 512] [--variants 0,1] [--terms 3] [--ragged]
+  python tools/attn_bench.py [--n 64] [--L 512] [--variants 0,1] [--terms 3] [--ragged] [--mask]
+
+--mask adds a random bit-packed key mask (the GraphCodeBERT launch; ~60 % of the keys kept, key 0
+always) to the pp variants and the reference.
 """
 import argparse
 import ctypes
@@ -25,7 +28,7 @@ import _apmc  # noqa: E402,F401
 H, HEADS, D = 768, 12, 64
 
 
-def reference(qkv, cu, n):
+def reference(qkv, cu, n, dense=None):
     outs = []
     for s in range(n):
         a, b = int(cu[s]), int(cu[s + 1])
@@ -33,7 +36,10 @@ def reference(qkv, cu, n):
         q = x[:, :H].view(-1, HEADS, D).transpose(0, 1)
         k = x[:, H:2 * H].view(-1, HEADS, D).transpose(0, 1)
         v = x[:, 2 * H:].view(-1, HEADS, D).transpose(0, 1)
-        p = torch.softmax(q @ k.transpose(1, 2) / 8.0, dim=-1)
+        sc = q @ k.transpose(1, 2) / 8.0
+        if dense is not None:  # HF's additive finfo(f32).min where the mask excludes a key
+            sc = sc + (~dense[s, : b - a, : b - a]).to(sc.device).double() * torch.finfo(torch.float32).min
+        p = torch.softmax(sc, dim=-1)
         outs.append((p @ v).transpose(0, 1).reshape(b - a, H))
     return torch.cat(outs)
 
@@ -45,6 +51,9 @@ def main():
     ap.add_argument("--variants", default="0")
     ap.add_argument("--terms", type=int, default=3)
     ap.add_argument("--ragged", action="store_true")
+    ap.add_argument("--mask", action="store_true")
+    ap.add_argument("--planes", action="store_true",
+                    help="packed-plane context output (the engine's launch) instead of f32")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--check-seqs", type=int, default=8)
@@ -75,7 +84,13 @@ def main():
     cu_d = cu.to(dev)
     flop = float(sum(4.0 * int(x) ** 2 * D * HEADS for x in lens))
     cs = min(args.check_seqs, n)
-    ref = reference(qkv[:int(cu[cs])], cu, cs)
+    dense, dmask = None, None
+    if args.mask:
+        dense = torch.rand(n, L, L, generator=g) < 0.6
+        dense[:, :, 0] = True
+        words = (dense.view(n, L, L // 32, 32).long() << torch.arange(32)).sum(-1)
+        dmask = (words - (words >= 2 ** 31).long() * 2 ** 32).to(torch.int32).to(dev)
+    ref = reference(qkv[:int(cu[cs])], cu, cs, dense)
 
     def p(t):
         return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(None)
@@ -91,10 +106,14 @@ def main():
     for v in args.variants.split(","):
         var = v if v.startswith("pp") else int(v)
         out = torch.zeros((T, H), device=dev)
+        opl = None
         if isinstance(var, str):
             pv = int(var[2:]) if len(var) > 2 else 0
-            call = (lambda out=out, pv=pv: fpp(p(planes), p(out), p(None), p(cu_d), p(None),
-                                               int(lens.max()), n, HEADS, p(None), 0, np_, pv, sp))
+            if args.planes:
+                opl = torch.zeros((T, np_ * H), dtype=torch.int16, device=dev)
+            call = (lambda out=out, pv=pv, opl=opl: fpp(p(planes), p(out), p(opl), p(cu_d), p(None),
+                                                        int(lens.max()), n, HEADS, p(dmask),
+                                                        L if args.mask else 0, np_, pv, sp))
         else:
             call = (lambda out=out, var=var: fn(p(qkv), p(out), p(None), p(cu_d), p(None),
                                                 int(lens.max()), n, HEADS, p(None), 0, args.terms,
@@ -104,6 +123,9 @@ def main():
         if rc != 0:
             print(json.dumps({"variant": var, "error": rc}))
             continue
+        if opl is not None:  # packed planes -> f32: per 32 columns [hi 32 | lo 32] (np 2)
+            pl_ = opl.view(torch.bfloat16).float().view(T, H // 32, np_, 32)
+            out = pl_.sum(2).reshape(T, H)
         err = float((out[:int(cu[cs])].double() - ref).abs().max())
         cases.append(dict(variant=var, call=call, t=[], err=err))
     for _ in range(args.rounds):
@@ -119,7 +141,7 @@ def main():
     for c in cases:
         med, mn = statistics.median(c["t"]), min(c["t"])
         print(json.dumps({"variant": c["variant"], "n": n, "L": L, "ragged": args.ragged,
-                          "terms": args.terms, "us_median": round(med, 2), "us_min": round(mn, 2),
+                          "terms": args.terms, "planes": args.planes, "mask": args.mask, "us_median": round(med, 2), "us_min": round(mn, 2),
                           "tflops_median": round(flop / med / 1e6, 1),
                           "max_abs_err_vs_f64": c["err"]}), flush=True)
 
