@@ -123,9 +123,12 @@ __global__ __launch_bounds__(256, (PIPE == 5 || (PIPE >= 60 && PIPE != 64 && !(H
   // timing diagnostics of 66 (results WRONG; tools/attn_bench.py only): 1 = no exp / P split
   // (P = bf16(S)), 2 = no tile max (fixed reference max 0), 3 = no barriers in the loop, 4 = no
   // PV MFMAs (no V reads), 5 = no S MFMAs after the prologue (no K reads)
+  // PIPE 67: 66 with the tile max as a 3-level tree of v_max3 (depth 3 instead of a chain of 8);
+  // PIPE 68: 67 with the exp / split on packed f32 pairs (experiments)
   constexpr int PB = PIPE >= 60 ? 6 : PIPE;
   constexpr int DG = (PIPE >= 61 && PIPE <= 65) ? PIPE - 60 : 0;
   constexpr bool FAST = PIPE >= 60;
+  constexpr bool TREE = PIPE == 67 || PIPE == 68, PKX = PIPE == 68;
   static_assert(!(HAS_MASK && PB == 6 && !FAST),
                 "PIPE 6 has no mask path (its loop keeps no ordinary global load, so its mask "
                 "launches run PIPE 4); PIPE 66 moves the mask words by LDS-DMA");
@@ -259,6 +262,34 @@ __global__ __launch_bounds__(256, (PIPE == 5 || (PIPE >= 60 && PIPE != 64 && !(H
       const float ly = py - __builtin_bit_cast(float, b1);
       hw[q >> 2][q & 3] = (b0 >> 16) | b1;  // [hi(p.x) | hi(p.y) << 16]
       const bf16x2 l2 = {(__bf16)lx, (__bf16)ly};
+      lw[q >> 2][q & 3] = __builtin_bit_cast(uint32_t, l2);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      ph[t] = __builtin_bit_cast(bf16x8, hw[t]);
+      pl[t] = __builtin_bit_cast(bf16x8, lw[t]);
+    }
+    return acc2.x + acc2.y;
+  };
+  // exp_split on packed f32 pairs with the same rounded hi / lo planes (only the row sum's
+  // association differs: two interleaved partial sums)
+  auto exp_split_pk = [&](floatx16& s, float m_new, bf16x8 (&ph)[2], bf16x8 (&pl)[2]) {
+    floatx2 acc2 = {0.f, 0.f};
+    const floatx2 mm = {m_new, m_new};
+    u32x4 hw[2], lw[2];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const floatx2 d = floatx2{s[2 * q], s[2 * q + 1]} - mm;
+      const float px = __builtin_amdgcn_exp2f(d.x), py = __builtin_amdgcn_exp2f(d.y);
+      const floatx2 pp = {px, py};
+      acc2 += pp;
+      const bf16x2 h2 = {(__bf16)px, (__bf16)py};
+      const uint32_t hb = __builtin_bit_cast(uint32_t, h2);
+      const floatx2 hf = {__builtin_bit_cast(float, hb << 16), __builtin_bit_cast(float, hb & 0xffff0000u)};
+      const floatx2 l = pp - hf;
+      const float lx = l.x, ly = l.y;
+      const bf16x2 l2 = {(__bf16)lx, (__bf16)ly};
+      hw[q >> 2][q & 3] = hb;
       lw[q >> 2][q & 3] = __builtin_bit_cast(uint32_t, l2);
     }
 #pragma unroll
@@ -434,8 +465,16 @@ __global__ __launch_bounds__(256, (PIPE == 5 || (PIPE >= 60 && PIPE != 64 && !(H
       if constexpr (DG != 2) {
         float mt = -INFINITY;
         if (!HAS_MASK && (kt + 1) * KT <= len) {
+          if constexpr (TREE) {
+            float a[6];
 #pragma unroll
-          for (int r = 0; r < 16; r += 2) mt = fmaxf(mt, fmaxf(s_cur[r], s_cur[r + 1]));
+            for (int r = 0; r < 5; ++r) a[r] = fmaxf(s_cur[3 * r], fmaxf(s_cur[3 * r + 1], s_cur[3 * r + 2]));
+            a[5] = s_cur[15];
+            mt = fmaxf(fmaxf(a[0], fmaxf(a[1], a[2])), fmaxf(a[3], fmaxf(a[4], a[5])));
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) mt = fmaxf(mt, fmaxf(s_cur[r], s_cur[r + 1]));
+          }
         } else {
           uint32_t mb = 0xffffffffu;
           if constexpr (HAS_MASK)
@@ -472,7 +511,7 @@ __global__ __launch_bounds__(256, (PIPE == 5 || (PIPE >= 60 && PIPE != 64 && !(H
         pl[1] = ph[1];
         psum = s_cur[0];
       } else {
-        psum = exp_split(s_cur, m_new, ph, pl);
+        psum = PKX ? exp_split_pk(s_cur, m_new, ph, pl) : exp_split(s_cur, m_new, ph, pl);
       }
       if constexpr (DG != 5) s_mfma(lds + KS_NEXT, s_next);
       __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
@@ -1664,8 +1703,12 @@ hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op
 // moves; bit-identical) 190.7 vs 178.3 us, and that on packed pairs 191.6
 // (profiles/r3z_attn_spec_ab.jsonl).  PIPE 61-65 timing diagnostics of 66 (r3y): without the
 // exp / split 160.5 us, without the tile max 161.5, without barriers 176.1, without the next
-// tile's S MFMAs 151.7 of 172.2 — no single stage bounds the loop.
-constexpr int APP_PIPE = 66;
+// tile's S MFMAs 151.7 of 172.2 — no single stage bounds the loop.  PIPE 67 (66 with the tile max
+// as a depth-3 tree of v_max3, bit-identical): 178.0 vs 181.5 us, ragged 121.2 vs 122.8
+// (profiles/r3an_attn_tree_max_ab.jsonl) — production; the masked launches run 66 (their max
+// takes the per-key select path).  PIPE 68 (67 with the exp / split on packed pairs): 193.1 vs
+// 184.5 (profiles/r3am_attn_ab.jsonl), not kept.
+constexpr int APP_PIPE = 67;
 }  // namespace
 
 extern "C" hipError_t ae_launch_attention_pp(const unsigned short* qkvp, float* out,
@@ -1682,7 +1725,7 @@ extern "C" hipError_t ae_launch_attention_pp(const unsigned short* qkvp, float* 
 // interleave hints), 5 = 4 at three workgroups per CU, 6 = the round-3 loop (3-slot rings,
 // deferred rescale), 7 = attn_pp8_kernel (8-wave ping-pong, keys split over two groups), 8 =
 // attn_pw64_kernel, 9 = attn_kt64_kernel, 61-65 = timing diagnostics of 66 (WRONG results), 66 =
-// the production loop.
+// saddr DMA + permlane max, 67 = the production loop (66 + tree max), 68 = 67 on packed pairs.
 // (An XCD-aware workgroup order — the q-blocks of one (sequence, head) on one XCD — measured 2-3 %
 // slower, profiles/r2i_attn_pp_ab.jsonl: the K/V re-reads are Infinity-Cache hits, not the bound.)
 extern "C" hipError_t ae_bench_attention_pp(const unsigned short* qkvp, float* out,
@@ -1696,6 +1739,8 @@ extern "C" hipError_t ae_bench_attention_pp(const unsigned short* qkvp, float* o
     case 64: return app_launch<64>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
     case 65: return app_launch<65>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
     case 66: return app_launch<66>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
+    case 67: return app_launch<67>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
+    case 68: return app_launch<68>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
     default: break;
   }
   if (variant == 9)

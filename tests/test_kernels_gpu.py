@@ -237,7 +237,7 @@ def _qkv_planes(qkv, np_):
     return _pack(hi, lo, np_)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 66])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 66, 67, 68])
 @pytest.mark.parametrize("np_", [2, 1])
 @pytest.mark.parametrize("case", ["ragged", "mask", "cls", "planes", "grow"])
 def test_attention_pp_matches_f64(gpu, np_, case, variant):
@@ -245,7 +245,8 @@ def test_attention_pp_matches_f64(gpu, np_, case, variant):
     reads) against the float64 reference, for both plane counts (np 1 = bf16 mode: stated
     tolerance 2e-2), every loop (1: software-pipelined, 6: 3-slot rings + deferred rescale, 7: the
     8-wave ping-pong kernel with the keys split between its two groups and merged, 8: 4 waves x
-    64 queries, one wave per SIMD, 9: 64-key tiles, 66 (production): 6 with saddr DMA and a permlane row max) and
+    64 queries, one wave per SIMD, 9: 64-key tiles, 66: 6 with saddr DMA and a permlane row max, 67 (production): 66 with a
+    tree row max, 68: 67 with the exp / split on packed pairs) and
     the ragged / mask / CLS-only / packed-output launches.  "grow": spike keys whose scores
     rise along the sequence, so every row max jumps past the deferred-rescale threshold (2^8)
     several times — the rare branch of variant 6."""
@@ -306,9 +307,9 @@ def test_attention_pp_matches_f64(gpu, np_, case, variant):
 
 @pytest.mark.parametrize("case", ["ragged", "grow"])
 def test_attention_pp_restructured_loops_bit_identical(gpu, case):
-    """Variant 66 (production: saddr DMA with clamped offsets in the last tile, permlane row max,
-    three workgroups per CU) restructures PIPE 6 without changing its arithmetic: its packed-plane
-    context must equal PIPE 6's bit for bit."""
+    """Variants 66 (saddr DMA with clamped offsets in the last tile, permlane row max, three
+    workgroups per CU) and 67 (production: 66 with a tree row max) restructure PIPE 6 without
+    changing its arithmetic: their packed-plane context must equal PIPE 6's bit for bit."""
     lib = _lib()
     vp, i32 = ctypes.c_void_p, ctypes.c_int32
     lib.ae_bench_attention_pp.argtypes = [vp] * 5 + [i32] * 3 + [vp, i32, i32, i32, vp]
@@ -332,13 +333,14 @@ def test_attention_pp_restructured_loops_bit_identical(gpu, case):
     dq, dcu = _qkv_planes(qkv, 2).cuda(), cu.cuda()
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     outs = {}
-    for v in (6, 66):
+    for v in (6, 66, 67):
         op = torch.zeros((T, 2 * 768), dtype=torch.int16, device="cuda")
         assert lib.ae_bench_attention_pp(_p(dq), None, _p(op), _p(dcu), None, max(lens), n, 12,
                                          None, 0, 2, v, st) == 0
         outs[v] = op
     torch.cuda.synchronize()
     assert torch.equal(outs[66], outs[6])
+    assert torch.equal(outs[67], outs[6])
 
 
 @pytest.mark.parametrize("M,K,np_", [(300, 768, 2), (512, 3072, 2), (1000, 768, 1), (37, 768, 2),
