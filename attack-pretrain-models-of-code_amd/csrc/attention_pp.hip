@@ -1707,7 +1707,8 @@ hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op
 // as a depth-3 tree of v_max3, bit-identical): 178.0 vs 181.5 us, ragged 121.2 vs 122.8
 // (profiles/r3an_attn_tree_max_ab.jsonl) — production; the masked launches run 66 (their max
 // takes the per-key select path).  PIPE 68 (67 with the exp / split on packed pairs): 193.1 vs
-// 184.5 (profiles/r3am_attn_ab.jsonl), not kept.
+// 184.5 (profiles/r3am_attn_ab.jsonl), and the row sum in two interleaved partial sums (a shorter
+// add chain) 188.5 / 188.2 vs 187.3 / 188.7 (profiles/r3ao_attn_psum2_ab.jsonl): not kept.
 constexpr int APP_PIPE = 67;
 }  // namespace
 
