@@ -157,10 +157,12 @@ def _inflight(max_inflight, n, world):
     """Examples a rank keeps in flight: on one rank all it may; on several, at most half an even
     share of the queue, so the other half is handed out as ranks free up (per-example cost is
     skewed; the ranks fill their first batches at the same instant after the barrier, and an
-    uncapped fill would hand the whole queue out statically)."""
+    uncapped fill would hand the whole queue out statically).  No floor: one GA example or two
+    MHM-NS chains already fill most of a 64-row device batch, while a floor of 8 left ranks idle
+    on short queues (32 MHM-NS examples over 8 ranks went to 4 of them)."""
     if world <= 1:
         return max_inflight
-    return max(1, min(max_inflight, max(8, -(-n // (2 * world)))))
+    return max(1, min(max_inflight, -(-n // (2 * world))))
 
 
 GI_STATS = ["examples", "total_cnt", "success", "queries", "ga_runs", "ga_successes", "wall_s"]

@@ -194,3 +194,16 @@ def test_two_ranks_batched_drivers_match_single_process(tmp_path):
         # (with this instant victim one rank can drain the queue before the other's first pull)
         assert len(tot["per_rank"]) == 2
         assert sum(r["examples"] for r in tot["per_rank"]) == N_EX
+
+
+def test_inflight_cap_spreads_short_queues():
+    """A rank keeps at most half an even share of the queue in flight (no floor), so a short
+    queue reaches every rank: 32 MHM-NS examples over 8 ranks -> 2 in flight each."""
+    sys.path.insert(0, str(ROOT))
+    import _apmc  # noqa: F401
+    from apmc_amd.dist import _inflight
+
+    assert _inflight(64, 32, 8) == 2
+    assert _inflight(64, 400, 8) == 25
+    assert _inflight(64, 400, 1) == 64
+    assert _inflight(64, 3, 8) == 1
