@@ -1708,7 +1708,10 @@ hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op
 // (profiles/r3an_attn_tree_max_ab.jsonl) — production; the masked launches run 66 (their max
 // takes the per-key select path).  PIPE 68 (67 with the exp / split on packed pairs): 193.1 vs
 // 184.5 (profiles/r3am_attn_ab.jsonl), and the row sum in two interleaved partial sums (a shorter
-// add chain) 188.5 / 188.2 vs 187.3 / 188.7 (profiles/r3ao_attn_psum2_ab.jsonl): not kept.
+// add chain) 188.5 / 188.2 vs 187.3 / 188.7 (profiles/r3ao_attn_psum2_ab.jsonl), and other
+// interleaves of the next S MFMAs with the exp / split (8 or 3 vector instructions per MFMA, or
+// the compiler's own order: 181.2 / 181.6 / 183.7 vs 179.8 / 179.5 us,
+// profiles/r3as_attn_interleave_ab.jsonl): not kept.
 constexpr int APP_PIPE = 67;
 }  // namespace
 
