@@ -1639,7 +1639,8 @@ hipError_t pp_dispatch(const unsigned short* A, const unsigned short* W, const f
 }  // namespace
 
 namespace {
-constexpr int PK_GROUP_M = 4;  // grouped tile order: 4 > 8 > 16 > 32 M-tiles by A/B (round 1)
+constexpr int PK_GROUP_M = 4;  // grouped tile order: 4 > 8 > 16 > 32 M-tiles by A/B (round 1);
+                               // re-swept on the ping-pong kernel (profiles/r3at_gemm_group_m_ab.jsonl)
 
 template <int BN, int NP, int EPI, int DIAG>
 hipError_t pk_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R, float* C,
@@ -1816,6 +1817,8 @@ extern "C" hipError_t ae_bench_gemm_packed(const unsigned short* A, const unsign
     PPRS(1, PK_EPI_BIAS_PACKED);
 #undef PPRS
   }
+  if (bn == 512 && diag >= 21 && diag <= 52)  // production kernel, grouped order of diag - 20 M-tiles
+    return pp_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, diag - 20, st);
   if (bn == 512) {  // the ping-pong 256 x 256 kernel
     switch (diag) {
       case 0: return pp_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
