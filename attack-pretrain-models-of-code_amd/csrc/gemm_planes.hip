@@ -1799,7 +1799,9 @@ extern "C" hipError_t ae_bench_gemm_packed(const unsigned short* A, const unsign
   if (!pk_shape_ok(M, N, K, np) ||
       (bn != 0 && bn != 128 && bn != 192 && bn != 256 && bn != 512))
     return hipErrorInvalidValue;
-  if (bn == 192) return pp192_dispatch(A, W, bias, R, C, M, N, K, epi, np, PK_GROUP_M, st, diag == 8);
+  if (bn == 192)  // diag 8: non-temporal stores; 21-52: grouped order of diag - 20 M-tiles
+    return pp192_dispatch(A, W, bias, R, C, M, N, K, epi, np,
+                          diag >= 21 && diag <= 52 ? diag - 20 : PK_GROUP_M, st, diag == 8);
   if (bn == 512 && diag >= 10 && diag <= 14) {  // role-split persistent kernel (experiment)
     // 10: whole chip, H = 8; 11: half the CUs (one of two streams), H = 8; 12 / 13: H = 4 / 12;
     // 14: no hand-over (every wave stores its own blocks: the kernel's base cost)
