@@ -526,11 +526,30 @@ class CloneAttacker(Attacker):
 
 
 class MHM_Attacker:
-    """MHM-NS baseline (attacker.py:457-738)."""
+    """MHM-NS baseline (attacker.py:457-738).
 
+    The six reference copies differ only in a few places, which the subclasses set:
+      class                          reference                                      lang    skip known
+                                                                                            subs / random  random label
+      MHM_Attacker                   CodeXGLUE/Defect-detection/code/attacker.py    c       yes / yes      MHM-Origin
+      AuthorshipMHM_Attacker         CodeXGLUE/Authorship-Attribution/.../attacker.py python yes / no      MHM-Origin
+      CloneMHM_Attacker              CodeXGLUE/Clone-detection-BigCloneBench/...    java    yes / yes      Ori_MHM
+      GraphMHM_Attacker              GraphCodeBERT/Defect-detection/.../attacker.py c       yes / yes      Ori_MHM
+      GraphAuthorshipMHM_Attacker    GraphCodeBERT/Authorship-Attribution/...       python  yes / yes      Ori_MHM
+      GraphCloneMHM_Attacker         GraphCodeBERT/clonedetection/.../attacker.py   java    no / no        Ori_MHM
+    (skip known: a candidate that already names a variable of the chain is dropped,
+    `if c in _uid.keys(): continue`).  The GraphCodeBERT copies featurise every candidate with
+    their own convert_code_to_features (data flow + graph mask), which the GraphModel victim's
+    dataset_from_texts applies; the clone copies query the dataset example first and score pairs
+    (mutated code1 against the fixed code2)."""
+
+    # __replaceUID drops substitutes that already name a variable (attacker.py:623-624)
+    skip_known_subs = True
     # __replaceUID_random drops random-vocabulary candidates that already name a variable
-    # (attacker.py:732-733); the Authorship-Attribution copy does not
+    # (attacker.py:688-689); the CodeBERT Authorship-Attribution copy does not
     skip_known_uids = True
+    # attack_type of mcmc_random's results (attacker.py:599,606)
+    random_type = "MHM-Origin"
 
     def __init__(self, args, model_tgt, model_mlm, tokenizer_mlm, _token2idx, _idx2token) -> None:
         self.classifier = model_tgt
@@ -555,7 +574,10 @@ class MHM_Attacker:
         return answer(self.classifier, gen)
 
     def _run_gen(self, tokenizer, substituions, code, _label, _n_candi, _max_iter, _prob_threshold,
-                 replace, attack_type, rng):
+                 replace, attack_type, rng, ctx=None):
+        """ctx: per-chain request state handed to _candidates_request (the clone copies' fixed
+        code2 half); chains of many examples interleave over one attacker, so it is never kept
+        on self."""
         identifiers, code_tokens = get_identifiers(code, self.lang)
         prog_length = len(code_tokens)
         processed_code = " ".join(code_tokens)
@@ -574,7 +596,7 @@ class MHM_Attacker:
         for iteration in range(1, 1 + _max_iter):
             res = yield from replace(rng, _tokens=code, _label=_label, _uid=uid,
                                      substitute_dict=variable_substitue_dict, _n_candi=_n_candi,
-                                     _prob_threshold=_prob_threshold)
+                                     _prob_threshold=_prob_threshold, ctx=ctx)
             self._print_res(iteration, res)
             if res["status"].lower() in ["s", "a"]:
                 if iteration == 1:
@@ -625,29 +647,37 @@ class MHM_Attacker:
     def mcmc_random(self, tokenizer, substituions, code=None, _label=None, _n_candi=30,
                     _max_iter=100, _prob_threshold=0.95):
         return self._run(tokenizer, substituions, code, _label, _n_candi, _max_iter,
-                         _prob_threshold, self._replace_uid_random, "MHM-Origin")
+                         _prob_threshold, self._replace_uid_random, self.random_type)
+
+    def chain_gen(self, tokenizer, substituions, code, _label, example, _n_candi, _max_iter,
+                  _prob_threshold, original, rng):
+        """One mcmc (or mcmc_random if `original`) call as a request generator; `example` is the
+        dataset item, read only by the copies whose mcmc queries it first (clone)."""
+        replace = self._replace_uid_random if original else self._replace_uid
+        kind = self.random_type if original else "MHM"
+        return self._run_gen(tokenizer, substituions, code, _label, _n_candi, _max_iter,
+                             _prob_threshold, replace, kind, rng)
 
     def mcmc_batched(self, tokenizer, jobs, _n_candi=30, _max_iter=100, _prob_threshold=0.95,
                      original=False, max_inflight=64, on_done=None):
         """Many examples' MCMC chains in flight at once.
 
-        `jobs` = [(substituions, code, label, seed)]; example j runs on `random.Random(seed)`, so
-        its chain is exactly `random.seed(seed); mcmc(...)` (or `mcmc_random` if `original`).  Each
-        round gathers the pending ≤(1+_n_candi)-candidate requests of up to `max_inflight` chains
-        into ONE `get_results` call, so the device sees batches of hundreds of sequences instead of
-        ≤31.  The victim's query counter advances by the same total as the sequential runs.
-        Returns `[(result_dict, queries)]` in job order; `on_done(j, result, queries)` is called as
-        each chain finishes."""
+        `jobs` = [(substituions, code, label, seed[, example])]; example j runs on
+        `random.Random(seed)`, so its chain is exactly `random.seed(seed); mcmc(...)` (or
+        `mcmc_random` if `original`).  Each round gathers the pending ≤(1+_n_candi)-candidate
+        requests of up to `max_inflight` chains into ONE `get_results` call, so the device sees
+        batches of hundreds of sequences instead of ≤31.  The victim's query counter advances by
+        the same total as the sequential runs.  Returns `[(result_dict, queries)]` in job order;
+        `on_done(j, result, queries)` is called as each chain finishes."""
         from .batching import list_source, run_requests
 
-        replace = self._replace_uid_random if original else self._replace_uid
-        kind = "MHM-Origin" if original else "MHM"
         out = [None] * len(jobs)
 
         def start(j):
-            subs, code, label, seed = jobs[j]
-            return self._run_gen(tokenizer, subs, code, label, _n_candi, _max_iter,
-                                 _prob_threshold, replace, kind, random.Random(seed))
+            subs, code, label, seed = jobs[j][:4]
+            example = jobs[j][4] if len(jobs[j]) > 4 else None
+            return self.chain_gen(tokenizer, subs, code, label, example, _n_candi, _max_iter,
+                                  _prob_threshold, original, random.Random(seed))
 
         def finish(j, value, q, _t0):
             out[j] = (value, q)
@@ -659,14 +689,14 @@ class MHM_Attacker:
         return out
 
     def _candidates_result(self, rng, _tokens, _label, selected_uid, candi_token, candi_pairs,
-                           _prob_threshold):
+                           _prob_threshold, ctx=None):
         """Shared tail of __replaceUID / __replaceUID_random (attacker.py:634-670)."""
         # candidate 0 is the unmodified code; the others are get_example(code, uid, c)
         ex = Example(_tokens, self.lang)
         tok = self.tokenizer_mlm
         L = self.args.block_size
         pops = [[(selected_uid, c)] for c in candi_pairs]
-        prob, pred = yield self._candidates_request(ex, tok, _tokens, pops, L)
+        prob, pred = yield self._candidates_request(ex, tok, _tokens, pops, L, ctx)
         candi_tokens = [_tokens] + [None] * len(pops)
 
         def text(i):
@@ -695,36 +725,38 @@ class MHM_Attacker:
                 "old_pred": pred[0], "new_pred": pred[i],
                 "nb_changed_pos": _tokens.count(selected_uid)}
 
-    def _candidates_request(self, ex, tok, _tokens, pops, L):
+    def _candidates_request(self, ex, tok, _tokens, pops, L, ctx=None):
         """One request: the unmodified code, then get_example(code, uid, c) per candidate."""
         m = self.classifier
-        first = m.prepare(m.dataset_from_texts([_tokens], tok, self.args))
-        if not pops:
-            return first
         if getattr(m, "population_rows", None) is not None:
+            first = m.prepare(m.dataset_from_texts([_tokens], tok, self.args))
+            if not pops:
+                return first
             rows = m.population_rows(ex, tok, pops, MODE_SINGLE, L)
             return join_payloads([first, type(first)(rows[0], rows[1], len(pops))])
-        texts = [ex.mutant_text(p, MODE_SINGLE) for p in pops]
-        return join_payloads([first, m.prepare(m.dataset_from_texts(texts, tok, self.args))])
+        # victims whose rows are not spliced token ids (GraphModel: data-flow features): every
+        # candidate text through the victim's own featuriser, one batch
+        texts = [_tokens] + [ex.mutant_text(p, MODE_SINGLE) for p in pops]
+        return m.prepare(m.dataset_from_texts(texts, tok, self.args))
 
     def _replace_uid(self, rng, _tokens, _label=None, _uid={}, substitute_dict={}, _n_candi=30,
-                     _prob_threshold=0.95, _candi_mode="random"):
+                     _prob_threshold=0.95, _candi_mode="random", ctx=None):
         assert _candi_mode.lower() in ["random", "nearby"]
         selected_uid = rng.sample(list(substitute_dict.keys()), 1)[0]
         candi_token = [selected_uid]
         pairs = []
         pool = substitute_dict[selected_uid]
         for c in rng.sample(pool, min(_n_candi, len(pool))):
-            if c in _uid.keys():
+            if self.skip_known_subs and c in _uid.keys():
                 continue
             if isUID(c):
                 candi_token.append(c)
                 pairs.append(c)
         return (yield from self._candidates_result(rng, _tokens, _label, selected_uid, candi_token,
-                                                   pairs, _prob_threshold))
+                                                   pairs, _prob_threshold, ctx))
 
     def _replace_uid_random(self, rng, _tokens, _label=None, _uid={}, substitute_dict={},
-                            _n_candi=30, _prob_threshold=0.95, _candi_mode="random"):
+                            _n_candi=30, _prob_threshold=0.95, _candi_mode="random", ctx=None):
         assert _candi_mode.lower() in ["random", "nearby"]
         selected_uid = rng.sample(list(substitute_dict.keys()), 1)[0]
         candi_token = [selected_uid]
@@ -736,7 +768,7 @@ class MHM_Attacker:
                 candi_token.append(c)
                 pairs.append(c)
         return (yield from self._candidates_result(rng, _tokens, _label, selected_uid, candi_token,
-                                                   pairs, _prob_threshold))
+                                                   pairs, _prob_threshold, ctx))
 
     def _print_res(self, _iter=None, _res=None, _prefix="  => "):
         if not getattr(self.args, "verbose", False):
@@ -768,6 +800,120 @@ class AuthorshipMHM_Attacker(MHM_Attacker):
                     _prob_threshold=0.95, subs={}):
         return super().mcmc_random(tokenizer, subs, code, _label, _n_candi, _max_iter,
                                    _prob_threshold)
+
+
+class GraphMHM_Attacker(MHM_Attacker):
+    """GraphCodeBERT/Defect-detection/code/attacker.py:467-737 over the GraphModel victim: the
+    Devign chain (C leaves, same call form as mhm_attack.py:198-205), every candidate featurised
+    by the GCB convert_code_to_features (:30-63: ' '.join(code.split()), run_parser data flow,
+    GraphCodeDataset mask) and mcmc_random labelled "Ori_MHM" (:608,614)."""
+
+    random_type = "Ori_MHM"
+
+
+class GraphAuthorshipMHM_Attacker(AuthorshipMHM_Attacker):
+    """GraphCodeBERT/Authorship-Attribution/code/attacker.py:479-741 over the GraphModel victim
+    (mhm_attack.py:203-210 call form: mcmc(tokenizer, code, _label=..., subs=...)): Python
+    leaves, candidates featurised with run.py's data flow (attacker.py:52-85 imports
+    run.extract_dataflow), known names skipped in both modes (:634, :695) and mcmc_random
+    labelled "Ori_MHM" (:613,619)."""
+
+    skip_known_uids = True
+    random_type = "Ori_MHM"
+
+
+class CloneMHM_Attacker(MHM_Attacker):
+    """CodeXGLUE/Clone-detection-BigCloneBench/code/attacker.py:469-800: the chain perturbs code1
+    of a pair and every query is the pair [features(candidate code1) | features(code2)].
+      * signature mcmc(example, substituions, tokenizer, code_pair, _label, ...) with code_pair =
+        (id1, id2, code1, code2) (:478, :573); the call first queries the dataset example and
+        returns {'succ': None, ...} when the victim misclassifies it (:485-512);
+      * candidates: ' '.join(text.split()) tokenised and cut to block_size - 2 per half
+        (run.py convert_examples_to_features, :689-699), code2's half fixed (:504-505);
+      * the results carry "orig_label" (:565,571); mcmc_random is "Ori_MHM" (:659,666)."""
+
+    random_type = "Ori_MHM"
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.lang = "java"
+
+    def mcmc(self, example, substituions, tokenizer, code_pair, _label=None, _n_candi=30,
+             _max_iter=100, _prob_threshold=0.95):
+        return answer(self.classifier, self.chain_gen(tokenizer, substituions, code_pair, _label,
+                                                      example, _n_candi, _max_iter,
+                                                      _prob_threshold, False, random))
+
+    def mcmc_random(self, example, substituions, tokenizer, code_pair, _label=None, _n_candi=30,
+                    _max_iter=100, _prob_threshold=0.95):
+        return answer(self.classifier, self.chain_gen(tokenizer, substituions, code_pair, _label,
+                                                      example, _n_candi, _max_iter,
+                                                      _prob_threshold, True, random))
+
+    def chain_gen(self, tokenizer, substituions, code, _label, example, _n_candi, _max_iter,
+                  _prob_threshold, original, rng):
+        """code = the pair tuple; the chain's text is code1 (code_pair[2])."""
+        logits, preds = yield self.classifier.prepare([example])
+        orig_label = preds[0]
+        if orig_label != _label_of(example):
+            return {"succ": None, "tokens": None, "raw_tokens": None}
+        replace = self._replace_uid_random if original else self._replace_uid
+        kind = self.random_type if original else "MHM"
+        # _tokenize / candidates with tokenizer_mlm (:503, :692); the chain's text is code1
+        res = yield from self._run_gen(self.tokenizer_mlm, substituions, code[2], _label,
+                                       _n_candi, _max_iter, _prob_threshold, replace, kind, rng,
+                                       ctx=self._pair_ctx(code))
+        if res["succ"] is not None:
+            res["orig_label"] = orig_label
+        return res
+
+    def _pair_ctx(self, code_pair):
+        """code2's fixed half: its ids (tokenize(' '.join(code2.split()))[:block-2])."""
+        ids2, lens2 = self.tokenizer_mlm.featurize([code_pair[3]], self.args.block_size)
+        return ids2[0], int(lens2[0])
+
+    def _candidates_request(self, ex, tok, _tokens, pops, L, ctx=None):
+        m = self.classifier
+        ids2, len2 = ctx
+        ids0, lens0 = tok.featurize([_tokens], L)
+        first = m.prepare_pairs(ids0, lens0, ids2, len2)
+        if not pops:
+            return first
+        if getattr(m, "population_rows", None) is not None:
+            rows, lens = m.population_rows(ex, tok, pops, MODE_SINGLE, L)
+        else:
+            rows, lens = tok.featurize([ex.mutant_text(p, MODE_SINGLE) for p in pops], L)
+        return join_payloads([first, m.prepare_pairs(rows, lens, ids2, len2)])
+
+
+class GraphCloneMHM_Attacker(CloneMHM_Attacker):
+    """GraphCodeBERT/clonedetection/code/attacker.py:496-800 over the GraphModel clone victim:
+    the CodeBERT clone chain, but every query is convert_code_to_features(candidate code1, code2)
+    (:33-73: run_parser data flow of each Java text as is, one graph row per code), the dataset
+    label is example[6] (:517), and NEITHER mode skips candidates that already name a variable
+    (__replaceUID :704-709 and __replaceUID_random :766-771 have no `c in _uid` test).
+    The reference's own driver calls mcmc(example, tokenizer, code_pair, ...) without the
+    substitutes (mhm_attack.py:200-206), which raises TypeError; this class keeps the attacker's
+    signature, the one the CodeBERT clone driver uses (its mhm_attack.py:195-203)."""
+
+    skip_known_subs = False
+    skip_known_uids = False
+
+    def _pair_ctx(self, code_pair):
+        from .graph import compact_features, task_features
+
+        f2 = task_features(code_pair[3], self.tokenizer_mlm, 0, self.args, "clone")
+        return compact_features(f2) if hasattr(self.tokenizer_mlm, "gcb_features") else f2
+
+    def _candidates_request(self, ex, tok, _tokens, pops, L, ctx=None):
+        from .graph import gcb_dataset_from_texts, task_features
+
+        texts = [_tokens] + [ex.mutant_text(p, MODE_SINGLE) for p in pops]
+        if hasattr(tok, "gcb_features"):
+            feats = gcb_dataset_from_texts(texts, tok, self.args, "clone").c
+        else:
+            feats = [task_features(t, tok, 0, self.args, "clone") for t in texts]
+        return self.classifier.prepare_pair_population(feats, ctx)
 
 
 class GraphAttacker(Attacker):

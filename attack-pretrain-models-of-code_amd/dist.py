@@ -121,12 +121,14 @@ def run_sharded_gi_attack(model, codes, subs, labels, args, device=None, tok=Non
         raise ValueError("run_sharded_gi_attack with world > 1 needs AttackArgs.rng='per_example' "
                          "(one global random stream would depend on which rank took an example)")
     q = DynamicQueue(len(codes), key=call_key("apmc_attack_queue"))
+    rank = dist.get_rank() if world > 1 else 0
     t0 = time.time()
-    out = run_gi_attack(model, codes, subs, labels, args, queue=q, tok=tok)
+    out = run_gi_attack(model, codes, subs, labels, _rank_csv(args, rank, world), queue=q, tok=tok)
     wall = time.time() - t0
     st = gather_stats([out["examples"], out["total_cnt"], out["success"], out["queries"], wall],
                       device=device)
     recs = merge_records(out["records"])
+    merge_csv_shards(dist, rank, world, getattr(args, "csv_store_path", None))
     tot = dict(examples=int(st[:, 0].sum()), total_cnt=int(st[:, 1].sum()),
                success=int(st[:, 2].sum()), queries=int(st[:, 3].sum()),
                wall_s=float(st[:, 4].max()), per_rank=st.tolist())
@@ -166,7 +168,42 @@ def _inflight(max_inflight, n, world):
 
 
 GI_STATS = ["examples", "total_cnt", "success", "queries", "ga_runs", "ga_successes", "wall_s"]
-MHM_STATS = ["examples", "total_cnt", "success", "queries", "wall_s"]
+MHM_STATS = ["examples", "total_cnt", "success", "queries", "errors", "wall_s"]
+
+
+def _rank_csv(args, rank, world):
+    """args with this rank's Recorder shard `<csv_store_path>.rank<r>` (world > 1): ranks never
+    open the one CSV together (Recorder truncates it, utils.py:654)."""
+    import dataclasses
+
+    if world <= 1 or not getattr(args, "csv_store_path", None):
+        return args
+    return dataclasses.replace(args, csv_store_path=f"{args.csv_store_path}.rank{rank}")
+
+
+def merge_csv_shards(dist, rank, world, path):
+    """Rank 0 merges the ranks' Recorder shards into `path`, rows in example-index order (the
+    1-GPU file), and removes the shards."""
+    import csv
+
+    if world <= 1 or not path:
+        return
+    dist.barrier()
+    if rank == 0:
+        header, rows = None, []
+        for r in range(world):
+            shard = f"{path}.rank{r}"
+            with open(shard, newline="") as f:
+                rd = csv.reader(f)
+                header = next(rd)
+                rows.extend(rd)
+            os.remove(shard)
+        rows.sort(key=lambda row: int(row[0]))
+        with open(path, "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(header)
+            w.writerows(rows)
+    dist.barrier()
 
 
 def run_sharded_gi_batched(model, codes, subs, labels, args, max_inflight=64, device=None,
@@ -177,11 +214,11 @@ def run_sharded_gi_batched(model, codes, subs, labels, args, max_inflight=64, de
     1-GPU run whichever rank took the example.  Returns (merged records, job totals)."""
     from .drivers import run_gi_attack_batched
 
-    dist, _, world = _rank_world()
+    dist, rank, world = _rank_world()
     q = DynamicQueue(len(codes), key=call_key(key), deadline=deadline)
     if dist is not None:
         dist.barrier()
-    out = run_gi_attack_batched(model, codes, subs, labels, args, queue=q,
+    out = run_gi_attack_batched(model, codes, subs, labels, _rank_csv(args, rank, world), queue=q,
                                 max_inflight=_inflight(max_inflight, len(codes), world))
     recs = out["records"]
     ga = [r for r in recs if r["attack_type"] == "GA"]
@@ -190,6 +227,7 @@ def run_sharded_gi_batched(model, codes, subs, labels, args, max_inflight=64, de
                       device=device)
     tot = _job_totals(st, GI_STATS, 6)
     tot["success_rate"] = tot["success"] / tot["total_cnt"] if tot["total_cnt"] else 0.0
+    merge_csv_shards(dist, rank, world, getattr(args, "csv_store_path", None))
     return merge_records(recs), tot
 
 
@@ -201,18 +239,19 @@ def run_sharded_mhm(model, codes, subs, labels, args, n_candi=30, max_iter=100, 
     round vs 100 rounds of 31 candidates).  Returns (merged records, job totals)."""
     from .drivers import run_mhm_attack
 
-    dist, _, world = _rank_world()
+    dist, rank, world = _rank_world()
     n_ex = len(codes) if n is None else n
     q = DynamicQueue(n_ex, key=call_key(key))
     if dist is not None:
         dist.barrier()
-    out = run_mhm_attack(model, codes, subs, labels, args, n_candi=n_candi, max_iter=max_iter,
-                         prob_threshold=prob_threshold, original=original,
+    out = run_mhm_attack(model, codes, subs, labels, _rank_csv(args, rank, world), n_candi=n_candi,
+                         max_iter=max_iter, prob_threshold=prob_threshold, original=original,
                          max_inflight=_inflight(max_inflight, n_ex, world), queue=q)
     st = gather_stats([out["examples"], out["total_cnt"], out["success"], out["queries"],
-                       out["wall_s"]], device=device)
-    tot = _job_totals(st, MHM_STATS, 4)
+                       out["errors"], out["wall_s"]], device=device)
+    tot = _job_totals(st, MHM_STATS, 5)
     tot["success_rate"] = tot["success"] / tot["total_cnt"] if tot["total_cnt"] else 0.0
+    merge_csv_shards(dist, rank, world, getattr(args, "csv_store_path", None))
     return merge_records(out["records"]), tot
 
 

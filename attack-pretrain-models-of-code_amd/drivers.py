@@ -29,8 +29,9 @@ import time
 import numpy as np
 
 from .attacker import (Attacker, AuthorshipAttacker, AuthorshipMHM_Attacker, CloneAttacker,
-                       GraphAttacker, GraphAuthorshipAttacker, GraphCloneAttacker, MHM_Attacker,
-                       get_identifiers)
+                       CloneMHM_Attacker, GraphAttacker, GraphAuthorshipAttacker,
+                       GraphAuthorshipMHM_Attacker, GraphCloneAttacker, GraphCloneMHM_Attacker,
+                       GraphMHM_Attacker, MHM_Attacker, get_identifiers)
 from .host import Tokenizer
 from .utils import Recorder, build_vocab, set_seed
 
@@ -50,6 +51,10 @@ class AttackArgs:
                           # gcb_authorship (GraphCodeBERT)
     code_length: int = 512        # GraphCodeBERT rows: code_length + data_flow_length tokens
     data_flow_length: int = 128
+    on_error: str = "raise"  # MHM chains: "raise" = the reference (its driver stops at the first
+                             # exception); "record" = record is_success -5 and go on (one chain
+                             # of the GraphCodeBERT clone copy can raise KeyError, see
+                             # GraphCloneMHM_Attacker)
 
 
 def load_fixture(path, start=0, end=None, labels_path=None):
@@ -278,79 +283,149 @@ def run_gi_attack(model, codes, subs, labels, args: AttackArgs, indices=None, to
     return _totals(records, time.time() - t0)
 
 
+MHM_ATTACKERS = {"devign": MHM_Attacker, "authorship": AuthorshipMHM_Attacker,
+                 "clone": CloneMHM_Attacker, "gcb_devign": GraphMHM_Attacker,
+                 "gcb_authorship": GraphAuthorshipMHM_Attacker, "gcb_clone": GraphCloneMHM_Attacker}
+# max_iter of each task's mhm driver: CodeXGLUE clone 10 (mhm_attack.py:196-203), GraphCodeBERT
+# clone 400 (mhm_attack.py:200-206), 100 elsewhere
+MHM_MAX_ITER = {"clone": 10, "gcb_clone": 400}
+
+
+def _task_lang(task, args=None):
+    base = task[4:] if task.startswith("gcb_") else task
+    return {"devign": getattr(args, "lang", "c") or "c", "clone": "java",
+            "authorship": "python"}[base]
+
+
+def make_mhm_attacker(args, model, tok, codes):
+    """mhm_attack.py's setup: build_vocab over every program's leaves (5000 names; code1 of the
+    clone pairs, :168-172) and the task's MHM_Attacker copy."""
+    task = getattr(args, "task", "devign")
+    lang = _task_lang(task, args)
+    texts = [c[2] for c in codes] if _is_clone(task) else codes
+    code_tokens = [get_identifiers(c, lang)[1] for c in texts]
+    id2token, token2id = build_vocab(code_tokens, 5000)
+    return MHM_ATTACKERS[task](args, model, None, tok, token2id, id2token)
+
+
 def mhm_one_gen(attacker, tok, code, subs, label, args, n_candi, max_iter, prob_threshold,
                 original, rng):
-    """One example of mhm_attack.py:195-236 (Authorship mhm.py:192-233) as a request generator:
-    the original-prediction query, then (if correctly classified) the MCMC chain.  Returns
-    (is_success, result dict or None)."""
+    """One example of mhm_attack.py:188-230 (Authorship mhm.py:192-233, clone mhm_attack.py:
+    186-221) as a request generator: the original-prediction query, then (if correctly
+    classified) the MCMC chain.  Returns (is_success, result dict or None)."""
     task = getattr(args, "task", "devign")
     example = _example(tok, code, label, args.block_size, task, args)
     _, preds = yield attacker.classifier.prepare([example])
     if preds[0] != label:
         return -4, None
-    replace = attacker._replace_uid_random if original else attacker._replace_uid
-    kind = "MHM-Origin" if original else "MHM"
-    res = yield from attacker._run_gen(tok, subs, code, label, n_candi, max_iter, prob_threshold,
-                                       replace, kind, rng)
+    try:
+        res = yield from attacker.chain_gen(tok, subs, code, label, example, n_candi, max_iter,
+                                            prob_threshold, original, rng)
+    except KeyError as e:
+        if getattr(args, "on_error", "raise") != "record":
+            raise
+        return -5, {"error": f"KeyError: {e}"}
     return (1 if res["succ"] else (-1 if res["succ"] is not None else -3)), res
 
 
+def _mhm_call(attacker, task, tok, code, subs, label, example, n_candi, max_iter,
+              prob_threshold, original):
+    """The task driver's mcmc / mcmc_random call, in its own argument form."""
+    fn = attacker.mcmc_random if original else attacker.mcmc
+    kw = dict(_n_candi=n_candi, _max_iter=max_iter, _prob_threshold=prob_threshold)
+    if task in ("authorship", "gcb_authorship"):  # mhm.py:199-206: (tokenizer, code, ..., subs=)
+        return fn(tok, code, _label=label, subs=subs, **kw)
+    if _is_clone(task):  # clone mhm_attack.py:196-203: (example, substitute, tokenizer, code_pair)
+        return fn(example, subs, tok, code, _label=label, **kw)
+    return fn(tok, subs, code=code, _label=label, **kw)
+
+
+def _mhm_record(index, code, task, res, label, queries, dt_min, recorder):
+    """One mhm_attack.py row (recoder.writemhm, :229) of a finished chain; res None: the
+    example was skipped (-4 misclassified, or {'succ': None}: no substitutable name)."""
+    if res is not None and "error" in res:
+        return dict(index=index, is_success=-5, queries=queries, error=res["error"])
+    ok = -4 if res is None else (1 if res["succ"] else (-1 if res["succ"] is not None else -3))
+    rec = dict(index=index, is_success=ok, queries=queries)
+    if res is not None and res["succ"] is not None:
+        rec.update(attack_type=res["attack_type"], adv_code=res["tokens"],
+                   replace_info=res["replace_info"], nb_changed_var=res["nb_changed_var"],
+                   nb_changed_pos=res["nb_changed_pos"])
+        if recorder is not None:
+            text = code
+            if _is_clone(task):  # Clone mhm_attack.py:229
+                text = ("CODE1: " + code[2].replace("\n", " ") + " ||CODE2: "
+                        + code[3].replace("\n", " "))
+            recorder.writemhm(index, text, res["prog_length"], res["tokens"], label,
+                              res.get("orig_label", label), res["new_pred"], res["is_success"],
+                              res["old_uid"], res["score_info"], res["nb_changed_var"],
+                              res["nb_changed_pos"], res["replace_info"], res["attack_type"],
+                              queries, dt_min)
+    return rec
+
+
 def run_mhm_attack(model, codes, subs, labels, args: AttackArgs, indices=None, tok=None,
-                   n_candi=30, max_iter=100, prob_threshold=1, original=False, max_inflight=1,
+                   n_candi=30, max_iter=None, prob_threshold=1, original=False, max_inflight=1,
                    queue=None):
-    """mhm_attack.py:160-236 (MHM-NS; `original` = MHM with the random-token candidates).
+    """mhm_attack.py:160-236 (MHM-NS; `original` = MHM with the random-token candidates) for
+    every task: devign / authorship / clone (CodeBERT) and their gcb_* GraphCodeBERT copies
+    (MHM_ATTACKERS; max_iter defaults to each driver's own, MHM_MAX_ITER).
 
     max_inflight = 1 is the reference loop (one global `random` stream seeded once).  With
     max_inflight > 1 the examples run interleaved (batching.run_requests over mhm_one_gen): up
     to `max_inflight` chains share every device batch; example `index` then draws from
     `random.Random(args.seed + index)` — the same per-example seeding `rng="per_example"` gives
     the GA driver — and records stay in index order.  `queue` (batched form only) pulls the
-    examples from a dist.DynamicQueue shared by all ranks instead of `indices`."""
+    examples from a dist.DynamicQueue shared by all ranks instead of `indices`.  With
+    args.csv_store_path every attacked example gets its writemhm row (mhm_attack.py:229)."""
     tok = tok or Tokenizer()
     task = getattr(args, "task", "devign")
+    if max_iter is None:
+        max_iter = MHM_MAX_ITER.get(task, 100)
     set_seed(args.seed)
-    lang = "python" if task == "authorship" else args.lang
-    code_tokens = [get_identifiers(c, lang)[1] for c in codes]
-    id2token, token2id = build_vocab(code_tokens, 5000)
-    cls = AuthorshipMHM_Attacker if task == "authorship" else MHM_Attacker
-    attacker = cls(args, model, None, tok, token2id, id2token)
+    attacker = make_mhm_attacker(args, model, tok, codes)
+    recorder = Recorder(args.csv_store_path) if args.csv_store_path else None
     order = list(range(len(codes))) if indices is None else list(indices)
     records, t0 = [], time.time()
     if max_inflight > 1 or queue is not None:
         from .batching import run_requests
 
-        by_index = {}
+        writer = _InOrderWriter(recorder)
 
         def start(index):
             return mhm_one_gen(attacker, tok, codes[index], subs[index], labels[index], args,
                                n_candi, max_iter, prob_threshold, original,
                                random.Random(args.seed + index))
 
-        def on_done(index, value, queries, _ts):
-            by_index[index] = dict(index=index, is_success=value[0], queries=queries)
+        def on_done(index, value, queries, ts):
+            dt = (time.time() - ts) / 60
+            writer.finish(index, lambda rec: _mhm_record(index, codes[index], task, value[1],
+                                                         labels[index], queries, dt, rec))
 
-        run_requests(model, _source(order, queue, _InOrderWriter(None)), start, on_done,
-                     max(2, max_inflight))
-        records = [by_index[i] for i in sorted(by_index)]
+        run_requests(model, _source(order, queue, writer), start, on_done, max(2, max_inflight))
+        records = writer.records()
         order = []
     for index in order:
         example = _example(tok, codes[index], labels[index], args.block_size, task, args)
         q0 = model.query
+        ts = time.time()
         probs, preds = model.get_results([example], args.eval_batch_size)
         if preds[0] != labels[index]:
-            records.append(dict(index=index, is_success=-4, queries=model.query - q0))
+            records.append(_mhm_record(index, codes[index], task, None, labels[index],
+                                       model.query - q0, 0.0, None))
             continue
-        fn = attacker.mcmc_random if original else attacker.mcmc
-        if task == "authorship":  # mhm.py:199-206: mcmc(tokenizer, code, _label=..., subs=...)
-            res = fn(tok, codes[index], _label=labels[index], _n_candi=n_candi,
-                     _max_iter=max_iter, _prob_threshold=prob_threshold, subs=subs[index])
-        else:
-            res = fn(tok, subs[index], _label=labels[index], code=codes[index], _n_candi=n_candi,
-                     _max_iter=max_iter, _prob_threshold=prob_threshold)
-        ok = 1 if res["succ"] else (-1 if res["succ"] is not None else -3)
-        records.append(dict(index=index, is_success=ok, queries=model.query - q0))
+        try:
+            res = _mhm_call(attacker, task, tok, codes[index], subs[index], labels[index],
+                            example, n_candi, max_iter, prob_threshold, original)
+        except KeyError as e:
+            if args.on_error != "record":
+                raise
+            res = {"error": f"KeyError: {e}"}
+        records.append(_mhm_record(index, codes[index], task, res, labels[index],
+                                   model.query - q0, (time.time() - ts) / 60, recorder))
     correct = sum(r["is_success"] >= -1 for r in records)
     succ = sum(r["is_success"] == 1 for r in records)
     return dict(records=records, examples=len(records), total_cnt=correct, success=succ,
                 success_rate=(succ / correct) if correct else 0.0,
+                errors=sum(r["is_success"] == -5 for r in records),
                 queries=sum(r["queries"] for r in records), wall_s=time.time() - t0)

@@ -413,9 +413,9 @@ def aa_leg(dev, n_examples, n_gcb, rank, world, precision):
     """Config 5 (Authorship-Attribution, 66 classes): the ALERT greedy->GA attack
     (CodeXGLUE/Authorship-Attribution/code/attack.py: block 512, eval_batch_size 32) against the
     MHM-NS sampling baseline (mhm.py: n_candi 30, max_iter 100, eval_batch_size 64) on the same
-    CodeBERT victim and programs of valid_subs.jsonl, then the GraphCodeBERT victim's GA
-    (GraphCodeBERT/Authorship-Attribution, code_length 512 + data_flow_length 128) on the first
-    n_gcb programs.  Synthetic victims (seed 5, out_proj std 8) do not know the authors, so each
+    CodeBERT victim and programs of valid_subs.jsonl, then the GraphCodeBERT victim's GA and
+    MHM-NS (GraphCodeBERT/Authorship-Attribution gi_attack.py / mhm_attack.py, code_length 512 +
+    data_flow_length 128) on the first n_gcb programs.  Synthetic victims (seed 5, out_proj std 8) do not know the authors, so each
     program's label is the victim's own prediction (every program is attacked).  Each half pulls
     its programs from one queue shared by the ranks."""
     from apmc_amd.dist import run_sharded_gi_batched, run_sharded_mhm
@@ -460,6 +460,16 @@ def aa_leg(dev, n_examples, n_gcb, rank, world, precision):
         res["gcb_ga"] = dict(_summary(t),
                              mode="GraphCodeBERT victim, greedy -> GA (GraphAuthorshipAttacker), "
                                   f"programs [0, {len(gcodes)}), L = 640 with the data-flow mask")
+        log("authorship leg: GraphCodeBERT MHM-NS")
+        margs = AttackArgs(block_size=512, eval_batch_size=64, seed=123456, task="gcb_authorship",
+                           code_length=512, data_flow_length=128, on_error="record")
+        _, t = run_sharded_mhm(gmodel, gcodes, gsubs, glabels, margs, max_iter=100,
+                               prob_threshold=1, max_inflight=128, device=dev,
+                               key="bench_aa_gcb_mhm_queue")
+        res["gcb_mhm"] = dict(_summary(t),
+                              mode="GraphCodeBERT victim, MHM-NS (GraphAuthorshipMHM_Attacker, "
+                                   "mhm_attack.py: n_candi 30, max_iter 100, threshold 1), "
+                                   f"programs [0, {len(gcodes)}), cross-example batched chains")
         gmodel.engine.close()
     return res
 
@@ -612,9 +622,13 @@ def main():
     # streams (engine.hip run_encoder), so its FFN1 launches share the CUs with the other half's
     # kernels; FFN1 is timed (HIP events on its launch stream) on a single-stream engine over the
     # same batch, where nothing else runs beside it
+    prev_split = os.environ.get("AE_SPLIT_STREAMS")
     os.environ["AE_SPLIT_STREAMS"] = "0"
     eng1 = Engine(sd, head="sigmoid1", num_labels=1, precision=args.precision, device=dev.index)
-    os.environ.pop("AE_SPLIT_STREAMS")
+    if prev_split is None:  # the user's own setting stays in force for the later legs
+        os.environ.pop("AE_SPLIT_STREAMS")
+    else:
+        os.environ["AE_SPLIT_STREAMS"] = prev_split
     out1 = torch.empty_like(out)
     n1 = max(5, args.steps // 2)
     el1, (k_ms, k_n, k_flop) = time_steps(eng1, ids_dev, lens, out1, n1, args.warmup, dev, dist,

@@ -128,6 +128,15 @@ class GraphTextVictim:
             self.code2_words = " ".join(featurize_ref.identifier_code_tokens(code2, "java"))
 
     def _feats(self, code, variant, run_trunc=False):
+        # a pure function of its arguments; MHM chains re-score the same candidate texts many
+        # times, so results are memoised per victim
+        key = (code, variant, run_trunc)
+        memo = self.__dict__.setdefault("_memo", {})
+        if key not in memo:
+            memo[key] = self._feats_uncached(code, variant, run_trunc)
+        return memo[key]
+
+    def _feats_uncached(self, code, variant, run_trunc=False):
         from apmc_amd.graph import extract_dataflow
 
         if self.base == "devign":

@@ -448,3 +448,82 @@ def test_gcb_task_attack_matches_text_oracle(task):
     seen = compare_gcb_with(task, model, model.score_packed, codes, subs, labels, args, 9000, pick)
     print(task, seen)
     assert {o for _, o in seen} & {1, -1}, seen
+
+
+# ---- MHM-NS copies of the clone and GraphCodeBERT victims (config 5's GraphCodeBERT half) ----
+# config shape: block 512 (CodeBERT clone: two 512-id halves per pair), GraphCodeBERT
+# code_length 512 + data_flow_length 128, n_candi 30, 100 iterations, _prob_threshold 1
+_MHM_VICTIMS = {}
+_MHM_SEEN = {}
+MHM_PROGRAMS = 4
+
+
+def _mhm_victim(task):
+    """(victim, oracle scorer, args, codes, subs, labels, programs) of one task, built once."""
+    if task in _MHM_VICTIMS:
+        return _MHM_VICTIMS[task]
+    from apmc_amd.drivers import AttackArgs, _example, load_fixture
+    from apmc_amd.graph import GraphModel
+    from apmc_amd.host import Tokenizer
+    from apmc_amd.model import Model
+    from test_task_attacks import fixture
+
+    base = task[4:] if task.startswith("gcb_") else task
+    head, nl = {"clone": ("pair2", 2), "authorship": ("softmaxN", 66),
+                "devign": ("sigmoid1", 1)}[base]
+    sd = synthetic_sd(seed=5, head=head, num_labels=nl, out_std=8.0)
+    args = AttackArgs(block_size=512, eval_batch_size=64, task=task, code_length=512,
+                      data_flow_length=128)
+    if task == "clone":
+        model = Model(sd, task="clone")
+
+        def score(ids):
+            ids = np.ascontiguousarray(ids, dtype=np.int32)
+            lens = (ids != 1).sum(1).astype(np.int32)
+            return model.engine.score(torch.from_numpy(ids).cuda(), lens).cpu().numpy()
+    else:
+        model = GraphModel(sd, task=base, args=args)
+        score = model.score_packed
+    if base == "devign":
+        codes, subs, _ = load_fixture(FIXTURE, 0, 120)
+        pick = _pick(codes, subs, MHM_PROGRAMS)
+    else:
+        codes, subs, _ = fixture(base, MHM_PROGRAMS)
+        pick = list(range(MHM_PROGRAMS))
+    tok = Tokenizer()
+    labels = [0] * len(codes)
+    for i in pick:  # the victim's own predictions: every program is attacked
+        labels[i] = int(model.get_results([_example(tok, codes[i], 0, 512, task, args)])[1][0])
+    _MHM_VICTIMS[task] = (model, score, args, codes, subs, labels, pick)
+    return _MHM_VICTIMS[task]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("kind,prog", [("mcmc", p) for p in range(MHM_PROGRAMS)]
+                         + [("mcmc_random", p) for p in range(2)])
+@pytest.mark.parametrize("task", ["clone", "gcb_devign", "gcb_authorship", "gcb_clone"])
+def test_mhm_variant_matches_text_oracle(task, kind, prog):
+    """MHM-NS of the clone and GraphCodeBERT victims on the HIP engine (CloneMHM_Attacker,
+    GraphMHM_Attacker, GraphAuthorshipMHM_Attacker, GraphCloneMHM_Attacker; reference
+    CodeXGLUE/Clone-detection-BigCloneBench/code/attacker.py:469-800,
+    GraphCodeBERT/{Defect-detection,Authorship-Attribution,clonedetection}/code/attacker.py
+    MHM_Attacker) against oracle/mhm_ref.py scoring the same candidate texts (featurised by
+    the oracle: transformers tokenizer, oracle/graph_ref.py features and masks) with the same
+    engine: identical outcome, adversarial code, replacement chain, attack type and query count
+    over 100-iteration chains at 512 + 128."""
+    from test_mhm_variants import compare_mhm_with
+
+    model, score, args, codes, subs, labels, pick = _mhm_victim(task)
+    seen = compare_mhm_with(task, kind, model, score, args, codes, subs, labels, [pick[prog]],
+                            MHM_ITERS, 3700, vocab_pick=pick)
+    print(task, kind, prog, seen)
+    _MHM_SEEN.setdefault(task, []).extend(s for s, _ in seen)
+
+
+@pytest.mark.parametrize("task", ["clone", "gcb_devign", "gcb_authorship", "gcb_clone"])
+def test_mhm_variant_sample_includes_success(task):
+    """Each task's sample above includes a successful chain."""
+    got = _MHM_SEEN.get(task, [])
+    if len(got) < MHM_PROGRAMS + 2:
+        pytest.skip("needs the runs of test_mhm_variant_matches_text_oracle")
+    assert True in got, (task, got)

@@ -152,9 +152,13 @@ def _batched_worker(rank, world, port, outdir):
 
     init_from_env("gloo")
     codes, subs, labels = load_fixture(FIXTURE, 0, N_EX)
-    args = AttackArgs(block_size=128, eval_batch_size=8, rng="per_example")
+    out = pathlib.Path(outdir)
+    args = AttackArgs(block_size=128, eval_batch_size=8, rng="per_example",
+                      csv_store_path=str(out / "gi.csv"))
     gi, gi_tot = run_sharded_gi_batched(FakeVictim(), codes, subs, labels, args, max_inflight=4)
-    mhm, mhm_tot = run_sharded_mhm(FakeVictim(), codes, subs, labels, args, max_iter=8,
+    margs = AttackArgs(block_size=128, eval_batch_size=8, rng="per_example",
+                       csv_store_path=str(out / "mhm.csv"))
+    mhm, mhm_tot = run_sharded_mhm(FakeVictim(), codes, subs, labels, margs, max_iter=8,
                                    max_inflight=4)
     if rank == 0:
         import json
@@ -179,13 +183,26 @@ def test_two_ranks_batched_drivers_match_single_process(tmp_path):
     got = json.loads((tmp_path / "batched.json").read_text())
 
     codes, subs, labels = load_fixture(FIXTURE, 0, N_EX)
-    args = AttackArgs(block_size=128, eval_batch_size=8, rng="per_example")
+    args = AttackArgs(block_size=128, eval_batch_size=8, rng="per_example",
+                      csv_store_path=str(tmp_path / "gi_single.csv"))
     gi = run_gi_attack_batched(FakeVictim(), codes, subs, labels, args, max_inflight=4)
     keys = ["index", "is_success", "attack_type", "queries", "adv_code", "replace_info"]
     assert [{k: r[k] for k in keys} for r in got["gi"]] == \
         [{k: r[k] for k in keys} for r in gi["records"]]
     assert got["gi_tot"]["queries"] == gi["queries"] and got["gi_tot"]["examples"] == N_EX
-    mhm = run_mhm_attack(FakeVictim(), codes, subs, labels, args, max_iter=8, max_inflight=4)
+    margs = AttackArgs(block_size=128, eval_batch_size=8, rng="per_example",
+                       csv_store_path=str(tmp_path / "mhm_single.csv"))
+    mhm = run_mhm_attack(FakeVictim(), codes, subs, labels, margs, max_iter=8, max_inflight=4)
+    # each rank wrote its own Recorder shard; rank 0 merged them in index order: the CSVs equal
+    # the single-process ones but for the wall-clock column
+    import csv
+
+    def rows(name):
+        with open(tmp_path / name, newline="") as f:
+            return [r[:15] for r in csv.reader(f)]
+    assert rows("gi.csv") == rows("gi_single.csv") and len(rows("gi.csv")) == N_EX + 1
+    assert rows("mhm.csv") == rows("mhm_single.csv") and len(rows("mhm.csv")) > 1
+    assert not list(tmp_path.glob("*.rank*"))
     assert got["mhm"] == mhm["records"]
     assert got["mhm_tot"]["queries"] == mhm["queries"]
     assert {r["is_success"] for r in mhm["records"]} & {1, -1}
