@@ -5,7 +5,7 @@ PKG := attack-pretrain-models-of-code_amd
 CSRC := $(PKG)/csrc
 OBJDIR := $(PKG)/build
 LIB := $(PKG)/lib/libalert_engine.so
-SRCS := $(CSRC)/engine.hip $(CSRC)/gemm_f32.hip $(CSRC)/gemm_x3.hip $(CSRC)/gemm_planes.hip $(CSRC)/gemm_w2.hip $(CSRC)/attention_f32.hip $(CSRC)/attention_x3.hip $(CSRC)/attention_pp.hip $(CSRC)/rowops.hip $(CSRC)/splice_topk.hip
+SRCS := $(CSRC)/engine.hip $(CSRC)/gemm_f32.hip $(CSRC)/gemm_x3.hip $(CSRC)/gemm_planes.hip $(CSRC)/attention_f32.hip $(CSRC)/attention_x3.hip $(CSRC)/attention_pp.hip $(CSRC)/rowops.hip $(CSRC)/splice_topk.hip $(CSRC)/cls_attention.hip
 OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS))
 HDRS := $(CSRC)/common.h include/alert_engine.h
 HIPFLAGS := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -Wall -Wno-unused-result

@@ -1,0 +1,289 @@
+// cls_attention.hip — the last encoder layer's attention for the one row the task heads read.
+//
+// The heads read features[:, 0, :] only (RobertaClassificationHead via
+// CodeXGLUE/Defect-detection/code/model.py:25; the clone / authorship heads likewise), so the last
+// layer needs the attention output of ONE query per sequence, the CLS row.  Per head h with
+// q = W_q x_0 + b_q (the CLS query) and keys / values k_j = W_k x_j + b_k, v_j = W_v x_j + b_v:
+//   s_j  = q·k_j / 8 = x_j · (W_k^T q) / 8 + q·b_k / 8        (the last term is the same for every
+//                                                           j, so softmax drops it)
+//   ctx  = Σ_j p_j v_j = W_v (Σ_j p_j x_j) + b_v              (Σ_j p_j = 1)
+// so W_k is absorbed into the query (u_h = W_k,h^T q_h: 768 values per head) and W_v is applied
+// once to the p-weighted row sum.  The layer's K / V projections over all T rows (the QKV GEMM,
+// 116 GFLOP at B=64 x L=512) are never computed: the attention reads the layer-input rows x_j
+// (f32, 3 KB each) once, which makes it HBM-bound at ~T·3 KB.
+//
+// Kernels (all f32 arithmetic, exact-f32 MFMA products; per-sequence work only, with key chunks
+// fixed at 64 keys, so a sequence's result does not depend on the batch it is in):
+//   cls_u_kernel       u[s][h][:] = Σ_d q[s][64h+d] W_k[64h+d][:]          (VALU, tiny)
+//   cls_attn_kernel    one workgroup per (sequence, 64-key chunk): scores of 16-key tiles by
+//                      v_mfma_f32_16x16x4_f32 (16 keys x 16 head slots x 768), online softmax in
+//                      the exp2 domain, y_h += Σ p x_j by the same MFMA (16 head slots x 768) ->
+//                      per-chunk (max, sum, y[12][768])
+//   cls_combine_kernel the chunks of a sequence merged in chunk order -> ybar[s][h][:]
+//   cls_vproj_kernel   ctx[s][64h+d] = b_v[64h+d] + Σ_c W_v[64h+d][c] ybar[s][h][c]
+// Masked (GraphCodeBERT) launches read row 0 of the sequence's bit-packed mask; the CLS row always
+// attends itself (special tokens see [:max_length], utils.py:555-557), so a fully masked CLS row
+// cannot occur — if it does the device error flag poisons the scores (alert_engine.h ae_score).
+#include "common.h"
+
+namespace {
+
+constexpr int H = AE_HIDDEN;        // 768
+constexpr int NH = 12;              // heads
+constexpr int DH = AE_HEAD_DIM;     // 64
+constexpr int KC = 64;              // keys per workgroup chunk
+constexpr int KT = 16;              // keys per MFMA tile
+constexpr int XS = H + 4;           // LDS row stride (floats) of the x / u tiles
+constexpr int REC = 32 + NH * H;    // floats per chunk record: m[16], l[16], y[12][768]
+
+__global__ __launch_bounds__(256) void cls_u_kernel(const float* __restrict__ q,
+                                                    const float* __restrict__ wk, int n,
+                                                    float* __restrict__ u) {
+  __shared__ float qs[16][DH];
+  const int h = blockIdx.y, s0 = blockIdx.x * 16, col = blockIdx.z * 256 + threadIdx.x;
+  for (int i = threadIdx.x; i < 16 * DH; i += 256) {
+    const int r = i / DH, d = i % DH;
+    qs[r][d] = s0 + r < n ? q[(size_t)(s0 + r) * H + h * DH + d] : 0.f;
+  }
+  __syncthreads();
+  float acc[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const float* w = wk + (size_t)h * DH * H + col;
+  for (int d = 0; d < DH; ++d) {
+    const float wv = w[(size_t)d * H];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = fmaf(qs[r][d], wv, acc[r]);
+  }
+  for (int r = 0; r < 16 && s0 + r < n; ++r) u[((size_t)(s0 + r) * NH + h) * H + col] = acc[r];
+}
+
+// one workgroup (8 waves) per (chunk c, sequence s); LDS: u [12][XS], x tile [16][XS], partial
+// score tiles [8][256], p [16][16], alpha / running max / running sum [16] each
+__global__ __launch_bounds__(512) void cls_attn_kernel(
+    const float* __restrict__ x, const float* __restrict__ u, const int* __restrict__ cu,
+    const uint32_t* __restrict__ mask, int mask_L, float scale, float* __restrict__ part) {
+  extern __shared__ float lds[];
+  float* us = lds;                  // [12][XS]
+  float* xs = us + NH * XS;         // [16][XS]
+  float* sred = xs + KT * XS;       // [8][256]
+  float* pt = sred + 8 * 256;       // [16 keys][16 heads]
+  float* alpha = pt + 256;          // [16]
+  float* mrun = alpha + 16;         // [16]
+  float* lrun = mrun + 16;          // [16]
+  const int c = blockIdx.x, s = blockIdx.y;
+  const int beg = cu[s], len = cu[s + 1] - beg, k0 = c * KC;
+  if (k0 >= len) return;
+  const int nk = min(KC, len - k0);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l15 = lane & 15, l4 = lane >> 4;
+  const uint32_t* mrow = mask ? mask + (size_t)s * mask_L * (mask_L / 32) : nullptr;
+
+  // u of this sequence -> LDS (12 x 192 float4)
+  const float4* u4 = reinterpret_cast<const float4*>(u + (size_t)s * NH * H);
+  for (int i = tid; i < NH * (H / 4); i += 512) {
+    const int r = i / (H / 4), c4 = i % (H / 4);
+    *reinterpret_cast<float4*>(us + r * XS + 4 * c4) = u4[i];
+  }
+  if (tid < 16) {
+    mrun[tid] = -INFINITY;
+    lrun[tid] = 0.f;
+  }
+  floatx4 acc[6];
+#pragma unroll
+  for (int t = 0; t < 6; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int ntile = (nk + KT - 1) / KT;
+  float4 pre[6];  // the next x tile, 16 rows x 192 float4 over 512 threads
+  auto load_tile = [&](int t) {
+    const int r0 = k0 + t * KT;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int f = tid + 512 * j, r = f / (H / 4), c4 = f % (H / 4);
+      pre[j] = r0 + r < len ? reinterpret_cast<const float4*>(x + (size_t)(beg + r0 + r) * H)[c4]
+                            : float4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  load_tile(0);
+  for (int t = 0; t < ntile; ++t) {
+    __syncthreads();  // the previous tile's readers are done with xs
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int f = tid + 512 * j, r = f / (H / 4), c4 = f % (H / 4);
+      *reinterpret_cast<float4*>(xs + r * XS + 4 * c4) = pre[j];
+    }
+    __syncthreads();
+    if (t + 1 < ntile) load_tile(t + 1);  // in flight under this tile's MFMAs
+    // scores: wave w contracts dims [96w, 96w + 96) -> D[key = 4*l4 + i][head slot = l15]
+    floatx4 d = floatx4{0.f, 0.f, 0.f, 0.f};
+    const float* xa = xs + l15 * XS + 96 * w + l4;
+    const float* ub = us + (l15 < NH ? l15 : 0) * XS + 96 * w + l4;
+#pragma unroll
+    for (int kk = 0; kk < 24; ++kk) {
+      const float b = l15 < NH ? ub[4 * kk] : 0.f;
+      d = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[4 * kk], b, d, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sred[w * 256 + (4 * l4 + i) * 16 + l15] = d[i];
+    __syncthreads();
+    if (tid < 256) {  // key = tid >> 4, head slot = tid & 15
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v += sred[q * 256 + tid];
+      const int key = k0 + t * KT + (tid >> 4);
+      bool ok = key < len;
+      if (ok && mrow) ok = (mrow[key >> 5] >> (key & 31)) & 1u;
+      pt[tid] = ok ? v * scale : -INFINITY;
+    }
+    __syncthreads();
+    if (tid < 16) {  // online softmax of head slot tid over the tile's 16 keys
+      const float mo = mrun[tid];
+      float mx = mo;
+#pragma unroll
+      for (int j = 0; j < KT; ++j) mx = fmaxf(mx, pt[j * 16 + tid]);
+      float a = 1.f, sum = 0.f;
+      if (mx != -INFINITY) {
+        a = __builtin_amdgcn_exp2f(mo - mx);
+#pragma unroll
+        for (int j = 0; j < KT; ++j) {
+          const float p = __builtin_amdgcn_exp2f(pt[j * 16 + tid] - mx);
+          pt[j * 16 + tid] = p;
+          sum += p;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < KT; ++j) pt[j * 16 + tid] = 0.f;
+      }
+      alpha[tid] = a;
+      mrun[tid] = mx;
+      lrun[tid] = fmaf(lrun[tid], a, sum);
+    }
+    __syncthreads();
+    // y[head slot][col] = alpha * y + Σ_key p[key][slot] x[key][col]; wave w owns cols [96w, +96)
+    float al[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) al[i] = alpha[4 * l4 + i];
+    float pa[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pa[q] = pt[(4 * q + l4) * 16 + l15];
+#pragma unroll
+    for (int ct = 0; ct < 6; ++ct) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[ct][i] *= al[i];
+      const float* xb = xs + l4 * XS + 96 * w + 16 * ct + l15;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[q], xb[4 * q * XS], acc[ct], 0, 0, 0);
+    }
+  }
+  float* rec = part + ((size_t)(beg >> 6) + s + c) * REC;
+  __syncthreads();
+  if (tid < 16) {
+    rec[tid] = mrun[tid];
+    rec[16 + tid] = lrun[tid];
+  }
+#pragma unroll
+  for (int ct = 0; ct < 6; ++ct)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int hs = 4 * l4 + i;
+      if (hs < NH) rec[32 + hs * H + 96 * w + 16 * ct + l15] = acc[ct][i];
+    }
+}
+
+// the chunks of sequence s merged in chunk order: ybar[s][h][:] = Σ_c 2^(m_c - M) y_c / L
+__global__ __launch_bounds__(256) void cls_combine_kernel(const float* __restrict__ part,
+                                                          const int* __restrict__ cu,
+                                                          float* __restrict__ ybar,
+                                                          int* __restrict__ err) {
+  const int s = blockIdx.x, h = blockIdx.y;
+  const int beg = cu[s], len = cu[s + 1] - beg, nc = (len + KC - 1) / KC;
+  const float* rec0 = part + ((size_t)(beg >> 6) + s) * REC;
+  float M = -INFINITY;
+  for (int c = 0; c < nc; ++c) M = fmaxf(M, rec0[(size_t)c * REC + h]);
+  float L = 0.f;
+  for (int c = 0; c < nc; ++c) {
+    const float m = rec0[(size_t)c * REC + h];
+    if (m != -INFINITY) L = fmaf(rec0[(size_t)c * REC + 16 + h], __builtin_amdgcn_exp2f(m - M), L);
+  }
+  if (!(L > 0.f)) {  // no key attended: cannot happen for a CLS row; poison the call
+    if (threadIdx.x == 0) atomicOr(err, 2);
+  }
+  const float inv = 1.f / L;
+  for (int col = threadIdx.x; col < H; col += 256) {
+    float y = 0.f;
+    for (int c = 0; c < nc; ++c) {
+      const float m = rec0[(size_t)c * REC + h];
+      if (m != -INFINITY)
+        y = fmaf(rec0[(size_t)c * REC + 32 + h * H + col], __builtin_amdgcn_exp2f(m - M), y);
+    }
+    ybar[((size_t)s * NH + h) * H + col] = y * inv;
+  }
+}
+
+// ctx[s][64h + d] = b_v[64h + d] + Σ_c W_v[64h + d][c] ybar[s][h][c]; 16 sequences x 64 d per block
+__global__ __launch_bounds__(256) void cls_vproj_kernel(const float* __restrict__ ybar,
+                                                        const float* __restrict__ wv,
+                                                        const float* __restrict__ bv, int n,
+                                                        float* __restrict__ ctx) {
+  __shared__ float ys[16][65];
+  __shared__ float ws[64][65];
+  const int h = blockIdx.y, s0 = blockIdx.x * 16, tid = threadIdx.x;
+  const int d = tid & 63, sg = tid >> 6;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < H; c0 += 64) {
+    for (int i = tid; i < 16 * 64; i += 256) {
+      const int r = i >> 6, cc = i & 63;
+      ys[r][cc] = s0 + r < n ? ybar[((size_t)(s0 + r) * NH + h) * H + c0 + cc] : 0.f;
+    }
+    for (int i = tid; i < 64 * 64; i += 256) {
+      const int r = i >> 6, cc = i & 63;
+      ws[r][cc] = wv[(size_t)(h * DH + r) * H + c0 + cc];
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int cc = 0; cc < 64; ++cc) {
+      const float wvv = ws[d][cc];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] = fmaf(ys[4 * sg + r][cc], wvv, acc[r]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int sidx = s0 + 4 * sg + r;
+    if (sidx < n) ctx[(size_t)sidx * H + h * DH + d] = acc[r] + bv[h * DH + d];
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// floats of the per-chunk partial records for sequences whose token rows total T (any lens)
+long ae_cls_attention_part_floats(long T, int n) { return ((T >> 6) + n + 2) * (long)REC; }
+
+// q: [n][768] CLS queries (the split modes' W_q carries log2(e)/8, so scale = 1; the exact mode's
+// does not, scale = log2(e)/8); wk, wv: [768][768] row-major K / V projection weights; bv: [768];
+// x: [T][768] layer-input rows (compacted, cu offsets); u_ws, ybar_ws: [n][12][768];
+// part_ws: ae_cls_attention_part_floats(T, n) floats; ctx: [n][768] out.
+hipError_t ae_launch_cls_attention(const float* x, const float* q, const float* wk,
+                                   const float* wv, const float* bv, const int* cu, int n,
+                                   int max_len, const uint32_t* mask, int mask_L, float scale,
+                                   float* u_ws, float* part_ws, float* ybar_ws, float* ctx,
+                                   int* err, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(cls_u_kernel, dim3((n + 15) / 16, NH, H / 256), dim3(256), 0, st, q, wk, n,
+                     u_ws);
+  const size_t lds = (size_t)(NH * XS + KT * XS + 8 * 256 + 256 + 48) * sizeof(float);
+  hipError_t e = ensure_dynamic_lds((const void*)cls_attn_kernel, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(cls_attn_kernel, dim3((max_len + KC - 1) / KC, n), dim3(512), lds, st, x,
+                     u_ws, cu, mask, mask_L, scale, part_ws);
+  hipLaunchKernelGGL(cls_combine_kernel, dim3(n, NH), dim3(256), 0, st, part_ws, cu, ybar_ws, err);
+  hipLaunchKernelGGL(cls_vproj_kernel, dim3((n + 15) / 16, NH), dim3(256), 0, st, ybar_ws, wv, bv,
+                     n, ctx);
+  return hipGetLastError();
+}
+
+}  // extern "C"

@@ -62,6 +62,10 @@ hipError_t ae_launch_scatter_rows(const float*, const int*, const int*, int, int
 hipError_t ae_launch_nll_rows(const float*, const int*, int, int, float*, hipStream_t);
 hipError_t ae_launch_graph_mask(const int*, const int*, const int*, const int*, int, int, int,
                                 uint32_t*, hipStream_t);
+long ae_cls_attention_part_floats(long, int);
+hipError_t ae_launch_cls_attention(const float*, const float*, const float*, const float*,
+                                   const float*, const int*, int, int, const uint32_t*, int, float,
+                                   float*, float*, float*, float*, int*, hipStream_t);
 }
 
 namespace {
@@ -117,6 +121,12 @@ struct ae_engine {
   int* lnctr = nullptr;
   bool planes = false;
   int np = 1;
+  // last-layer CLS attention with W_k absorbed into the query (cls_attention.hip): per-sequence
+  // u = W_k^T q and p-weighted row sums [n][12][768], per-64-key-chunk partial records
+  // (AE_CLS_ABSORB=0 at engine creation: the full-T QKV GEMM + one-query attention instead)
+  bool cls_absorb = true;
+  float *cls_u = nullptr, *cls_y = nullptr, *cls_part = nullptr;
+  size_t cap_cls_part = 0;
   int *tok_ids = nullptr, *tok_pos = nullptr, *src_col = nullptr, *cu = nullptr, *one = nullptr;
   int* err = nullptr;  // device flag: some row's lens disagreed with its ids (compact_kernel)
   float* logits = nullptr;
@@ -269,9 +279,12 @@ int ensure_workspace(ae_engine* e, size_t T, size_t n) {
   if (n + 1 > e->cap_n) {
     size_t nn = n + n / 4 + 64;
     HIPC(hipDeviceSynchronize());
-    for (void* p : {(void*)e->xc, (void*)e->cc, (void*)e->tc, (void*)e->hc, (void*)e->cu})
+    for (void* p : {(void*)e->xc, (void*)e->cc, (void*)e->tc, (void*)e->hc, (void*)e->cu,
+                    (void*)e->cls_u, (void*)e->cls_y})
       dev_free(e, p);
     int rc = 0;
+    if ((rc = dev_alloc(e, (void**)&e->cls_u, nn * 12 * H * 4))) return rc;
+    if ((rc = dev_alloc(e, (void**)&e->cls_y, nn * 12 * H * 4))) return rc;
     if ((rc = dev_alloc(e, (void**)&e->xc, nn * H * 4))) return rc;
     if ((rc = dev_alloc(e, (void**)&e->cc, nn * H * 4))) return rc;
     if ((rc = dev_alloc(e, (void**)&e->tc, nn * H * 4))) return rc;
@@ -282,6 +295,20 @@ int ensure_workspace(ae_engine* e, size_t T, size_t n) {
     HIPC(hipHostMalloc((void**)&e->pinned_cu, (nn + 1) * 4, hipHostMallocDefault));
     e->cap_pinned = nn + 1;
   }
+  return AE_OK;
+}
+
+// Partial records of the last layer's CLS attention for T rows of n sequences.
+int ensure_cls_part(ae_engine* e, int64_t T, int n) {
+  const size_t need = (size_t)ae_cls_attention_part_floats((long)T, n);
+  if (need <= e->cap_cls_part) return AE_OK;
+  HIPC(hipDeviceSynchronize());
+  dev_free(e, e->cls_part);
+  e->cls_part = nullptr;
+  const size_t cap = need + need / 4;
+  int rc = dev_alloc(e, (void**)&e->cls_part, cap * 4);
+  if (rc) return rc;
+  e->cap_cls_part = cap;
   return AE_OK;
 }
 
@@ -477,7 +504,22 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
     const LayerW& w = e->layers[li];
     const bool last_cls = cls_only && li == NL - 1;
     int rc;
-    if (pl) {
+    if (last_cls && e->cls_absorb) {
+      // the CLS query per sequence, then attention with W_k absorbed / W_v deferred over the
+      // layer-input rows (cls_attention.hip); no K / V projection of the T rows
+      HIPC(ae_launch_gather_cls(e->x, e->x, e->cu, n, e->cc, e->xc, st));
+      if ((rc = gemm(e, e->xc, w.wqkv, w.wqkv_h, w.wqkv_l, w.bqkv, nullptr, e->hc, n, H, H,
+                     EPI_BIAS, st, false)))
+        return rc;
+      if ((rc = ensure_cls_part(e, T, n))) return rc;
+      Prof p(e, st, e->prof_kind == AE_KIND_ATTENTION, 0.0);
+      // split modes fold log2(e)/8 into W_q (ae_create); the exact mode scales here
+      const float scale = e->cfg.precision == AE_PREC_FP32 ? 0.18033688011112042f : 1.0f;
+      HIPC(ae_launch_cls_attention(e->x, e->hc, w.wqkv + (size_t)H * H,
+                                   w.wqkv + (size_t)2 * H * H, w.bqkv + 2 * H, e->cu, n, max_len,
+                                   mask_bits, L, scale, e->cls_u, e->cls_part, e->cls_y, e->cc,
+                                   e->err, st));
+    } else if (pl) {
       // Q | K | V as packed planes (Q pre-scaled) straight into the attention's LDS-DMA
       if ((rc = gemm_pk(e, e->xp, w.wqkv_p, w.bqkv, nullptr, nullptr, qkvp, (int)T, 3 * H, H,
                         EPI_BIAS_PACKED, st, false)))
@@ -486,7 +528,7 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
                           3 * H, H, EPI_BIAS, st, false))) {
       return rc;
     }
-    {
+    if (!(last_cls && e->cls_absorb)) {
       const double flop = 0.0;  // attention FLOP are accounted by the caller
       Prof p(e, st, e->prof_kind == AE_KIND_ATTENTION, flop);
       if (e->cfg.precision == AE_PREC_FP32)
@@ -517,7 +559,7 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
         return rc;
       HIPC(ae_launch_layernorm(e->tmp, w.ln2g, w.ln2b, eps, (int)T, e->x, nullptr, 0, st));
     } else {
-      HIPC(ae_launch_gather_cls(e->ctx, e->x, e->cu, n, e->cc, e->xc, st));
+      if (!e->cls_absorb) HIPC(ae_launch_gather_cls(e->ctx, e->x, e->cu, n, e->cc, e->xc, st));
       if ((rc = gemm(e, e->cc, w.wo, w.wo_h, w.wo_l, w.bo, e->xc, e->tc, n, H, H, EPI_BIAS_RESIDUAL, st,
                      false)))
         return rc;
@@ -694,6 +736,10 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
   HIPC(hipMemcpy(e->one, one_host, 16, hipMemcpyHostToDevice));
   HIPC(hipEventCreateWithFlags(&e->pinned_ready, hipEventDisableTiming));
   HIPC(hipEventRecord(e->pinned_ready, nullptr));
+  {
+    const char* ca = std::getenv("AE_CLS_ABSORB");  // A/B runs: 0 = full-T QKV + attention
+    e->cls_absorb = !(ca && ca[0] == '0');
+  }
   if (e->planes) {
     // on unless AE_SPLIT_STREAMS=0 (tools/split_ab.py, profiles/r3s_split_streams_ab.json:
     // B=64 x L=512 16.58 -> 16.35 ms per step, ragged lens 40..512 11.36 -> 9.53 ms)
@@ -701,8 +747,15 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
     e->split = !(sp && sp[0] == '0');
     const char* lag = std::getenv("AE_SPLIT_LAG");  // experiments: 1 (QKV) .. 7 (whole layer 0)
     if (lag && lag[0] >= '1' && lag[0] <= '7') e->split_lag = lag[0] - '0';
-    const char* av = std::getenv("AE_ATTN_VARIANT");  // experiments: e.g. 6 (the round-3 loop)
-    if (av) e->attn_variant = std::atoi(av);
+    const char* av = std::getenv("AE_ATTN_VARIANT");  // A/B runs: 6 or 66 (67 = production)
+    if (av) {
+      const int v = std::atoi(av);
+      if (v != 0 && v != 6 && v != 66 && v != 67) {
+        ae_destroy(e);
+        return fail(AE_EINVAL, "AE_ATTN_VARIANT must be 6, 66 or 67 (the exact loops)");
+      }
+      e->attn_variant = v == 67 ? 0 : v;
+    }
     const char* parts = std::getenv("AE_SPLIT_PARTS");  // experiments: 2 (default) .. 4
     if (parts && parts[0] >= '2' && parts[0] <= '4') e->split_parts = parts[0] - '0';
     if (e->split) {

@@ -10,26 +10,19 @@
 //     a·w ≈ a_hi·w_hi + a_hi·w_lo + a_lo·w_hi          (3 bf16 MFMAs, f32 accumulate)
 // from ONE load of the four planes.
 //
-// Three kernels: gemm_pp_kernel and gemm_pp192_kernel (below; the production path, chosen per
-// shape by ae_launch_gemm_packed) and gemm_pk_kernel (the round-1 kernel, now reachable only
-// through ae_bench_gemm_packed for A/B runs; its gfx950 mapping:)
-//   * tile 256 x BN (BN = 256: 8 waves as 2 x 4, wave tile 128 x 64; BN = 128: 4 x 2, 64 x 64),
-//     one 512-thread workgroup per CU, LDS NST x (256 + BN) x 128 B (NST = 3 stages for BN = 128,
-//     2 for BN = 256)
+// Two kernels, chosen per shape by ae_launch_gemm_packed: gemm_pp_kernel (256 x 256 tiles, every
+// epilogue) and gemm_pp192_kernel (256 x 192 tiles for the N = 768 GEMMs, f32 epilogues and the
+// fused residual + LayerNorm).  Both:
 //   * operands reach LDS by LDS-DMA (global_load_lds_dwordx4, one wave instruction = 8 rows x
 //     128 B, lane-linear image); the 16-B chunk of row r is XOR-swizzled by (r >> 1) & 7 on the
 //     SOURCE address, so fragment ds_read_b128s of 16 rows hit 16 different bank slots
-//   * a K-tile's fragments are pulled from LDS into registers as soon as the tile has landed;
-//     2 stages (BN = 256): once every wave holds them (a second barrier) the stage is refilled
-//     with tile k+2; 3 stages (BN = 128): tile k+2 goes into tile k-1's stage right after the
-//     K-tile's one barrier, so two K-tiles of DMA are in flight behind the MFMAs — the kernel is
-//     bound by how many bytes a CU keeps in flight (tools/gemm_bench.py diag runs)
-//   * the MFMAs of the first half of the tile run between the fragment reads and that barrier,
-//     overlapping the LDS reads of the other waves
 //   * DMA issued from inline asm with hand-counted vmcnt (the compiler's wait-count pass would
 //     otherwise drain it before every fragment read); raw s_barrier; XCD-aware tile order
 //   * epilogues: +bias -> f32, +bias+residual -> f32, +bias -> tanh -> f32, +bias -> GELU -> packed
-//     bf16 planes (the FFN2 operand)
+//     bf16 planes (the FFN2 operand), +bias -> packed planes (QKV), +bias+residual -> LayerNorm
+// The round-1 kernel (gemm_pk_kernel, one wave group, 2-3 stage ring), the role-split persistent
+// kernel (gemm_pprs_kernel) and the two-workgroups-per-CU kernel (gemm_w2.hip) were measured
+// slower and removed (git history before round 4; DESIGN.md §3 keeps their numbers).
 #include <type_traits>
 
 #include "common.h"
@@ -70,7 +63,7 @@ struct LnArgs {
 };
 
 namespace {
-constexpr int PK_BM = 256, PK_ROWB = 128;
+constexpr int PK_ROWB = 128;
 
 // One LDS-DMA wave instruction: 64 lanes x 16 B from per-lane global addresses into
 // lds_base + 16 * lane (SALU write of m0 -> LDS-DMA needs one wait state).
@@ -94,9 +87,6 @@ __device__ __forceinline__ void wait_vm() {
   else static_assert(N == 0, "unsupported vmcnt");
 }
 
-// LDS stages of the DMA ring: 3 when they fit in 160 KiB (256 x 128 tiles: 3 x 48 KiB), else 2
-template <int BN>
-constexpr int pk_stages() { return 3 * (256 + BN) * 128 <= 160 * 1024 ? 3 : 2; }
 }  // namespace
 
 // keeps a value live in a diagnostic build whose consumer was cut out (rule 17)
@@ -107,317 +97,11 @@ __device__ __forceinline__ size_t pk_index(int row, int col, int ld, int np, int
   return (size_t)row * np * ld + (size_t)(col >> 5) * 32 * np + 32 * p + (col & 31);
 }
 
-// DIAG (timing experiments only, reachable only through ae_bench_gemm_packed; results WRONG):
-// 1 = no refill DMA after the first two K-tiles, 2 = no post-read barrier, 3 = no barriers at
-// all, 4 = no fragment reads after the first K-tile, 5 = no MFMAs, 6 = epilogue only,
-// 7 = no epilogue stores.  The production instantiations have DIAG = 0.
-template <int BN, int NP, int EPI, int DIAG>
-__global__ __launch_bounds__(512, 1) void gemm_pk_kernel(
-    const __bf16* __restrict__ A, const __bf16* __restrict__ W, const float* __restrict__ bias,
-    const float* __restrict__ R, float* __restrict__ C, __bf16* __restrict__ Cp, int M, int N,
-    int K, int group_m) {
-  constexpr int diag = DIAG;
-  extern __shared__ __attribute__((aligned(16))) unsigned char pk_smem[];
-  constexpr int WM = BN == 256 ? 2 : 4, WN = 8 / WM;
-  constexpr int TM = PK_BM / WM / 32, TN = BN / WN / 32;
-  constexpr int A_BYTES = PK_BM * PK_ROWB, W_BYTES = BN * PK_ROWB;
-  constexpr int STAGE = A_BYTES + W_BYTES;
-  constexpr int NST = pk_stages<BN>();                 // ring depth: NST-1 K-tiles in flight
-  constexpr int A_DMA = PK_BM / 64, W_DMA = BN / 64;  // DMA instructions per wave per K-tile
-  constexpr int DMA = A_DMA + W_DMA;
-  constexpr int KB = 64 / NP;                          // k per K-tile
-  constexpr int NS = KB / 16;                          // 16-deep MFMA steps per K-tile
-  constexpr int NS0 = NS / 2;                          // steps multiplied before the refill
-
-  const int tiles_n = (N + BN - 1) / BN;
-  const int tiles_m = (M + PK_BM - 1) / PK_BM;
-  // XCD-contiguous tile order, then grouped: group_m M-tiles sweep the N-tiles together, so the
-  // ~32 tiles an XCD runs at once share both their A rows and their W rows in its L2
-  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int per_group = group_m * tiles_n;
-  const int g = t / per_group, first_m = g * group_m;
-  const int gsize = min(tiles_m - first_m, group_m);
-  const int tm = first_m + (t - g * per_group) % gsize, tn = (t - g * per_group) / gsize;
-  const int m0 = tm * PK_BM, n0 = tn * BN;
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WN, wn = wave % WN;
-  const int li = lane & 31, lh = lane >> 5;
-  const size_t lda = (size_t)NP * K;  // packed row length (elements), A and W
-
-  // ---- per-lane DMA sources at K-tile 0 (instruction u covers rows 8 * (DMA_X * wave + u) + lane/8)
-  const char* a_src[A_DMA];
-  const char* w_src[W_DMA];
-#pragma unroll
-  for (int u = 0; u < A_DMA; ++u) {
-    const int r = 8 * (A_DMA * wave + u) + (lane >> 3);
-    const int cs = (lane & 7) ^ ((r >> 1) & 7);
-    const int gr = m0 + r < M ? m0 + r : M - 1;
-    a_src[u] = reinterpret_cast<const char*>(A + gr * lda) + 16 * cs;
-  }
-#pragma unroll
-  for (int u = 0; u < W_DMA; ++u) {
-    const int r = 8 * (W_DMA * wave + u) + (lane >> 3);
-    const int cs = (lane & 7) ^ ((r >> 1) & 7);
-    const int gr = n0 + r < N ? n0 + r : N - 1;
-    w_src[u] = reinterpret_cast<const char*>(W + gr * lda) + 16 * cs;
-  }
-  const uint32_t lds0 = (uint32_t)(uintptr_t)pk_smem;
-  const int nk = diag == 6 ? 0 : K / KB;
-
-  auto issue = [&](int kt) {
-    const int kb = kt * PK_ROWB;  // byte offset of K-tile kt in a packed row
-    const uint32_t st = lds0 + (kt % NST) * STAGE;
-#pragma unroll
-    for (int u = 0; u < A_DMA; ++u) dma16(a_src[u] + kb, st + (A_DMA * wave + u) * 1024);
-#pragma unroll
-    for (int u = 0; u < W_DMA; ++u) dma16(w_src[u] + kb, st + A_BYTES + (W_DMA * wave + u) * 1024);
-  };
-
-  floatx16 acc[TM][TN];
-#pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int b = 0; b < TN; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-
-  // fragment rows are 32-aligned + li, so the row swizzle is (li >> 1) & 7
-  const int sw = (li >> 1) & 7;
-  const int a_row0 = (wm * (PK_BM / WM) + li) * PK_ROWB;
-  const int w_row0 = A_BYTES + (wn * (BN / WN) + li) * PK_ROWB;
-
-  auto mfma_step = [&](const bf16x8 (&fa)[NP][TM], const bf16x8 (&fw)[NP][TN]) {
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        if (NP == 2) {
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][a], fw[0][b], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][a], fw[1][b], acc[a][b], 0, 0, 0);
-        }
-        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][a], fw[0][b], acc[a][b], 0, 0, 0);
-      }
-  };
-
-  auto keep_live = [&](const bf16x8 (&fa)[NP][TM], const bf16x8 (&fw)[NP][TN]) {
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-#pragma unroll
-      for (int a = 0; a < TM; ++a) asm volatile("" ::"v"(fa[p][a]));
-#pragma unroll
-      for (int b = 0; b < TN; ++b) asm volatile("" ::"v"(fw[p][b]));
-    }
-  };
-
-  bf16x8 fa[NS][NP][TM], fw[NS][NP][TN];
-  // prologue: tiles 0 and 1 (both ring depths refill with tile kt+2 during iteration kt)
-  if (nk > 0) issue(0);
-  if (nk > 1) issue(1);
-  for (int kt = 0; kt < nk; ++kt) {
-    // tile kt landed (this wave's DMA; kt+1 may still be in flight), then visible to all waves
-    if (kt + 1 < nk) wait_vm<DMA>();
-    else wait_vm<0>();
-    if (diag != 3) __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    const unsigned char* st = pk_smem + (kt % NST) * STAGE;
-    if constexpr (NST == 3) {
-      // 3-stage ring: every wave is past this barrier, so every wave has finished reading tile
-      // kt-1 — its stage takes tile kt+2 during this K-tile, and one barrier per K-tile suffices.
-      // Issue order, pinned: step-0 fragment reads, then the step-0.. MFMAs with the later
-      // steps' fragment reads and the DMA pieces of tile kt+2 spread between them (a DMA piece
-      // issued in a burst holds the wave's issue for ~60-100 cycles each; between MFMAs it
-      // hides in their issue gaps), then the last step's MFMAs.
-      constexpr int T = NP == 2 ? 3 : 1;
-      constexpr int MPS = T * TM * TN;           // MFMAs per 16-deep step
-      constexpr int RPS = NP * (TM + TN);         // fragment reads per step
-      constexpr int MU = (NS - 1) * MPS, RU = (NS - 1) * RPS;
-      auto read_one = [&](int s, int i) {        // i-th fragment read of step s
-        const int p = i / (TM + TN), j = i % (TM + TN);
-        const int coff = 16 * ((4 * p + 2 * s + lh) ^ sw);
-        if (j < TN)
-          fw[s][p][j] = *reinterpret_cast<const bf16x8*>(st + w_row0 + j * 32 * PK_ROWB + coff);
-        else
-          fa[s][p][j - TN] =
-              *reinterpret_cast<const bf16x8*>(st + a_row0 + (j - TN) * 32 * PK_ROWB + coff);
-      };
-      auto mfma_one = [&](int s, int i) {        // i-th MFMA of step s
-        const int a = i / (T * TN), b = (i / T) % TN, term = i % T;
-        if (diag == 5) {
-          keep_f32(acc[a][b][0]);
-          return;
-        }
-        const bf16x8& x = (T == 3 && term == 0) ? fa[s][NP - 1][a] : fa[s][0][a];
-        const bf16x8& y = (T == 3 && term == 1) ? fw[s][NP - 1][b] : fw[s][0][b];
-        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, acc[a][b], 0, 0, 0);
-      };
-      const bool refill = kt + 2 < nk && diag != 1;
-      const int kb = (kt + 2) * PK_ROWB;
-      const uint32_t nst = lds0 + ((kt + 2) % NST) * STAGE;
-      auto dma_one = [&](int j) {
-        if (!refill) return;
-        if (j < A_DMA) dma16(a_src[j] + kb, nst + (A_DMA * wave + j) * 1024);
-        else dma16(w_src[j - A_DMA] + kb, nst + A_BYTES + (W_DMA * wave + j - A_DMA) * 1024);
-      };
-#pragma unroll
-      for (int i = 0; i < RPS; ++i)
-        if (diag != 4 || kt == 0) read_one(0, i);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_sched_barrier(0);
-      // MU MFMAs, RU reads and the DMA pieces in DMA groups, each group's share pinned in order
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int g = 0; g < DMA; ++g) {
-#pragma unroll
-        for (int i = g * MU / DMA; i < (g + 1) * MU / DMA; ++i) mfma_one(i / MPS, i % MPS);
-#pragma unroll
-        for (int i = g * RU / DMA; i < (g + 1) * RU / DMA; ++i)
-          if (diag != 4 || kt == 0) read_one(1 + i / RPS, i % RPS);
-        __builtin_amdgcn_sched_barrier(0);
-        dma_one(g);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#pragma unroll
-      for (int i = 0; i < MPS; ++i) mfma_one(NS - 1, i);
-      __builtin_amdgcn_s_setprio(0);
-      continue;
-    }
-    auto read_step = [&](int s) {
-#pragma unroll
-      for (int p = 0; p < NP; ++p) {
-        const int coff = 16 * ((4 * p + 2 * s + lh) ^ sw);
-#pragma unroll
-        for (int b = 0; b < TN; ++b)
-          fw[s][p][b] = *reinterpret_cast<const bf16x8*>(st + w_row0 + b * 32 * PK_ROWB + coff);
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-          fa[s][p][a] = *reinterpret_cast<const bf16x8*>(st + a_row0 + a * 32 * PK_ROWB + coff);
-      }
-    };
-#pragma unroll
-    for (int s = 0; s < NS0; ++s)
-      if (diag != 4 || kt == 0) read_step(s);
-    __builtin_amdgcn_sched_barrier(0);
-    // first-half MFMAs interleaved with the second-half fragment reads (<= 15 LDS ops in flight)
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = NS0; s < NS; ++s)
-      if (diag != 4 || kt == 0) read_step(s);
-#pragma unroll
-    for (int s = 0; s < NS0; ++s) {
-      if (diag != 5) mfma_step(fa[s], fw[s]);
-      else keep_live(fa[s], fw[s]);
-    }
-    {
-      constexpr int RD1 = (NS - NS0) * NP * (TM + TN);
-      constexpr int MF0 = NS0 * (NP == 2 ? 3 : 1) * TM * TN;
-      constexpr int PER = MF0 / RD1 > 0 ? MF0 / RD1 : 1;
-#pragma unroll
-      for (int i = 0; i < RD1; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, PER, 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);    // DS read
-      }
-      if (MF0 > PER * RD1) __builtin_amdgcn_sched_group_barrier(0x008, MF0 - PER * RD1, 0);
-    }
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (NST == 2) {
-      // every wave holds tile kt in registers: refill its stage with tile kt+2
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (diag != 2 && diag != 3) __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      if (kt + 2 < nk && diag != 1) issue(kt + 2);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = NS0; s < NS; ++s) {
-      if (diag != 5) mfma_step(fa[s], fw[s]);
-      else keep_live(fa[s], fw[s]);
-    }
-    __builtin_amdgcn_s_setprio(0);
-  }
-  if constexpr (DIAG == 7) {
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int b = 0; b < TN; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) keep_f32(acc[a][b][r]);
-    return;
-  }
-
-  // ---- epilogue through LDS: each 32x32 accumulator tile is transposed through a private
-  // 32 x 33-float LDS slab so that every global access is a 16-byte-per-lane row segment
-  // (4 floats of C / R, or 8 hi + 8 lo bf16 of a packed block) instead of one element per lane
-  __syncthreads();  // the stages are reused as scratch: every wave has finished the main loop
-  float* slab = reinterpret_cast<float*>(pk_smem) + wave * 32 * 33;
-#pragma unroll
-  for (int b = 0; b < TN; ++b) {
-    const int cb = n0 + wn * (BN / WN) + b * 32;  // first column of the tile (N % 32 == 0)
-#pragma unroll
-    for (int a = 0; a < TM; ++a) {
-      const int rb = m0 + wm * (PK_BM / WM) + a * 32;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) slab[mfma32_row(r, lh) * 33 + li] = acc[a][b][r];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slab is written before it is read
-      if (cb < N) {
-        if (EPI == PK_EPI_GELU_PACKED) {
-          // lane -> row (lane >> 2) + 16 pass, 8 columns c8 = 8 * (lane & 3)
-          const int c8 = 8 * (lane & 3);
-          floatx4 b0 = *reinterpret_cast<const floatx4*>(bias + cb + c8);
-          floatx4 b1 = *reinterpret_cast<const floatx4*>(bias + cb + c8 + 4);
-#pragma unroll
-          for (int pass = 0; pass < 2; ++pass) {
-            const int rr = 16 * pass + (lane >> 2);
-            const int row = rb + rr;
-            bf16x8 h, l;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float v = gelu_erfc_fast(slab[rr * 33 + c8 + e] + (e < 4 ? b0[e] : b1[e - 4]));
-              const __bf16 hv = (__bf16)v;
-              h[e] = hv;
-              l[e] = (__bf16)(v - (float)hv);
-            }
-            if (row < M) {
-              __bf16* dst = Cp + (size_t)row * NP * N + (size_t)(cb >> 5) * 32 * NP + c8;
-              *reinterpret_cast<bf16x8*>(dst) = h;
-              if (NP == 2) *reinterpret_cast<bf16x8*>(dst + 32) = l;
-            }
-          }
-        } else {
-          // lane -> row (lane >> 3) + 8 pass, 4 columns c4 = 4 * (lane & 7)
-          const int c4 = 4 * (lane & 7);
-          const floatx4 bv = *reinterpret_cast<const floatx4*>(bias + cb + c4);
-#pragma unroll
-          for (int pass = 0; pass < 4; ++pass) {
-            const int rr = 8 * pass + (lane >> 3);
-            const int row = rb + rr;
-            if (row < M) {
-              const size_t o = (size_t)row * N + cb + c4;
-              floatx4 v;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = slab[rr * 33 + c4 + e] + bv[e];
-              if (EPI == PK_EPI_TANH)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
-              if (EPI == PK_EPI_RES) v += *reinterpret_cast<const floatx4*>(R + o);
-              *reinterpret_cast<floatx4*>(C + o) = v;
-            }
-          }
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slab reads done before the next tile overwrites it
-    }
-  }
-}
-
 // ------------------------------------------------------------------------------------------
 // Ping-pong 256 x 256 packed GEMM (gemm_pp_kernel).
 //
-// The same product over the same packed planes as gemm_pk_kernel, with the main loop built so
-// that a SIMD's matrix pipe is fed by one wave while its other wave moves data:
+// The main loop is built so that a SIMD's matrix pipe is fed by one wave while its other wave
+// moves data:
 //   * 8 waves = two groups of four (wave w sits on SIMD w % 4, so each SIMD holds one wave of
 //     each group); group g owns rows 128 g .. 128 g + 127 of the tile, wave (g, wn) a 128 x 64
 //     block.  Group 1 executes one extra s_barrier before the loop, so between any two barriers
@@ -770,309 +454,6 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
-  }  // tile loop
-}
-
-// ------------------------------------------------------------------------------------------
-// Role-split persistent ping-pong GEMM (gemm_pprs_kernel; experiment, packed-plane epilogues
-// only, reachable through ae_bench_gemm_packed diag 10 / 11).
-//
-// gemm_pp_kernel's main loop and tile order on a persistent grid, arranged so that a tile's
-// epilogue write burst drains behind the next tile's MFMAs.  vmcnt is per wave and counts stores
-// and loads in issue order, so a wave that stores cannot wait for a DMA issued after its stores
-// without waiting for the stores too.  Hence the roles alternate by tile: at the end of local tile
-// i only wave group (i & 1) issues the tile's global stores (its own 64-row blocks and its
-// partner's — wave w ^ 4 — through the LDS staging regions); for the prologue and the first H
-// K-tiles of tile i + 1 the other group issues every DMA piece (its own and its partner's, the
-// counted waits doubled) while the storing group issues and waits for nothing.  From K-tile H on
-// both groups run the production schedule; the storing group's first wait (for a piece it issued
-// itself, at K-tile H + 1) comes after its stores in the queue, by then H K-tiles of MFMAs later.
-// DMA sources as saddr offsets: per-lane 32-bit byte offsets from the tile's first A / W row,
-// the K-tile advance on the scalar base.
-namespace {
-__device__ __forceinline__ void dma16s_pk(uint32_t voff, const void* sbase, uint32_t lds_base) {
-  asm volatile(
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %0, %1"
-      :
-      : "v"(voff), "s"(sbase), "s"(lds_base)
-      : "memory", "m0");
-}
-// s_waitcnt vmcnt(x) with x the largest supported value <= n (waiting longer is always safe)
-__device__ __forceinline__ void pprs_wait(int n) {
-  if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else if (n >= 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-}  // namespace
-
-template <int NP, int EPI>
-__global__ __launch_bounds__(512, 1) void gemm_pprs_kernel(
-    const __bf16* __restrict__ A, const __bf16* __restrict__ W, const float* __restrict__ bias,
-    __bf16* __restrict__ Cp, int M, int N, int K, int group_m, int H) {
-  static_assert(EPI == PK_EPI_GELU_PACKED || EPI == PK_EPI_BIAS_PACKED, "packed epilogues only");
-  extern __shared__ __attribute__((aligned(16))) unsigned char pk_smem[];
-  constexpr int BM = 256, BN = 256, ROWB = PK_ROWB;
-  constexpr int A_BYTES = BM * ROWB, STAGE = (BM + BN) * ROWB;
-  constexpr int KB = 64 / NP, NS = KB / 16, T = NP == 2 ? 3 : 1;
-  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM, tiles = tiles_m * tiles_n;
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int lda = NP * K;
-  const uint32_t lds0 = (uint32_t)(uintptr_t)pk_smem;
-  const int nk = K / KB;
-  const bool split_ok = nk >= H + 3;  // enough K-tiles for the hand-over (uniform)
-
-  int it = 0;
-  for (int vb = blockIdx.x; vb < tiles; vb += gridDim.x, ++it) {
-    // the lane id made opaque per tile: every lane-derived address is recomputed inside the tile
-    // instead of hoisted out of the tile loop (which spills)
-    int lane = tid & 63;
-    asm volatile("" : "+v"(lane));
-    const int li = lane & 31, lh = lane >> 5;
-    const int sw = (li >> 1) & 7;
-    const int a_row = (wm * 128 + li) * ROWB;
-    const int w_row = A_BYTES + (wn * 64 + li) * ROWB;
-    const int t = xcd_remap(vb, tiles);
-    const int per_group = group_m * tiles_n;
-    const int g = t / per_group, first_m = g * group_m;
-    const int gsize = min(tiles_m - first_m, group_m);
-    const int tm0 = first_m + (t - g * per_group) % gsize, tn0 = (t - g * per_group) / gsize;
-    const int m0 = tm0 * BM, n0 = tn0 * BN;
-    // roles of this tile's hand-over (tile it - 1 was stored by group (it - 1) & 1)
-    const bool hand = it > 0 && split_ok;
-    const bool idle = hand && wm != (it & 1);  // stored the previous tile: no DMA before K-tile H
-    const bool dbl = hand && wm == (it & 1);   // issues its partner's pieces too
-    const char* abase = reinterpret_cast<const char*>(A + (size_t)m0 * lda);
-    const char* wbase = reinterpret_cast<const char*>(W + (size_t)n0 * lda);
-    // DMA pieces (8 rows x 128 B), as gemm_pp_kernel: [0,1] A(mh 0), [2,3] W(nh 0), [4,5] W(nh 1),
-    // [6,7] A(mh 1); off[0] this wave's, off[1] its partner's (wave ^ 4)
-    uint32_t off[2][8];
-#pragma unroll
-    for (int w2 = 0; w2 < 2; ++w2) {
-      const int wv = w2 ? (wave ^ 4) : wave;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int pidx = 2 * wv + (j & 1);
-        const bool is_a = j < 2 || j >= 6;
-        const int r0 = is_a ? (pidx >> 3) * 128 + (pidx & 7) * 8 + (j >= 6 ? 64 : 0)
-                            : (pidx >> 2) * 64 + (pidx & 3) * 8 + (j >= 4 ? 32 : 0);
-        const int r = r0 + (lane >> 3);
-        const int cs = (lane & 7) ^ ((r >> 1) & 7);
-        const int gr = is_a ? min(m0 + r, M - 1) - m0 : min(n0 + r, N - 1) - n0;
-        off[w2][j] = (uint32_t)gr * (uint32_t)(lda * 2) + 16u * cs;
-      }
-    }
-    auto piece = [&](int w2, int j, int kd) {
-      const int wv = w2 ? (wave ^ 4) : wave;
-      const int pidx = 2 * wv + (j & 1);
-      const bool is_a = j < 2 || j >= 6;
-      const int r0 = is_a ? (pidx >> 3) * 128 + (pidx & 7) * 8 + (j >= 6 ? 64 : 0)
-                          : (pidx >> 2) * 64 + (pidx & 3) * 8 + (j >= 4 ? 32 : 0);
-      const uint32_t dst = (is_a ? 0u : (uint32_t)A_BYTES) + (uint32_t)r0 * ROWB;
-      dma16s_pk(off[w2][j], (is_a ? abase : wbase) + (size_t)kd * ROWB,
-                lds0 + (kd & 1) * STAGE + dst);
-    };
-    // quarter q of K-tile kd, by the roles in force at loop K-tile kt (kt = -1: the prologue)
-    auto issue_q = [&](int q, int kd, int kt) {
-      const bool early = kt < H;
-      if (!(idle && early)) {
-        piece(0, 2 * q, kd);
-        piece(0, 2 * q + 1, kd);
-      }
-      if (dbl && early) {
-        piece(1, 2 * q, kd);
-        piece(1, 2 * q + 1, kd);
-      }
-    };
-
-    floatx16 acc[4][2];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-    bf16x8 fa[2][NS][NP];
-    bf16x8 fw[2][NS][NP];
-    auto read_a = [&](const unsigned char* st, int mh) {
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-        for (int s = 0; s < NS; ++s)
-#pragma unroll
-          for (int p = 0; p < NP; ++p)
-            fa[tt][s][p] = *reinterpret_cast<const bf16x8*>(
-                st + a_row + (2 * mh + tt) * 32 * ROWB + 16 * ((4 * p + 2 * s + lh) ^ sw));
-    };
-    auto read_w = [&](const unsigned char* st, int nh) {
-#pragma unroll
-      for (int s = 0; s < NS; ++s)
-#pragma unroll
-        for (int p = 0; p < NP; ++p)
-          fw[nh][s][p] = *reinterpret_cast<const bf16x8*>(
-              st + w_row + nh * 32 * ROWB + 16 * ((4 * p + 2 * s + lh) ^ sw));
-    };
-    // a quadrant's MFMAs with DMA quarter q of K-tile kd in the issue gaps (both halves of the
-    // quarter's pieces after the first and second thirds of the MFMAs, as gemm_pp_kernel)
-    auto mfma_quad = [&](int mh, int nh, auto qc, bool dma, int kd, int kt) {
-      constexpr int q = decltype(qc)::value;
-      constexpr int NM = NS * 2 * T;
-      const bool own = dma && !(idle && kt < H), part = dma && dbl && kt < H;
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < NM; ++i) {
-        const int s = i / (2 * T), tt = (i / T) % 2, term = i % T;
-        floatx16& c = acc[2 * mh + tt][nh];
-        const bf16x8& x = (T == 3 && term == 1) ? fw[nh][s][NP - 1] : fw[nh][s][0];
-        const bf16x8& y = (T == 3 && term == 0) ? fa[tt][s][NP - 1] : fa[tt][s][0];
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, c, 0, 0, 0);
-        if (i == NM / 3 - 1 || i == 2 * NM / 3 - 1) {
-          const int j = 2 * q + (i == NM / 3 - 1 ? 0 : 1);
-          __builtin_amdgcn_sched_barrier(0);
-          if (own) piece(0, j, kd);
-          if (part) piece(1, j, kd);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      __builtin_amdgcn_s_setprio(0);
-    };
-    auto sync_compute = [&]() {
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    auto sync_load = [&]() {
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    // counted wait at phase ph of K-tile kt for this wave's own pieces (see the role comment):
-    // doubled counts while it issues its partner's pieces, none while it issues nothing
-    auto wait_q = [&](int ph, int kt, bool full) {
-      if (!full) pprs_wait(0);
-      else if (idle && kt <= H) {
-      } else if (dbl && kt < H) pprs_wait(12);
-      else if (dbl && kt == H) pprs_wait(ph == 0 ? 12 : ph == 1 ? 10 : 6);
-      else pprs_wait(6);
-    };
-
-    // prologue: K-tile 0 whole and K-tile 1's first two quarters
-#pragma unroll
-    for (int q = 0; q < 4; ++q) issue_q(q, 0, -1);
-    if (nk > 1) {
-      issue_q(0, 1, -1);
-      issue_q(1, 1, -1);
-      if (!idle) pprs_wait(dbl ? 16 : 8);  // K-tile 0's A(mh 0) + W(nh 0) of what this wave issued
-    } else {
-      pprs_wait(0);
-    }
-    __builtin_amdgcn_s_barrier();
-    if (wm == 1) sync_load();  // group 1 runs one phase behind
-
-    for (int kt = 0; kt < nk; ++kt) {
-      const unsigned char* st = pk_smem + (kt & 1) * STAGE;
-      const bool next1 = kt + 1 < nk, next2 = kt + 2 < nk;
-      wait_q(0, kt, next1);
-      read_a(st, 0);
-      read_w(st, 0);
-      sync_compute();
-      mfma_quad(0, 0, std::integral_constant<int, 2>(), next1, kt + 1, kt);
-      sync_load();
-      wait_q(1, kt, next1);
-      read_w(st, 1);
-      sync_compute();
-      mfma_quad(0, 1, std::integral_constant<int, 3>(), next1, kt + 1, kt);
-      sync_load();
-      read_a(st, 1);
-      sync_compute();
-      mfma_quad(1, 1, std::integral_constant<int, 0>(), next2, kt + 2, kt);
-      sync_load();
-      wait_q(3, kt, next2);
-      sync_compute();
-      mfma_quad(1, 0, std::integral_constant<int, 1>(), next2, kt + 2, kt);
-      sync_load();
-    }
-    pprs_wait(0);  // (nothing of this tile's DMA stays in flight into the epilogue)
-    if (wm == 0) sync_load();
-
-    // ---- epilogue: every wave stages its 64-row halves in its own 16-KiB region (as
-    // gemm_pp_kernel); with the role split, group (it & 1) stores its own and its partner's
-    // regions and the other group stores nothing
-    constexpr int RB = 64 * 2 * NP, CPR = RB / 16, RPI = 64 / CPR;
-    const bool rs = split_ok;
-    const bool storer = !rs || wm == (it & 1);
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      unsigned char* reg = pk_smem + wave * 16384;
-      const int cb0 = n0 + wn * 64;
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
-        const int lr = tt * 32 + li;
-#pragma unroll
-        for (int tn = 0; tn < 2; ++tn) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const floatx16& c = acc[2 * half + tt][tn];
-            const int cc = tn * 32 + 8 * j + 4 * lh;
-            const int col = cb0 + cc < N ? cb0 + cc : N - 4;
-            const floatx4 bv = *reinterpret_cast<const floatx4*>(bias + col);
-            ushortx4 h, l;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const float y = EPI == PK_EPI_GELU_PACKED ? gelu_erfc_fast(c[4 * j + i] + bv[i])
-                                                        : c[4 * j + i] + bv[i];
-              const __bf16 hv = (__bf16)y;
-              h[i] = __builtin_bit_cast(unsigned short, hv);
-              l[i] = f2bf(y - (float)hv);
-            }
-            const int hb = tn * 64 * NP + 2 * (8 * j + 4 * lh);
-            const int ch = ((hb >> 4) ^ (lr & 15)) & (CPR - 1);
-            *reinterpret_cast<ushortx4*>(reg + lr * RB + ch * 16 + (hb & 15)) = h;
-            if (NP == 2) {
-              const int lb = hb + 64;
-              const int cl = ((lb >> 4) ^ (lr & 15)) & (CPR - 1);
-              *reinterpret_cast<ushortx4*>(reg + lr * RB + cl * 16 + (lb & 15)) = l;
-            }
-          }
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (rs) sync_load();  // every region written before the storing group reads its partner's
-      if (storer) {
-#pragma unroll
-        for (int w2 = 0; w2 < 2; ++w2) {
-          if (w2 == 1 && !rs) break;
-          const int sw2 = w2 ? (wave ^ 4) : wave;  // whose block
-          const unsigned char* rg = pk_smem + sw2 * 16384;
-          const int lr0 = lane / CPR, c = lane % CPR;
-          const int rbase = m0 + (sw2 >> 2) * 128 + half * 64;
-          const uint32_t ldc = (uint32_t)(NP * N);
-          uint32_t off0 = (uint32_t)lr0 * ldc + c * 8;
-          asm("" : "+v"(off0));
-          const int col = cb0 + (c * 16) / (2 * NP);
-          __bf16* const tb = Cp + (size_t)rbase * NP * N + (size_t)(cb0 >> 5) * 32 * NP;
-#pragma unroll
-          for (int k = 0; k < 64 / RPI; ++k) {
-            const int lr = k * RPI + lr0;
-            const uint4 v = *reinterpret_cast<const uint4*>(rg + lr * RB + ((c ^ (lr & 15)) & (CPR - 1)) * 16);
-            if (rbase + lr < M && col < N)
-              __builtin_nontemporal_store(__builtin_bit_cast(floatx4, v),
-                                          reinterpret_cast<floatx4*>(tb + off0 + (uint32_t)(k * RPI) * ldc));
-          }
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // region reads done before it is rewritten
-      if (rs) sync_load();
-    }
-    // every wave's staging reads done before the next tile's prologue DMA rewrites the stages
-    sync_load();
   }  // tile loop
 }
 
@@ -1575,21 +956,6 @@ hipError_t pp_epi(int epi, const __bf16* A, const __bf16* W, const float* bias, 
   }
 }
 
-// the role-split persistent kernel (experiment): grid = min(tiles, CUs / share), H K-tiles of
-// hand-over
-template <int NP, int EPI>
-hipError_t pprs_launch(const __bf16* A, const __bf16* W, const float* bias, __bf16* Cp, int M,
-                       int N, int K, int group_m, int share, int H, hipStream_t st) {
-  constexpr int lds = 2 * (256 + 256) * PK_ROWB;  // 128 KiB
-  if (hipError_t e = ensure_dynamic_lds((const void*)gemm_pprs_kernel<NP, EPI>, lds); e != hipSuccess)
-    return e;
-  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
-  const int grid = std::max(1, std::min(tiles, cu_count() / share));
-  hipLaunchKernelGGL((gemm_pprs_kernel<NP, EPI>), dim3(grid), dim3(512), lds, st, A, W, bias, Cp,
-                     M, N, K, group_m, H);
-  return hipGetLastError();
-}
-
 template <int NP, int EPI, bool NT = false>
 hipError_t pp192_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R,
                         float* C, int M, int N, int K, int group_m, hipStream_t st,
@@ -1641,59 +1007,6 @@ hipError_t pp_dispatch(const unsigned short* A, const unsigned short* W, const f
 namespace {
 constexpr int PK_GROUP_M = 4;  // grouped tile order: 4 > 8 > 16 > 32 M-tiles by A/B (round 1);
                                // re-swept on the ping-pong kernel (profiles/r3at_gemm_group_m_ab.jsonl)
-
-template <int BN, int NP, int EPI, int DIAG>
-hipError_t pk_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R, float* C,
-                     __bf16* Cp, int M, int N, int K, hipStream_t st) {
-  constexpr int lds = pk_stages<BN>() * (PK_BM + BN) * PK_ROWB;
-  if (hipError_t e = ensure_dynamic_lds((const void*)gemm_pk_kernel<BN, NP, EPI, DIAG>, lds); e != hipSuccess)
-    return e;
-  const int tiles = ((M + PK_BM - 1) / PK_BM) * ((N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_pk_kernel<BN, NP, EPI, DIAG>), dim3(tiles), dim3(512), lds, st, A, W,
-                     bias, R, C, Cp, M, N, K, PK_GROUP_M);
-  return hipGetLastError();
-}
-
-template <int BN, int NP, int DIAG>
-hipError_t pk_epi(int epi, const __bf16* A, const __bf16* W, const float* bias, const float* R,
-                  float* C, __bf16* Cp, int M, int N, int K, hipStream_t st) {
-  if constexpr (DIAG != 0) {  // diagnostic builds: split-bf16, bias / GELU epilogues only
-    if (NP != 2 || (epi != PK_EPI_BIAS && epi != PK_EPI_GELU_PACKED)) return hipErrorInvalidValue;
-    if (epi == PK_EPI_BIAS)
-      return pk_launch<BN, 2, PK_EPI_BIAS, DIAG>(A, W, bias, R, C, Cp, M, N, K, st);
-    return pk_launch<BN, 2, PK_EPI_GELU_PACKED, DIAG>(A, W, bias, R, C, Cp, M, N, K, st);
-  }
-  if (epi == PK_EPI_BIAS_PACKED) return hipErrorInvalidValue;  // ping-pong kernel only
-  switch (epi) {
-    case PK_EPI_BIAS: return pk_launch<BN, NP, PK_EPI_BIAS, DIAG>(A, W, bias, R, C, Cp, M, N, K, st);
-    case PK_EPI_GELU_PACKED:
-      return pk_launch<BN, NP, PK_EPI_GELU_PACKED, DIAG>(A, W, bias, R, C, Cp, M, N, K, st);
-    case PK_EPI_RES: return pk_launch<BN, NP, PK_EPI_RES, DIAG>(A, W, bias, R, C, Cp, M, N, K, st);
-    default: return pk_launch<BN, NP, PK_EPI_TANH, DIAG>(A, W, bias, R, C, Cp, M, N, K, st);
-  }
-}
-
-// Tile width per problem: wall time ~ rounds of 256 CUs x per-tile time (256x128 ~0.55 of 256^2)
-int pick_bn(int M, int N) {
-  const long tm = (M + PK_BM - 1) / PK_BM;
-  const long t256 = tm * ((N + 255) / 256), t128 = tm * ((N + 127) / 128);
-  const double c256 = (double)((t256 + 255) / 256), c128 = 0.55 * (double)((t128 + 255) / 256);
-  return c128 < c256 ? 128 : 256;
-}
-
-template <int DIAG>
-hipError_t pk_dispatch(const unsigned short* A, const unsigned short* W, const float* bias,
-                       const float* R, float* C, unsigned short* Cp, int M, int N, int K, int epi,
-                       int np, int bn, hipStream_t st) {
-  auto bf = [](const unsigned short* p) { return reinterpret_cast<const __bf16*>(p); };
-  auto bfm = [](unsigned short* p) { return reinterpret_cast<__bf16*>(p); };
-  if (np == 2) {
-    if (bn == 256) return pk_epi<256, 2, DIAG>(epi, bf(A), bf(W), bias, R, C, bfm(Cp), M, N, K, st);
-    return pk_epi<128, 2, DIAG>(epi, bf(A), bf(W), bias, R, C, bfm(Cp), M, N, K, st);
-  }
-  if (bn == 256) return pk_epi<256, 1, DIAG>(epi, bf(A), bf(W), bias, R, C, bfm(Cp), M, N, K, st);
-  return pk_epi<128, 1, DIAG>(epi, bf(A), bf(W), bias, R, C, bfm(Cp), M, N, K, st);
-}
 
 bool pk_shape_ok(int M, int N, int K, int np) {
   return K % 64 == 0 && N % 32 == 0 && (np == 1 || np == 2) && N > 0 && M >= 0;
@@ -1796,29 +1109,12 @@ extern "C" hipError_t ae_bench_gemm_packed(const unsigned short* A, const unsign
                                            unsigned short* Cp, int M, int N, int K, int epi,
                                            int np, int bn, int diag, hipStream_t st) {
   if (M <= 0) return hipSuccess;
-  if (!pk_shape_ok(M, N, K, np) ||
-      (bn != 0 && bn != 128 && bn != 192 && bn != 256 && bn != 512))
+  if (!pk_shape_ok(M, N, K, np) || (bn != 0 && bn != 192 && bn != 512))
     return hipErrorInvalidValue;
+  if (bn == 0) bn = pp_choose(M, N, epi) == 192 ? 192 : 512;
   if (bn == 192)  // diag 8: non-temporal stores; 21-52: grouped order of diag - 20 M-tiles
     return pp192_dispatch(A, W, bias, R, C, M, N, K, epi, np,
                           diag >= 21 && diag <= 52 ? diag - 20 : PK_GROUP_M, st, diag == 8);
-  if (bn == 512 && diag >= 10 && diag <= 14) {  // role-split persistent kernel (experiment)
-    // 10: whole chip, H = 8; 11: half the CUs (one of two streams), H = 8; 12 / 13: H = 4 / 12;
-    // 14: no hand-over (every wave stores its own blocks: the kernel's base cost)
-    if (!Cp || (epi != PK_EPI_GELU_PACKED && epi != PK_EPI_BIAS_PACKED)) return hipErrorInvalidValue;
-    const int share = diag == 11 ? 2 : 1, H = diag == 12 ? 4 : diag == 13 ? 12 : diag == 14 ? 1 << 20 : 8;
-    auto a = reinterpret_cast<const __bf16*>(A);
-    auto w = reinterpret_cast<const __bf16*>(W);
-    auto cp = reinterpret_cast<__bf16*>(Cp);
-#define PPRS(NPV, E) return pprs_launch<NPV, E>(a, w, bias, cp, M, N, K, PK_GROUP_M, share, H, st)
-    if (np == 2) {
-      if (epi == PK_EPI_GELU_PACKED) PPRS(2, PK_EPI_GELU_PACKED);
-      PPRS(2, PK_EPI_BIAS_PACKED);
-    }
-    if (epi == PK_EPI_GELU_PACKED) PPRS(1, PK_EPI_GELU_PACKED);
-    PPRS(1, PK_EPI_BIAS_PACKED);
-#undef PPRS
-  }
   if (bn == 512 && diag >= 21 && diag <= 52)  // production kernel, grouped order of diag - 20 M-tiles
     return pp_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, diag - 20, st);
   if (bn == 512) {  // the ping-pong 256 x 256 kernel
@@ -1836,16 +1132,5 @@ extern "C" hipError_t ae_bench_gemm_packed(const unsigned short* A, const unsign
       default: return hipErrorInvalidValue;
     }
   }
-  if (bn == 0) bn = pick_bn(M, N);
-  switch (diag) {
-    case 0: return pk_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, bn, st);
-    case 1: return pk_dispatch<1>(A, W, bias, R, C, Cp, M, N, K, epi, np, bn, st);
-    case 2: return pk_dispatch<2>(A, W, bias, R, C, Cp, M, N, K, epi, np, bn, st);
-    case 3: return pk_dispatch<3>(A, W, bias, R, C, Cp, M, N, K, epi, np, bn, st);
-    case 4: return pk_dispatch<4>(A, W, bias, R, C, Cp, M, N, K, epi, np, bn, st);
-    case 5: return pk_dispatch<5>(A, W, bias, R, C, Cp, M, N, K, epi, np, bn, st);
-    case 6: return pk_dispatch<6>(A, W, bias, R, C, Cp, M, N, K, epi, np, bn, st);
-    case 7: return pk_dispatch<7>(A, W, bias, R, C, Cp, M, N, K, epi, np, bn, st);
-    default: return hipErrorInvalidValue;
-  }
+  return hipErrorInvalidValue;
 }

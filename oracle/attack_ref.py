@@ -38,6 +38,10 @@ class Victim:
 
     def __init__(self, score, block_size=512, task="devign", code2=None):
         self.score = score
+        # decision margins (tests of a split-precision victim against this oracle): when a list,
+        # every |p - 0.5| of a Devign prediction and every |a - b| of a comparison the attack
+        # makes (gap > most_gap, fitness > min, the importance order) is appended
+        self.margins = None
         self.block = block_size
         self.task = task
         self.base = task[4:] if task.startswith("gcb_") else task
@@ -89,10 +93,29 @@ class Victim:
     def format(self, out):
         if self.base == "devign":
             p = out.reshape(-1)
+            if self.margins is not None:
+                self.margins.extend(abs(float(x) - 0.5) for x in p)
             return [[1 - x, x] for x in p], [1 if x > 0.5 else 0 for x in p]
         if self.base == "clone":  # Clone-detection-BigCloneBench/code/model.py:81-82
             return list(out), [0 if x > 0.5 else 1 for x in out[:, 0]]
         return list(out), [int(np.argmax(x)) for x in out]  # Authorship model.py:84-89
+
+
+def _gt(victim, a, b):
+    """a > b, recording the comparison's margin on victims that collect them."""
+    m = getattr(victim, "margins", None)
+    if m is not None:
+        m.append(abs(float(a) - float(b)))
+    return a > b
+
+
+def _order_margins(victim, values):
+    """Record the gaps between adjacent values of a sort (a stable sort flips nearly-equal keys
+    when they move)."""
+    m = getattr(victim, "margins", None)
+    if m is not None:
+        v = sorted(float(x) for x in values)
+        m.extend(b - a for a, b in zip(v, v[1:]))
 
 
 def _positions(words, names):
@@ -134,6 +157,7 @@ def greedy(victim, ids0, true_label, code, subs):
     imp = [base - x[pr[0]] for x in lg[1:]]
     at = {p: i for i, p in enumerate(where)}
     score = {n: sum(imp[at[p]] for p in pos[n]) for n in pos}
+    _order_margins(victim, score.values())
     order = sorted(score.items(), key=lambda kv: kv[1], reverse=True)
     final_code, replaced, n_var, n_pos, temp_label = code, {}, 0, 0, None
     for name, _ in order:
@@ -151,9 +175,9 @@ def greedy(victim, ids0, true_label, code, subs):
                             nb_changed_var=n_var + 1, nb_changed_pos=n_pos + len(pos[name]),
                             replaced=replaced, scores=score)
             gap = current - pv[temp_label]
-            if gap > best_gap:
+            if _gt(victim, gap, best_gap):
                 best_gap, best = gap, cands[i]
-        if best_gap > 0:
+        if _gt(victim, best_gap, 0):
             n_var += 1
             n_pos += len(pos[name])
             current -= best_gap
@@ -194,7 +218,7 @@ def ga(victim, ids0, true_label, code, subs, initial_replace=None, eval_batch_si
             for i, pv in enumerate(lg):
                 temp_label = pr[i]
                 g = top - pv[temp_label]
-                if g > best_gap:
+                if _gt(victim, g, best_gap):
                     best_gap, best = g, i
             init = name if best == -1 else cands[best]
         else:
@@ -254,7 +278,7 @@ def ga(victim, ids0, true_label, code, subs, initial_replace=None, eval_batch_si
             fits.append(top - pv[orig_label])
         for i, f in enumerate(fits):
             lo = min(fitness)
-            if f > lo:
+            if _gt(victim, f, lo):
                 j = fitness.index(lo)
                 population[j] = kids[i]
                 fitness[j] = f

@@ -279,3 +279,39 @@ def test_two_stream_encoder_matches_single_stream(gpu, monkeypatch, precision, n
     np.testing.assert_allclose(a, b, atol=tol, rtol=0)
     for e in engines.values():
         e.close()
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", 2e-6), ("f32x3", 2e-5), ("bf16", 2e-2)])
+def test_cls_absorbed_attention_matches_full_path(gpu, monkeypatch, precision, tol):
+    """The last layer's CLS attention with W_k absorbed into the query and W_v applied to the
+    p-weighted row sum (cls_attention.hip, the default) against the same engine built with
+    AE_CLS_ABSORB=0 (the full-T QKV GEMM and a one-query attention): ragged lengths with
+    1..10 chunks of 64 keys and partial 16-key tiles, and the 66-way head; the two differ only
+    by summation order (plus the split products of the full path's K / V in split modes)."""
+    from apmc_amd.engine import Engine
+    sd = synthetic_sd(7, "softmaxN", 66)
+    engines = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("AE_CLS_ABSORB", mode)
+        engines[mode] = Engine(sd, head="softmaxN", num_labels=66, precision=precision)
+    rng = np.random.default_rng(40)
+    L = 640
+    lens = np.array([640, 1, 2, 17, 63, 64, 65, 130, 511, 512, 333, 600], np.int32)
+    ids = _rand_ids(rng, len(lens), L, lens)
+    a, b = _score(engines["1"], ids), _score(engines["0"], ids)
+    np.testing.assert_allclose(a, b, atol=tol, rtol=0)
+    for e in engines.values():
+        e.close()
+
+
+@pytest.mark.parametrize("precision", ["fp32", "f32x3"])
+def test_long_rows_batch_invariant_bitwise(gpu, precision):
+    """Rows of 512 tokens (8 key chunks of the CLS attention, the two-stream encoder's parts):
+    a row's probability is bit-identical whether it is scored among 200 rows or 5."""
+    eng = _engine(4, "sigmoid1", 1, precision=precision)
+    rng = np.random.default_rng(22)
+    n, L = 200, 512
+    ids = _rand_ids(rng, n, L, rng.integers(200, L + 1, n))
+    big = _score(eng, ids)
+    small = _score(eng, ids[:5])
+    assert np.array_equal(big[:5], small), np.abs(big[:5] - small).max()

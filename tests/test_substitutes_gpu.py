@@ -223,3 +223,111 @@ def test_gcb_no_cosine_substitutes_match_oracle_12_layers(gpu):
             assert set(got.get(word, [])) == set(exp.get(word, [])), word
     assert compared >= 10 and excused <= compared // 4, (compared, excused)
     eng.close()
+
+
+def _items_between(n, lo, hi):
+    """The first n fixture functions whose whitespace-joined text has lo..hi sub-words."""
+    from apmc_amd.host import Tokenizer
+    tok = Tokenizer()
+    out = []
+    with open(ROOT / "data" / "devign" / "test_subs_0_400.jsonl") as f:
+        for line in f:
+            js = json.loads(line)
+            if lo <= len(tok.encode_ids(" ".join(js["func"].split()))) <= hi:
+                out.append(js)
+            if len(out) == n:
+                break
+    return out
+
+
+def test_cosine_substitutes_f32x3_match_fp32(gpu):
+    """Config 3 ran in f32x3 (profiles/r3_config3_full.json, the bench's substitutes leg): the
+    same 12-layer cosine path in f32x3 against (i) the CPU oracle's logits for the top-60 of
+    every row and (ii) the fp32 engine — itself pinned to the CPU oracle by
+    test_cosine_substitutes_match_oracle_12_layers — for the cosine top-30 and the final sets,
+    on 8 short functions and 2 of 300-510 sub-words.  Tie bounds are MEASURED on this run:
+    eps_logit = max |f32x3 logit - oracle logit| over the top-60 entries, eps_sim = max
+    |f32x3 - fp32| cosine score; a row is excused only if the oracle's 60th/61st gap is below
+    2 eps_logit, a word only if a cut it reads (30th/31st score, 4th/5th for multi-sub-word
+    spans) is within 2 eps_sim or one of its rows is excused."""
+    from apmc_amd.attacker import get_identifiers
+    from apmc_amd.engine import Engine
+    from apmc_amd.host import Tokenizer, remove_comments
+    from apmc_amd.substitutes import SubstituteGenerator
+    from apmc_amd.utils import _tokenize
+    from apmc_amd.weights import synthetic_state_dict
+    from oracle import roberta_cpu as ora
+
+    sd = synthetic_state_dict(seed=4, head="none", with_mlm=True)
+    tok = Tokenizer()
+    e32 = Engine(sd, head="none", with_mlm=True, precision="fp32")
+    e3 = Engine(sd, head="none", with_mlm=True, precision="f32x3")
+    g32 = SubstituteGenerator(e32, tok, block_size=512)
+    g3 = SubstituteGenerator(e3, tok, block_size=512)
+    items = _items(8, 120) + _items_between(2, 300, 510)
+    runs = []
+    eps_logit = 0.0
+    for js in items:
+        idents, code_tokens = get_identifiers(remove_comments(js["func"]), "c")
+        names = [i[0] for i in idents if " " not in i[0].strip()]
+        t32, t3 = {}, {}
+        got32 = g32.generate_from_tokens(code_tokens, names, trace=t32)
+        got3 = g3.generate_from_tokens(code_tokens, names, trace=t3)
+        assert (t32["ids"] == t3["ids"]).all()
+        logits = ora.mlm_logits(sd, t3["ids"][None].astype(np.int64), layers=12,
+                                no_mask=True)[0].numpy()[1:]  # rows 1.. as the traces
+        rows = np.arange(len(t3["topk_ids"]))[:, None]
+        eps_logit = max(eps_logit, float(np.abs(t3["topk_scores"] -
+                                                logits[rows, t3["topk_ids"]]).max()))
+        runs.append((code_tokens, names, logits, t32, t3, got32, got3))
+    tie_logit = 2 * eps_logit + 1e-6
+    n_rows = n_tied = 0
+    eps_sim = 0.0
+    for code_tokens, names, logits, t32, t3, got32, got3 in runs:
+        srt = -np.sort(-logits, axis=1)[:, :61]
+        tied = set(np.nonzero(srt[:, 59] - srt[:, 60] < tie_logit)[0].tolist())
+        for r in range(len(t3["topk_ids"])):
+            if r in tied:
+                n_tied += 1
+                continue
+            top = set(np.argsort(-logits[r], kind="stable")[:60].tolist())
+            assert set(t3["topk_ids"][r].tolist()) == top == set(t32["topk_ids"][r].tolist()), r
+            n_rows += 1
+        for (w3, p3, s3, c3), (w32, p32, s32, c32) in zip(t3["sims"], t32["sims"]):
+            if c3 == c32:
+                eps_sim = max(eps_sim, float(np.abs(np.asarray(s3) - np.asarray(s32)).max()))
+    tie_sim = 2 * eps_sim + 1e-7
+    compared = excused = long_compared = 0
+    for k, (code_tokens, names, logits, t32, t3, got32, got3) in enumerate(runs):
+        srt = -np.sort(-logits, axis=1)[:, :61]
+        tied = set(np.nonzero(srt[:, 59] - srt[:, 60] < tie_logit)[0].tolist())
+        tied4 = set(np.nonzero(srt[:, 3] - srt[:, 4] < tie_logit)[0].tolist())
+        words, _, keys = _tokenize(" ".join(code_tokens), tok)
+        bad = set()
+        for (w3, p3, s3, c3), (w32, p32, s32, c32) in zip(t3["sims"], t32["sims"]):
+            assert (w3, p3) == (w32, p32)
+            k0, k1 = keys[p3]
+            span = set(range(k0, k1))
+            multi = k1 - k0 > 1
+            if span & tied or (multi and span & tied4):
+                bad.add(w3)
+                continue
+            assert c3 == c32, (w3, p3)  # the same 60 candidates, in the same order
+            s = np.sort(np.asarray(s32, np.float64))[::-1]
+            if s[29] - s[30] < tie_sim or (multi and s[3] - s[4] < tie_sim):
+                bad.add(w3)
+        for word in set(got3) | set(got32):
+            if word in bad:
+                excused += 1
+                continue
+            compared += 1
+            long_compared += k >= 8
+            assert set(got3.get(word, [])) == set(got32.get(word, [])), word
+    print(f"f32x3 substitutes: eps_logit {eps_logit:.2e}, eps_sim {eps_sim:.2e}; {n_rows} top-60 "
+          f"rows exact ({n_tied} tied), {compared} words exact ({long_compared} in the 300-510 "
+          f"sub-word functions), {excused} excused")
+    assert n_rows >= 1000 and compared >= 20 and long_compared >= 5, \
+        (n_rows, compared, long_compared, excused)
+    assert excused <= compared // 3, (compared, excused)
+    e32.close()
+    e3.close()

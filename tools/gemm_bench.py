@@ -7,8 +7,8 @@ per variant: median / min µs per launch and the algorithmic TFLOP/s (2·M·N·K
   python tools/gemm_bench.py [--shapes ffn1,ffn2,qkv,oproj] [--variants 0,5,1] [--rounds 7]
 
 A variant is "diag" (ae_bench_gemm_packed's DIAG: 0 = production kernel, other values time parts
-of the pipeline and give wrong results) optionally with "@bn" (tile width 128/256) and ":np".
-A variant "g@2" times ae_launch_gemm_w2 (two workgroups per CU, gemm_w2.hip) with group_m = g.
+of the pipeline and give wrong results) optionally with "@bn" (kernel: 512 = the 256 x 256
+ping-pong kernel, 192 = the 256 x 192 one, 0 = the production choice) and ":np".
 The *_ln shapes time ae_bench_gemm_packed_ln (O-proj / FFN2 + residual + LayerNorm fused); their
 diag is its mode (0 production, 1 no cross-workgroup exchange, 2 grouped tile order).
 """
@@ -58,9 +58,6 @@ def main():
     fn = getattr(lib, args.entry)
     fn.argtypes = [vp] * 6 + [i32] * 7 + [vp]
     fn.restype = ctypes.c_int
-    fw2 = lib.ae_launch_gemm_w2
-    fw2.argtypes = [vp] * 6 + [i32] * 6 + [vp]
-    fw2.restype = ctypes.c_int
     fln = lib.ae_bench_gemm_packed_ln
     fln.argtypes = [vp] * 6 + [i32] * 4 + [vp, vp, ctypes.c_float] + [vp] * 3 + [i32, vp]
     fln.restype = ctypes.c_int
@@ -113,10 +110,6 @@ def main():
                         stats=stats, ctr=ctr, err=err, bias=bias, Cp=Cp:
                         fln(p(A), p(W), p(bias), p(R), p(R), p(Cp), M, N, K, np_, p(gam), p(bet),
                             1e-5, p(stats), p(ctr), p(err), diag, sp))
-            elif bn == 2:  # the two-workgroups-per-CU kernel (gemm_w2.hip); diag = group_m
-                call = (lambda A=A, W=W, bias=bias, C=C, Cp=Cp, N=N, K=K, epi=epi, np_=np_,
-                        diag=diag: fw2(p(A), p(W), p(bias), p(None), p(C), p(Cp), M, N, K, epi,
-                                       np_, max(diag, 1), sp))
             else:
                 call = (lambda A=A, W=W, bias=bias, C=C, Cp=Cp, N=N, K=K, epi=epi, np_=np_, bn=bn,
                         diag=diag, R=R: fn(p(A), p(W), p(bias), p(R), p(C), p(Cp), M, N, K, epi,
