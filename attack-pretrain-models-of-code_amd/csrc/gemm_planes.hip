@@ -92,6 +92,10 @@ __device__ __forceinline__ void wait_vm() {
 // keeps a value live in a diagnostic build whose consumer was cut out (rule 17)
 __device__ __forceinline__ void keep_f32(float x) { asm volatile("" ::"v"(x)); }
 
+// 16-B chunk swizzle of row r of an epilogue staging region (gemm_pp_kernel): rows r and r + 16
+// land on different banks
+__device__ __forceinline__ int pk_swz(int r) { return (r & 15) ^ (((r >> 4) & 1) << 3); }
+
 // element offset of (row, col) in a packed [rows][NP*ld] matrix, plane p
 __device__ __forceinline__ size_t pk_index(int row, int col, int ld, int np, int p) {
   return (size_t)row * np * ld + (size_t)(col >> 5) * 32 * np + 32 * p + (col & 31);
@@ -354,8 +358,11 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
   // column wn*64 + tn*32 + 8 j + 4 (l >> 5) + i.  Per 64-row half (tm pair), the wave writes its
   // 64 x 64 block into its own 16-KiB LDS region in the output's byte image — f32 rows of 256 B,
   // or packed rows (NP 2: two 128-B [hi 32 | lo 32] blocks; NP 1: 128 B of hi) — with the 16-B
-  // chunk index XOR-ed by (row & 15) (conflict-free 16-row groups), then stores it with 16-B
-  // lanes, whole row segments per instruction.
+  // chunk index XOR-ed by pk_swz(row), then stores it with 16-B lanes, whole row segments per
+  // instruction.  A 256-B row is one sweep of the 64 LDS banks, so the 32 rows a store
+  // instruction writes (lanes 0-31) would meet rows r and r + 16 on the same banks under a plain
+  // (row & 15) swizzle: pk_swz also flips chunk bit 3 for rows 16-31 (the round-3 counters put
+  // exactly 2048 conflict cycles on every 256 x 256 tile, profiles/r3ap_pmc_sq.json).
   constexpr bool PACKED = EPI == PK_EPI_GELU_PACKED || EPI == PK_EPI_BIAS_PACKED;
   constexpr int RB = PACKED ? 64 * 2 * NP : 256;  // bytes of a row segment
   constexpr int CPR = RB / 16;                                       // 16-B chunks per row
@@ -386,18 +393,18 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
             }
             // byte of column cc's hi in the packed row: block tn, element 8 j + 4 lh
             const int hb = tn * 64 * NP + 2 * (8 * j + 4 * lh);
-            const int ch = ((hb >> 4) ^ (lr & 15)) & (CPR - 1);
+            const int ch = ((hb >> 4) ^ pk_swz(lr)) & (CPR - 1);
             *reinterpret_cast<ushortx4*>(reg + lr * RB + ch * 16 + (hb & 15)) = h;
             if (NP == 2) {
               const int lb = hb + 64;
-              const int cl = ((lb >> 4) ^ (lr & 15)) & (CPR - 1);
+              const int cl = ((lb >> 4) ^ pk_swz(lr)) & (CPR - 1);
               *reinterpret_cast<ushortx4*>(reg + lr * RB + cl * 16 + (lb & 15)) = l;
             }
           } else {
             floatx4 v;
 #pragma unroll
             for (int i = 0; i < 4; ++i) v[i] = c[4 * j + i];
-            const int ch = (cc >> 2) ^ (lr & 15);
+            const int ch = (cc >> 2) ^ pk_swz(lr);
             *reinterpret_cast<floatx4*>(reg + lr * RB + ch * 16) = v;
           }
         }
@@ -421,7 +428,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
     for (int k = 0; k < 64 / RPI; ++k) {
       const int lr = k * RPI + lr0;
       const bool ok = rbase + lr < M;
-      const uint4 v = *reinterpret_cast<const uint4*>(reg + lr * RB + ((c ^ (lr & 15)) & (CPR - 1)) * 16);
+      const uint4 v = *reinterpret_cast<const uint4*>(reg + lr * RB + ((c ^ pk_swz(lr)) & (CPR - 1)) * 16);
       const uint32_t o = off0 + (uint32_t)(k * RPI) * ldc;
       if (PACKED) {
         if (ok && col < N) {

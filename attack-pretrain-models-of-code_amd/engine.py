@@ -37,7 +37,7 @@ EXPORTS = ("ae_create", "ae_destroy", "ae_score", "ae_score_graph", "ae_graph_ma
            "ae_encode_ex", "ae_mlm_topk",
            "ae_mlm_nll", "ae_splice",
            "ae_topk", "ae_cosine_rank", "ae_set_profiling", "ae_kernel_time", "ae_last_error",
-           "ae_version")
+           "ae_version", "ae_source_hash")
 
 _LIB = None
 
@@ -55,6 +55,14 @@ def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         raise RuntimeError(f"HIP engine library not built: {p} is missing (run `make` or "
                            f"__graft_entry__.build()); there is no CPU fallback")
     lib = ctypes.CDLL(p)
+    if path is None:
+        from .buildinfo import source_hash
+
+        lib.ae_source_hash.restype = ctypes.c_char_p
+        built, here = lib.ae_source_hash().decode(), source_hash("engine")
+        if built != here:
+            raise RuntimeError(f"{p} was built from other sources (hash {built}, this tree "
+                               f"{here}): rebuild it (`make` or __graft_entry__.build())")
     vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
     lib.ae_create.argtypes = [ctypes.POINTER(AeConfig), ctypes.POINTER(AeWeightView), i32, i32,
                               ctypes.POINTER(vp)]
@@ -75,7 +83,7 @@ def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     lib.ae_last_error.restype = ctypes.c_char_p
     lib.ae_version.restype = ctypes.c_char_p
     for name in EXPORTS:
-        if name not in ("ae_last_error", "ae_version"):
+        if name not in ("ae_last_error", "ae_version", "ae_source_hash"):
             getattr(lib, name).restype = ctypes.c_int
     _LIB = lib
     return lib

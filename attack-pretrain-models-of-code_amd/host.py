@@ -26,6 +26,14 @@ def load_host_library(path=None) -> ctypes.CDLL:
     if not os.path.exists(p):
         raise RuntimeError(f"host featurisation library not built: {p} missing (run `make`)")
     lib = ctypes.CDLL(p)
+    if path is None:
+        from .buildinfo import source_hash
+
+        lib.ah_source_hash.restype = ctypes.c_char_p
+        built, here = lib.ah_source_hash().decode(), source_hash("host")
+        if built != here:
+            raise RuntimeError(f"{p} was built from other sources (hash {built}, this tree "
+                               f"{here}): rebuild it (`make` or __graft_entry__.build())")
     vp, i32, cp = ctypes.c_void_p, ctypes.c_int32, ctypes.c_char_p
     pp = ctypes.POINTER(ctypes.c_char_p)
     lib.ah_tokenizer_load.restype = vp

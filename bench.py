@@ -83,6 +83,8 @@ def parse_args():
     ap.add_argument("--clone-examples", type=int, default=32,
                     help="config-4 leg: GraphCodeBERT BigCloneBench pairs attacked (0 = skip)")
     ap.add_argument("--no-config1", action="store_true", help="skip the config-1 leg")
+    ap.add_argument("--no-microbench", action="store_true",
+                    help="skip the SURVEY §8(d) microbenchmarks (batch 1024, varlen, GCB 640)")
     ap.add_argument("--no-fp32-mode", action="store_true")
     return ap.parse_args()
 
@@ -105,13 +107,14 @@ def relaunch_as_ranks(args):
 
 
 def executed_flops_per_query(L, C=1):
-    """FLOP the engine executes per query of L tokens: 11 full layers, then the last layer's
-    QKV projection over every row but attention / O-proj / FFN for the CLS row only
-    (engine.hip run_encoder), then the head."""
-    H, F = 768, 3072
+    """FLOP the engine executes per query of L tokens: 11 full layers, then the last layer for
+    the CLS row only (engine.hip run_encoder, cls_attention.hip): its query, u = W_k^T q per head,
+    scores and the p-weighted row sum over the L layer-input rows, W_v of that sum, the O
+    projection and the FFN — no K / V projection of the L rows — then the head."""
+    H, F, NH, D = 768, 3072, 12, 64
     per_tok = 2 * (4 * H * H + 2 * H * F)
     full = 11 * (L * per_tok + 4 * L * L * H)
-    last = 2 * L * H * 3 * H + 4 * L * H + 2 * H * H + 4 * H * F
+    last = 2 * H * H + 2 * NH * D * H + 4 * L * H * NH + 2 * NH * H * D + 2 * H * H + 4 * H * F
     return full + last + 2 * H * H + 2 * H * C
 
 
@@ -124,7 +127,13 @@ def flops_per_query(L, C=1):
 def pmc_traffic_per_launch(precision):
     """HBM bytes per FFN1 launch of this precision's kernel from the committed rocprofv3 PMC
     summary (profiles/*pmc*ffn1*.json, newest round first), or None."""
-    for f in sorted(glob.glob(str(ROOT / "profiles" / "*pmc*ffn1*.json")), reverse=True):
+    import re
+
+    def order(f):  # r<round><letters>_...: r3z < r3aa < r3ap (round, then run letters)
+        m = re.match(r"r(\d+)([a-z]*)_", pathlib.Path(f).name)
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+    for f in sorted(glob.glob(str(ROOT / "profiles" / "*pmc*ffn1*.json")), key=order,
+                    reverse=True):
         try:
             d = json.load(open(f))
             if d.get("precision", "fp32") == precision:
@@ -186,15 +195,18 @@ def time_steps(eng, ids_dev, lens, out, steps, warmup, dev, dist, profile):
     return elapsed, kt
 
 
-def cpu_baseline(L, seconds, threads):
-    """The reference's CPU path on the scoring step: oracle/roberta_cpu.py (PyTorch-CPU fp32 eager
-    restatement of Model.get_results' forward) over [64, L] batches — the DataLoader batch of
-    model.py:40 — on `threads` torch threads; whole batches until `seconds` have passed."""
+def cpu_baseline(L, seconds, threads, impl="oracle"):
+    """The reference's CPU path on the scoring step over [64, L] batches — the DataLoader batch of
+    model.py:40 — on `threads` torch threads; whole batches until `seconds` have passed.
+    impl "oracle": oracle/roberta_cpu.py (PyTorch-CPU fp32 eager restatement of Model.get_results'
+    forward); "hf": the installed transformers RobertaForSequenceClassification (the library the
+    reference's Model.forward calls, model.py:25), built from a local config (eager attention,
+    fp32) with the same synthetic weights, called as the reference does:
+    sigmoid(model(ids, attention_mask=ids.ne(1))[0])."""
     import numpy as np
     import torch
 
     from apmc_amd.weights import synthetic_state_dict
-    from oracle import roberta_cpu as ora
 
     torch.set_num_threads(threads)
     sd = synthetic_state_dict(seed=0, head="sigmoid1")
@@ -202,13 +214,36 @@ def cpu_baseline(L, seconds, threads):
     B = 64
     ids = rng.integers(4, 50264, size=(B, L)).astype(np.int64)
     ids[:, 0], ids[:, -1] = 0, 2
-    ora.score(sd, ids[:2, :64], "sigmoid1")  # warm up allocator / threads
+    if impl == "hf":
+        from apmc_amd.weights import to_hf_state_dict
+        from transformers import RobertaConfig, RobertaForSequenceClassification
+
+        c = RobertaConfig(vocab_size=50265, hidden_size=768, num_hidden_layers=12,
+                          num_attention_heads=12, intermediate_size=3072,
+                          max_position_embeddings=514, type_vocab_size=1, pad_token_id=1,
+                          bos_token_id=0, eos_token_id=2, layer_norm_eps=1e-5, num_labels=1,
+                          hidden_act="gelu", hidden_dropout_prob=0.0,
+                          attention_probs_dropout_prob=0.0)
+        c._attn_implementation = "eager"
+        m = RobertaForSequenceClassification(c).eval()
+        m.load_state_dict(to_hf_state_dict(sd, "seqcls"), strict=False)
+
+        @torch.no_grad()
+        def run(x):
+            t = torch.from_numpy(x)
+            return torch.sigmoid(m(t, attention_mask=t.ne(1))[0]).numpy()
+    else:
+        from oracle import roberta_cpu as ora
+
+        def run(x):
+            return ora.score(sd, x, "sigmoid1")
+    run(ids[:2, :64])  # warm up allocator / threads
     done, t0 = 0, time.perf_counter()
     while True:
-        ora.score(sd, ids, "sigmoid1")
+        run(ids)
         done += B
         el = time.perf_counter() - t0
-        log(f"CPU baseline: {done} queries in {el:.1f} s ({threads} threads)")
+        log(f"CPU baseline ({impl}): {done} queries in {el:.1f} s ({threads} threads)")
         if el >= seconds:
             break
     return done / el, f"{done} queries of L={L} (batches of {B}, model.py:40) in {el:.1f} s"
@@ -564,6 +599,153 @@ def subs_leg(dev, seconds, rank, world, precision):
             "encoder_tflops": round(tot[4] / wall / 1e12, 2)}
 
 
+def devign_lengths():
+    """Sub-word lengths (CLS + tokens[:510] + SEP) of the 2,732 Devign test functions of the seven
+    fixture files — the varlen mix of SURVEY §8(d) is resampled from this distribution."""
+    from apmc_amd.host import Tokenizer
+
+    tok = Tokenizer()
+    codes = []
+    for f in sorted(glob.glob(str(ROOT / "data" / "devign" / "test_subs_*.jsonl"))):
+        codes += [json.loads(line)["func"] for line in open(f)]
+    _, lens = tok.featurize(codes, 512)
+    return lens
+
+
+def synthetic_gcb_batch(B, code_len=512, nodes=128, seed=0):
+    """SURVEY §8(d) GraphCodeBERT step input: L = code_len + nodes = 640 with every position used
+    (CLS + 510 code tokens + SEP, then `nodes` data-flow nodes, id <unk> at position 0), each node
+    spanning 1-3 code tokens and with 1-2 edges to other nodes (seed 0); the reference's mask
+    (utils.py:540-576, graph.graph_mask) bit-packed."""
+    import numpy as np
+
+    from apmc_amd.graph import graph_mask, pack_mask
+
+    rng = np.random.default_rng(seed)
+    L = code_len + nodes
+    ids = np.empty((B, L), np.int32)
+    pos = np.empty((B, L), np.int32)
+    bits = np.empty((B, L, L // 32), np.int32)
+    for b in range(B):
+        ids[b, 0], ids[b, code_len - 1] = 0, 2
+        ids[b, 1:code_len - 1] = rng.integers(4, 50264, code_len - 2)
+        ids[b, code_len:] = 3
+        pos[b, :code_len] = np.arange(2, code_len + 2)
+        pos[b, code_len:] = 0
+        starts = rng.integers(1, code_len - 4, nodes)
+        d2c = [(int(s), int(s + rng.integers(1, 4))) for s in starts]
+        d2d = [sorted({int(x) for x in rng.integers(0, nodes, rng.integers(1, 3))})
+               for _ in range(nodes)]
+        bits[b] = pack_mask(graph_mask(ids[b], pos[b], d2c, d2d, L))
+    return ids, pos, bits
+
+
+def microbench_leg(dev, precision, steps, warmup, world):
+    """SURVEY §8(d)'s scoring microbenchmarks beside the headline shape, on the same synthetic
+    victim and precision: batch 1024 x 512 (several examples' populations in flight), the
+    Devign varlen mix (B = 64, lengths resampled from the fixture distribution, pads skipped),
+    and the GraphCodeBERT step (B = 64 x L = 640 with the data-flow mask, node averaging,
+    explicit positions).  Each: HIP-event-free wall time of `steps` batches bracketed by device
+    syncs, victim queries/s, algorithmic TFLOP/s of F(L) per row and its fraction
+    of the arithmetic's ceiling."""
+    import numpy as np
+    import torch
+
+    from apmc_amd.engine import Engine
+    from apmc_amd.weights import synthetic_state_dict
+
+    peak = {"fp32": FP32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS,
+            "f32x3": BF16_MFMA_PEAK_TFLOPS / 3}[precision]
+    eng = Engine(synthetic_state_dict(seed=0, head="sigmoid1"), head="sigmoid1", num_labels=1,
+                 precision=precision, device=dev.index)
+    out = {}
+
+    def timed(fn, n_steps, kind=None):
+        for _ in range(warmup):
+            fn()
+        torch.cuda.synchronize(dev)
+        if kind:
+            eng.kernel_time()
+            eng.set_profiling(kind, True)
+        t0 = time.perf_counter()
+        for _ in range(n_steps):
+            fn()
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        kt = None
+        if kind:
+            eng.set_profiling(kind, False)
+            kt = eng.kernel_time()
+        return el, kt
+
+    def summary(rows_flop, rows, el, n_steps, what):
+        tf = rows_flop * n_steps / el / 1e12
+        return {"workload": what, "steps": n_steps, "ms_per_step": round(1e3 * el / n_steps, 3),
+                "victim_queries_per_s": round(rows * n_steps / el, 1),
+                "algorithmic_tflops": round(tf, 2), "frac_of_peak": round(tf / peak, 4),
+                "peak_tflops": peak}
+
+    rng = np.random.default_rng(0)
+    # (1) batch 1024 x 512
+    B, L = 1024, 512
+    ids = rng.integers(4, 50264, size=(B, L)).astype(np.int32)
+    ids[:, 0], ids[:, -1] = 0, 2
+    ids_d = torch.from_numpy(ids).to(dev)
+    lens = np.full((B,), L, np.int32)
+    o = torch.empty((B, 1), dtype=torch.float32, device=dev)
+    n1 = max(3, steps // 4)
+    el, _ = timed(lambda: eng.score(ids_d, lens, out=o), n1)
+    out["batch1024"] = summary(flops_per_query(L) * B, B, el, n1,
+                               "B = 1024 x L = 512 uniform ids (16 GA populations in flight)")
+    log(f"microbench batch 1024: {out['batch1024']['victim_queries_per_s']} q/s")
+    # (2) Devign varlen mix: 8 batches of 64 resampled lengths, cycled
+    dl = devign_lengths()
+    batches = []
+    for _ in range(8):
+        ln = rng.choice(dl, 64).astype(np.int32)
+        x = np.full((64, 512), 1, np.int32)
+        for i, n in enumerate(ln):
+            x[i, 0], x[i, n - 1] = 0, 2
+            x[i, 1:n - 1] = rng.integers(4, 50264, n - 2)
+        batches.append((torch.from_numpy(x).to(dev), ln))
+    ov = torch.empty((64, 1), dtype=torch.float32, device=dev)
+    it = iter(range(1 << 30))
+    el, _ = timed(lambda: eng.score(*batches[next(it) % 8], out=ov), steps)
+    flop = np.mean([sum(flops_per_query(int(n)) for n in ln) for _, ln in batches])
+    tok = np.mean([int(ln.sum()) for _, ln in batches])
+    out["varlen"] = dict(summary(flop, 64, el, steps,
+                                 "B = 64, lengths resampled (seed 0) from the 2,732 Devign test "
+                                 "functions' sub-word lengths (truncated at 512), pads skipped"),
+                         mean_tokens_per_row=round(tok / 64, 1),
+                         fixture_median_len=int(np.median(dl)),
+                         fixture_frac_over_400=round(float((dl > 400).mean()), 3))
+    log(f"microbench varlen: {out['varlen']['victim_queries_per_s']} q/s")
+    # (3) GraphCodeBERT L = 640 with the data-flow mask
+    gi, gp, gb = synthetic_gcb_batch(64)
+    gi_d, gp_d, gb_d = (torch.from_numpy(a).to(dev) for a in (gi, gp, gb))
+    glens = np.full((64,), 640, np.int32)
+    el, (a_ms, a_n, _) = timed(lambda: eng.score_graph(gi_d, glens, gp_d, gb_d, out=ov), steps,
+                               kind="attention")
+    res = summary(flops_per_query(640) * 64, 64, el, steps,
+                  "GraphCodeBERT step: B = 64 x L = 640 (512 code + 128 data-flow nodes, 1-3 code "
+                  "tokens and 1-2 edges per node, seed 0), bit-packed mask, node averaging")
+    # attention of the 11 full-length masked layers (4·L²·64 per (sequence, head)) over the time
+    # of every attention launch of the step (the CLS-only last layer's included: conservative)
+    per_layer_flop = 4.0 * 640 * 640 * 64 * 12 * 64
+    if a_n:
+        attn_ms = a_ms / steps
+        res["attention"] = {"ms_per_step": round(attn_ms, 4), "launches_per_step": a_n // steps,
+                            "full_layer_algorithmic_gflop": round(per_layer_flop / 1e9, 2),
+                            "algorithmic_tflops": round(11 * per_layer_flop / attn_ms / 1e9, 2),
+                            "frac_of_peak": round(11 * per_layer_flop / attn_ms / 1e9 / peak, 4),
+                            "timing": "HIP events on the engine stream around every attention "
+                                      "launch (11 masked full layers + the CLS-only last layer)"}
+    out["gcb640"] = res
+    log(f"microbench gcb640: {res['victim_queries_per_s']} q/s")
+    eng.close()
+    return out
+
+
 # ------------------------------------------------------------------------------------------ main
 def main():
     args = parse_args()
@@ -752,17 +934,28 @@ def main():
         for t in sweep:
             log(f"CPU baseline ({t} threads)")
             v, sample = cpu_baseline(L, args.cpu_seconds, t)
-            points.append({"cores": t, "value": round(v, 4), "sample": sample})
+            points.append({"cores": t, "value": round(v, 4), "sample": sample,
+                           "path": "oracle/roberta_cpu.py fp32 eager"})
+        best = max(points, key=lambda q: q["value"])
+        try:  # the transformers forward the reference itself calls, at the best thread count
+            v, sample = cpu_baseline(L, args.cpu_seconds, best["cores"], impl="hf")
+            points.append({"cores": best["cores"], "value": round(v, 4), "sample": sample,
+                           "path": "transformers RobertaForSequenceClassification eager fp32"})
+        except ImportError as e:
+            log(f"transformers not importable: {e}")
         best = max(points, key=lambda q: q["value"])
         threads = best["cores"]
         _torch.set_num_threads(host_threads)
         res["cpu_baseline"] = {"value": best["value"], "unit": "victim queries/s",
                                "cores": best["cores"], "kind": "port",
-                               "sample": best["sample"] + f", oracle/roberta_cpu.py fp32 eager, "
-                                                          f"torch threads={best['cores']} (the "
-                                                          "fastest point of the sweep)",
+                               "sample": best["sample"] + f", {best['path']}, torch "
+                                                          f"threads={best['cores']} (the fastest "
+                                                          "point of the sweep)",
                                "thread_sweep": points, **cpu_facts}
         res["speedup_vs_cpu"] = round(value / best["value"], 2)
+    if not args.no_microbench:
+        log("microbenchmarks (batch 1024, varlen, GCB 640)")
+        res["microbench"] = microbench_leg(dev, args.precision, args.steps, args.warmup, world)
     if args.attack_examples > 0:
         log("config-2 attack leg")
         res["attack"] = attack_leg(dev, args.attack_examples, args.attack_deadline,

@@ -199,6 +199,9 @@ int ae_kernel_time(ae_engine *eng, double *ms_total, int64_t *launches, double *
 
 const char *ae_last_error(void);
 const char *ae_version(void);
+/* Hash of the sources this library was built from (attack-pretrain-models-of-code_amd/
+ * buildinfo.py); the Python loader refuses a library whose hash differs from its tree. */
+const char *ae_source_hash(void);
 
 #ifdef __cplusplus
 }

@@ -146,6 +146,9 @@ int32_t ah_gcb_features_batch(ah_tokenizer *tok, int32_t n, const char *const *c
                               int32_t *spans_out, int32_t *edges_out);
 
 const char *ah_last_error(void);
+/* Hash of the sources this library was built from (attack-pretrain-models-of-code_amd/
+ * buildinfo.py); the Python loader refuses a library whose hash differs from its tree. */
+const char *ah_source_hash(void);
 
 #ifdef __cplusplus
 }

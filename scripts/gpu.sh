@@ -3,7 +3,8 @@
 # Steps run in order; the first failing step ends the call (no retries).  Everything lands under
 # gpurun_out/TAG/.
 #   rebuild   make clean + __graft_entry__.build() on the box (proves the tree builds from source)
-#   tests     pytest -m gpu            (K=<-k filter>, MAXFAIL=<n>, default -x)
+#   tests     pytest -m gpu            (K=<-k filter>, MAXFAIL=<n>, default -x; KEEPGOING=1: go on
+#             to the next step after test failures, never after a crash / abort / time limit)
 #   smoke     __graft_entry__.smoke()
 #   bench     python bench.py $BENCH_FULL_ARGS        (the default run: every leg)
 #   short     scoring-only bench, 20 steps             ($BENCH_ARGS appended)
@@ -30,7 +31,11 @@ for S in "$@"; do
   case $S in
     rebuild) run rebuild 600 bash -c 'make clean && python -c "import __graft_entry__ as g; g.build()" && ls -l attack-pretrain-models-of-code_amd/lib' || exit $? ;;
     tests) XF="-x"; [ -n "$MAXFAIL" ] && XF="--maxfail=$MAXFAIL"
-           run pytest_gpu 1100 python -u -m pytest ${TESTS:-tests} -m gpu $XF -v --timeout 300 --timeout-method thread ${K:+-k "$K"} || exit $? ;;
+           run pytest_gpu 1100 python -u -m pytest ${TESTS:-tests} -m gpu $XF -v --timeout 300 --timeout-method thread ${PYTEST_EXTRA:-} ${K:+-k "$K"}
+           rc=$?
+           # KEEPGOING=1: test FAILURES (pytest rc 1) do not end the call; a crash, abort or
+           # time limit (any other non-zero rc) still does
+           if [ $rc -ne 0 ] && ! { [ "${KEEPGOING:-0}" = 1 ] && [ $rc -eq 1 ]; }; then exit $rc; fi ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench) run bench 1000 python -u bench.py ${BENCH_FULL_ARGS:-} || exit $? ;;
     short) run short 400 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --attack-examples 0 --subs-seconds 0 --mhm-examples 0 --aa-examples 0 --clone-examples 0 --no-config1 ${BENCH_ARGS:-} || exit $? ;;

@@ -38,3 +38,18 @@ def test_library_has_gfx950_code_object():
     from apmc_amd import LIB_PATH
     data = LIB_PATH.read_bytes()
     assert b"gfx950" in data
+
+
+def test_libraries_built_from_this_tree():
+    """Both libraries embed the hash of the sources they were built from (buildinfo.py); the
+    loaders refuse a library left over from other sources, so the tests and the bench can only
+    run binaries built from exactly this tree."""
+    from apmc_amd import HOSTLIB_PATH, LIB_PATH
+    from apmc_amd.buildinfo import source_hash
+    import torch  # noqa: F401
+    eng = ctypes.CDLL(str(LIB_PATH))
+    eng.ae_source_hash.restype = ctypes.c_char_p
+    assert eng.ae_source_hash().decode() == source_hash("engine")
+    host = ctypes.CDLL(str(HOSTLIB_PATH))
+    host.ah_source_hash.restype = ctypes.c_char_p
+    assert host.ah_source_hash().decode() == source_hash("host")

@@ -564,6 +564,12 @@ def _mhm_victim(task):
     if base == "devign":
         codes, subs, _ = load_fixture(FIXTURE, 0, 120)
         pick = _pick(codes, subs, MHM_PROGRAMS)
+    elif task == "gcb_clone":
+        # the GraphCodeBERT clone copy skips no known name, so two variable names can merge and
+        # its chain raise KeyError (the reference's own failure, reproduced); the pairs with the
+        # fewest substitutable names chain longest without one
+        codes, subs, _ = fixture(base, 40)
+        pick = sorted(range(40), key=lambda i: (len(subs[i]), i))[:MHM_PROGRAMS]
     else:
         codes, subs, _ = fixture(base, MHM_PROGRAMS)
         pick = list(range(MHM_PROGRAMS))

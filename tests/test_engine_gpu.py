@@ -296,7 +296,7 @@ def test_cls_absorbed_attention_matches_full_path(gpu, monkeypatch, precision, t
         engines[mode] = Engine(sd, head="softmaxN", num_labels=66, precision=precision)
     rng = np.random.default_rng(40)
     L = 640
-    lens = np.array([640, 1, 2, 17, 63, 64, 65, 130, 511, 512, 333, 600], np.int32)
+    lens = np.array([640, 2, 3, 17, 63, 64, 65, 130, 511, 512, 333, 600], np.int32)
     ids = _rand_ids(rng, len(lens), L, lens)
     a, b = _score(engines["1"], ids), _score(engines["0"], ids)
     np.testing.assert_allclose(a, b, atol=tol, rtol=0)

@@ -294,8 +294,9 @@ def test_cosine_substitutes_f32x3_match_fp32(gpu):
             assert set(t3["topk_ids"][r].tolist()) == top == set(t32["topk_ids"][r].tolist()), r
             n_rows += 1
         for (w3, p3, s3, c3), (w32, p32, s32, c32) in zip(t3["sims"], t32["sims"]):
-            if c3 == c32:
-                eps_sim = max(eps_sim, float(np.abs(np.asarray(s3) - np.asarray(s32)).max()))
+            d3, d32 = dict(zip(c3, s3)), dict(zip(c32, s32))
+            if set(d3) == set(d32):  # the same 60 candidates (their ORDER follows the logits)
+                eps_sim = max(eps_sim, max(abs(d3[c] - d32[c]) for c in d32))
     tie_sim = 2 * eps_sim + 1e-7
     compared = excused = long_compared = 0
     for k, (code_tokens, names, logits, t32, t3, got32, got3) in enumerate(runs):
@@ -312,7 +313,9 @@ def test_cosine_substitutes_f32x3_match_fp32(gpu):
             if span & tied or (multi and span & tied4):
                 bad.add(w3)
                 continue
-            assert c3 == c32, (w3, p3)  # the same 60 candidates, in the same order
+            # the same 60 candidates (in the order of their logits, which may swap near-equal
+            # neighbours: only the cosine ranking below decides what survives)
+            assert set(c3) == set(c32), (w3, p3)
             s = np.sort(np.asarray(s32, np.float64))[::-1]
             if s[29] - s[30] < tie_sim or (multi and s[3] - s[4] < tie_sim):
                 bad.add(w3)
