@@ -41,6 +41,10 @@ hipError_t ae_launch_gemm_packed_ln(const unsigned short*, const unsigned short*
                                     const float*, float*, unsigned short*, int, int, int, int,
                                     const float*, const float*, float, uint64_t*, int*, int*,
                                     hipStream_t);
+hipError_t ae_launch_gemm_packed_ln_fix(const unsigned short*, const unsigned short*,
+                                        const float*, const float*, float*, float*,
+                                        unsigned short*, int, int, int, int, const float*,
+                                        const float*, float, uint64_t*, int*, hipStream_t);
 hipError_t ae_launch_compact(const int*, const int*, const int*, int, int, int, int, int*, int*,
                              int*, int*, hipStream_t);
 hipError_t ae_launch_embed_ln(const int*, const int*, const float*, const float*, const float*,
@@ -125,6 +129,11 @@ struct ae_engine {
   // u = W_k^T q and p-weighted row sums [n][12][768], per-64-key-chunk partial records
   // (AE_CLS_ABSORB=0 at engine creation: the full-T QKV GEMM + one-query attention instead)
   bool cls_absorb = true;
+  // residual + LayerNorm inside the O-projection / FFN2 GEMM by the row block's last-arriving
+  // tile (gemm_planes.hip LnArgs mode 5) on both encoder forms (AE_LN_FIX=0 at engine creation:
+  // the two-stream form's separate LayerNorm kernel and the single-stream form's co-resident
+  // exchange, mode 0)
+  bool ln_fix = true;
   float *cls_u = nullptr, *cls_y = nullptr, *cls_part = nullptr;
   size_t cap_cls_part = 0;
   int *tok_ids = nullptr, *tok_pos = nullptr, *src_col = nullptr, *cu = nullptr, *one = nullptr;
@@ -271,8 +280,10 @@ int ensure_workspace(ae_engine* e, size_t T, size_t n) {
       if ((rc = dev_alloc(e, (void**)&e->hp, nt * F * 2 * e->np))) return rc;
       const size_t blocks = (nt + 255) / 256;
       if ((rc = dev_alloc(e, (void**)&e->lnst, blocks * 256 * 4 * 8))) return rc;
-      if ((rc = dev_alloc(e, (void**)&e->lnctr, 2 * blocks * 4))) return rc;
-      HIPC(hipMemset(e->lnctr, 0, 2 * blocks * 4));
+      // counters per 256-row block; a part of the two-stream encoder offsets its own by
+      // (t0 >> 8) + part, so (T >> 8) + parts + 1 slots suffice
+      if ((rc = dev_alloc(e, (void**)&e->lnctr, (2 * blocks + 8) * 4))) return rc;
+      HIPC(hipMemset(e->lnctr, 0, (2 * blocks + 8) * 4));
     }
     e->cap_T = nt;
   }
@@ -396,6 +407,20 @@ int gemm_pk_ln(ae_engine* e, const unsigned short* A, const unsigned short* Wp, 
   return AE_OK;
 }
 
+// The same over the rows [t0, t0 + M) of part `part` with the last-arriver LayerNorm (mode 5):
+// the pre-LayerNorm rows go to tmp, x and its planes receive the LayerNorm output.
+int gemm_pk_lnfix(ae_engine* e, const unsigned short* A, const unsigned short* Wp,
+                  const float* bias, const float* g, const float* b, int64_t t0, int M, int K,
+                  int part, hipStream_t st) {
+  const int H = e->cfg.hidden;
+  Prof p(e, st, e->prof_kind == AE_KIND_GEMM_ANY, 2.0 * M * H * K);
+  float* x = e->x + t0 * H;
+  HIPC(ae_launch_gemm_packed_ln_fix(A, Wp, bias, x, e->tmp + t0 * H, x, e->xp + t0 * H * e->np,
+                                    M, H, K, e->np, g, b, e->cfg.ln_eps, e->lnst + t0 * 4,
+                                    e->lnctr + (t0 >> 8) + part, st));
+  return AE_OK;
+}
+
 // attention over packed planes: the production loop, or an experiment variant (unmasked launches)
 hipError_t attention_pp(ae_engine* e, const unsigned short* qkvp, float* out, unsigned short* op,
                         const int* cu, const int* q_rows, int max_q, int n, int heads,
@@ -411,7 +436,7 @@ hipError_t attention_pp(ae_engine* e, const unsigned short* qkvp, float* out, un
 // two-stream encoder; results equal the fused path's to LayerNorm rounding).
 int layer_rows(ae_engine* e, const LayerW& w, int64_t t0, int M, int s0, int ns, int max_len,
                const uint32_t* mask_bits, int L, hipStream_t st, hipEvent_t mark = nullptr,
-               int mark_after = 1) {
+               int mark_after = 1, int part = 0) {
   const int H = e->cfg.hidden, F = e->cfg.ffn, np = e->np;
   unsigned short* qkvp = reinterpret_cast<unsigned short*>(e->qkv);
   unsigned short* xp = e->xp + t0 * H * np;
@@ -433,14 +458,23 @@ int layer_rows(ae_engine* e, const LayerW& w, int64_t t0, int M, int s0, int ns,
                       L, np, st));
   }
   if ((rc = done())) return rc;
-  if ((rc = gemm_pk(e, e->cp + t0 * H * np, w.wo_p, w.bo, x, tmp, nullptr, M, H, H,
-                    EPI_BIAS_RESIDUAL, st, false)) || (rc = done()))
-    return rc;
-  HIPC(ae_launch_layernorm(tmp, w.ln1g, w.ln1b, e->cfg.ln_eps, M, x, xp, np, st));
-  if ((rc = done())) return rc;
+  if (e->ln_fix) {
+    if ((rc = gemm_pk_lnfix(e, e->cp + t0 * H * np, w.wo_p, w.bo, w.ln1g, w.ln1b, t0, M, H, part,
+                            st)) || (rc = done()))
+      return rc;
+  } else {
+    if ((rc = gemm_pk(e, e->cp + t0 * H * np, w.wo_p, w.bo, x, tmp, nullptr, M, H, H,
+                      EPI_BIAS_RESIDUAL, st, false)) || (rc = done()))
+      return rc;
+    HIPC(ae_launch_layernorm(tmp, w.ln1g, w.ln1b, e->cfg.ln_eps, M, x, xp, np, st));
+    if ((rc = done())) return rc;
+  }
   if ((rc = gemm_pk(e, xp, w.w1_p, w.b1, nullptr, nullptr, e->hp + t0 * F * np, M, F, H,
                     EPI_BIAS_GELU, st, true)) || (rc = done()))
     return rc;
+  if (e->ln_fix)
+    return gemm_pk_lnfix(e, e->hp + t0 * F * np, w.w2_p, w.b2, w.ln2g, w.ln2b, t0, M, F, part,
+                         st);
   if ((rc = gemm_pk(e, e->hp + t0 * F * np, w.w2_p, w.b2, x, tmp, nullptr, M, H, F,
                     EPI_BIAS_RESIDUAL, st, false)) || (rc = done()))
     return rc;
@@ -490,7 +524,7 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
         int rc;
         if ((rc = layer_rows(e, w, t0, M, s_beg[p], s_beg[p + 1] - s_beg[p], ml[p], mask_bits, L,
                              stream_of(p), li == 0 && p + 1 < P ? e->ev_lag[p] : nullptr,
-                             e->split_lag)))
+                             e->split_lag, p)))
           return rc;
       }
     }
@@ -541,11 +575,17 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
     }
     if (!last_cls && pl) {
       // O-proj + residual + LN1 and FFN2 + residual + LN2 each one kernel (x updated in place)
-      if ((rc = gemm_pk_ln(e, e->cp, w.wo_p, w.bo, w.ln1g, w.ln1b, (int)T, H, st))) return rc;
+      if ((rc = e->ln_fix ? gemm_pk_lnfix(e, e->cp, w.wo_p, w.bo, w.ln1g, w.ln1b, 0, (int)T, H,
+                                          0, st)
+                          : gemm_pk_ln(e, e->cp, w.wo_p, w.bo, w.ln1g, w.ln1b, (int)T, H, st)))
+        return rc;
       if ((rc = gemm_pk(e, e->xp, w.w1_p, w.b1, nullptr, nullptr, e->hp, (int)T, F, H,
                         EPI_BIAS_GELU, st, true)))
         return rc;
-      if ((rc = gemm_pk_ln(e, e->hp, w.w2_p, w.b2, w.ln2g, w.ln2b, (int)T, F, st))) return rc;
+      if ((rc = e->ln_fix ? gemm_pk_lnfix(e, e->hp, w.w2_p, w.b2, w.ln2g, w.ln2b, 0, (int)T, F,
+                                          0, st)
+                          : gemm_pk_ln(e, e->hp, w.w2_p, w.b2, w.ln2g, w.ln2b, (int)T, F, st)))
+        return rc;
     } else if (!last_cls) {
       if ((rc = gemm(e, e->ctx, w.wo, w.wo_h, w.wo_l, w.bo, e->x, e->tmp, (int)T, H, H, EPI_BIAS_RESIDUAL,
                      st, false)))
@@ -739,6 +779,8 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
   {
     const char* ca = std::getenv("AE_CLS_ABSORB");  // A/B runs: 0 = full-T QKV + attention
     e->cls_absorb = !(ca && ca[0] == '0');
+    const char* lf = std::getenv("AE_LN_FIX");  // A/B runs: 0 = separate LN / co-resident exchange
+    e->ln_fix = !(lf && lf[0] == '0');
   }
   if (e->planes) {
     // on unless AE_SPLIT_STREAMS=0 (tools/split_ab.py, profiles/r3s_split_streams_ab.json:

@@ -315,3 +315,26 @@ def test_long_rows_batch_invariant_bitwise(gpu, precision):
     big = _score(eng, ids)
     small = _score(eng, ids[:5])
     assert np.array_equal(big[:5], small), np.abs(big[:5] - small).max()
+
+
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_last_arriver_layernorm_matches_unfused(gpu, monkeypatch, split):
+    """Residual + LayerNorm inside the O-projection / FFN2 GEMM by each row block's last-arriving
+    tile (LnArgs mode 5, the default of both encoder forms) against AE_LN_FIX=0 (the two-stream
+    form's separate LayerNorm kernel, the single-stream form's co-resident exchange): ragged
+    lengths across 256-row blocks and the parts' boundaries; LayerNorm rounding only."""
+    from apmc_amd.engine import Engine
+    sd = synthetic_sd(6, "softmaxN", 5)
+    monkeypatch.setenv("AE_SPLIT_STREAMS", split)
+    engines = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("AE_LN_FIX", mode)
+        engines[mode] = Engine(sd, head="softmaxN", num_labels=5, precision="f32x3")
+    rng = np.random.default_rng(50)
+    for n, L in ((64, 384), (5, 300), (1, 77)):
+        ids = _rand_ids(rng, n, L, rng.integers(3, L + 1, n))
+        a, b = _score(engines["1"], ids), _score(engines["0"], ids)
+        np.testing.assert_allclose(a, b, atol=2e-5, rtol=0)
+        assert np.array_equal(a, _score(engines["1"], ids))  # counters re-armed: same bits again
+    for e in engines.values():
+        e.close()
