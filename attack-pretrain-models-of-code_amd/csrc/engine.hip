@@ -37,6 +37,9 @@ hipError_t ae_launch_attention_x3(const float*, float*, unsigned short*, const i
 hipError_t ae_launch_gemm_packed(const unsigned short*, const unsigned short*, const float*,
                                  const float*, float*, unsigned short*, int, int, int, int, int,
                                  hipStream_t);
+hipError_t ae_launch_gemm_packed_qkv192(const unsigned short*, const unsigned short*, const float*,
+                                        const float*, float*, unsigned short*, int, int, int, int,
+                                        int, hipStream_t);
 hipError_t ae_launch_gemm_packed_ln(const unsigned short*, const unsigned short*, const float*,
                                     const float*, float*, unsigned short*, int, int, int, int,
                                     const float*, const float*, float, uint64_t*, int*, int*,
@@ -134,6 +137,9 @@ struct ae_engine {
   // the two-stream form's separate LayerNorm kernel and the single-stream form's co-resident
   // exchange, mode 0)
   bool ln_fix = true;
+  // the QKV GEMM may run on 256 x 192 tiles (its packed-plane epilogue) where that finishes in
+  // fewer tile rounds (AE_QKV192=1 at engine creation)
+  bool qkv192 = false;
   float *cls_u = nullptr, *cls_y = nullptr, *cls_part = nullptr;
   size_t cap_cls_part = 0;
   int *tok_ids = nullptr, *tok_pos = nullptr, *src_col = nullptr, *cu = nullptr, *one = nullptr;
@@ -392,7 +398,10 @@ int gemm_pk(ae_engine* e, const unsigned short* A, const unsigned short* Wp, con
             hipStream_t st, bool is_ffn1) {
   const bool prof = (e->prof_kind == AE_KIND_GEMM_ANY) || (e->prof_kind == AE_KIND_GEMM_FFN1 && is_ffn1);
   Prof p(e, st, prof, 2.0 * M * N * K);
-  HIPC(ae_launch_gemm_packed(A, Wp, bias, R, C, Cp, M, N, K, epi, e->np, st));
+  if (e->qkv192 && Cp && !is_ffn1)  // the QKV GEMM (packed output, not FFN1)
+    HIPC(ae_launch_gemm_packed_qkv192(A, Wp, bias, R, C, Cp, M, N, K, epi, e->np, st));
+  else
+    HIPC(ae_launch_gemm_packed(A, Wp, bias, R, C, Cp, M, N, K, epi, e->np, st));
   return AE_OK;
 }
 
@@ -781,6 +790,8 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
     e->cls_absorb = !(ca && ca[0] == '0');
     const char* lf = std::getenv("AE_LN_FIX");  // A/B runs: 0 = separate LN / co-resident exchange
     e->ln_fix = !(lf && lf[0] == '0');
+    const char* q192 = std::getenv("AE_QKV192");  // A/B runs: 1 = 256 x 192 QKV tiles allowed
+    e->qkv192 = q192 && q192[0] == '1';
   }
   if (e->planes) {
     // on unless AE_SPLIT_STREAMS=0 (tools/split_ab.py, profiles/r3s_split_streams_ab.json:

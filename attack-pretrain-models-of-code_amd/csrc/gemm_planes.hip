@@ -869,7 +869,9 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0 && ln.mode != 1) {
-      __hip_atomic_fetch_add(ln.arrive + tm0, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // release / acquire at agent scope around the exchange (the workgroup's statistics stores
+      // are ordered before the arrival, the partners' after the wait), as mode 5's hand-off
+      __hip_atomic_fetch_add(ln.arrive + tm0, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       // bounded wait (~1 s): a partner that never arrives flags the engine instead of hanging
       int ok = 0;
       for (int spin = 0; spin < (1 << 20); ++spin) {
@@ -879,6 +881,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
         }
         __builtin_amdgcn_s_sleep(2);
       }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       if (!ok) __hip_atomic_store(ln.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
@@ -979,6 +982,59 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
           }
           unsigned short* dst = reinterpret_cast<unsigned short*>(ln.xp) + (size_t)prow0 * NP * N +
                                 (uint32_t)(lr + tm * 32) * (uint32_t)(NP * N) +
+                                (uint32_t)((col >> 5) * 32 * NP + (col & 31));
+          *reinterpret_cast<uint4*>(dst) = uint4{h[0], h[1], h[2], h[3]};
+          if (NP == 2) *reinterpret_cast<uint4*>(dst + 32) = uint4{l[0], l[1], l[2], l[3]};
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    return;
+  }
+
+  if constexpr (EPI == PK_EPI_BIAS_PACKED) {
+    // ---- +bias -> packed planes (the QKV GEMM of the half-batch streams: N = 2304 = 12 x 192
+    // tiles = 3 full rounds of 256 CUs where 256-wide tiles take 2.25).  C is the packed output
+    // [M][NP * N] here.  Per 32-row pass the wave's 32 x 96 block (+ bias) goes to its LDS region
+    // (400-B rows), then every lane takes 8 consecutive columns of a row: one 16-B store per
+    // plane (the mode-0 LayerNorm store pattern without the f32 copy).  Requires N % 192 == 0.
+    constexpr int RS = 400;
+    unsigned char* reg = pk_smem + wave * 32 * RS;
+    const int cb0 = n0 + sn * 96;
+    const int prow0 = m0 + wm * 128 + sm * 64;
+    unsigned short* const cp = reinterpret_cast<unsigned short*>(C);
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm) {
+#pragma unroll
+      for (int tn = 0; tn < 3; ++tn)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const floatx4 bv = *reinterpret_cast<const floatx4*>(bias + cb0 + tn * 32 + 8 * j + 4 * lh);
+          floatx4 v;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = acc[tm][tn][4 * j + i] + bv[i];
+          *reinterpret_cast<floatx4*>(reg + li * RS + (tn * 8 + 2 * j + lh) * 16) = v;
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const int kk = k % 3, g = k / 3;
+        const int idx = kk * 64 + lane, lr = idx / 12 + 16 * g, c8 = idx % 12;
+        const int row = prow0 + tm * 32 + lr;
+        const floatx4 o0 = *reinterpret_cast<const floatx4*>(reg + lr * RS + c8 * 32);
+        const floatx4 o1 = *reinterpret_cast<const floatx4*>(reg + lr * RS + c8 * 32 + 16);
+        if (row < M) {
+          const int col = cb0 + 8 * c8;
+          uint32_t h[4], l[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float a = i < 2 ? o0[2 * i] : o1[2 * i - 4], b = i < 2 ? o0[2 * i + 1] : o1[2 * i - 3];
+            const uint32_t ha = f2bf(a), hb = f2bf(b);
+            h[i] = ha | (hb << 16);
+            l[i] = (uint32_t)f2bf(a - __builtin_bit_cast(float, ha << 16)) |
+                   ((uint32_t)f2bf(b - __builtin_bit_cast(float, hb << 16)) << 16);
+          }
+          unsigned short* dst = cp + (size_t)prow0 * NP * N + (uint32_t)(lr + tm * 32) * (uint32_t)(NP * N) +
                                 (uint32_t)((col >> 5) * 32 * NP + (col & 31));
           *reinterpret_cast<uint4*>(dst) = uint4{h[0], h[1], h[2], h[3]};
           if (NP == 2) *reinterpret_cast<uint4*>(dst + 32) = uint4{l[0], l[1], l[2], l[3]};
@@ -1105,11 +1161,17 @@ hipError_t pp192_launch(const __bf16* A, const __bf16* W, const float* bias, con
 
 // f32 epilogues only (bias, +residual, tanh); N % 32 == 0
 hipError_t pp192_dispatch(const unsigned short* A, const unsigned short* W, const float* bias,
-                          const float* R, float* C, int M, int N, int K, int epi, int np,
-                          int group_m, hipStream_t st, bool nt = false) {
+                          const float* R, float* C, unsigned short* Cp, int M, int N, int K,
+                          int epi, int np, int group_m, hipStream_t st, bool nt = false) {
   auto a = reinterpret_cast<const __bf16*>(A);
   auto w = reinterpret_cast<const __bf16*>(W);
-  if (epi == PK_EPI_GELU_PACKED || epi == PK_EPI_BIAS_PACKED) return hipErrorInvalidValue;
+  if (epi == PK_EPI_GELU_PACKED) return hipErrorInvalidValue;
+  if (epi == PK_EPI_BIAS_PACKED) {  // packed planes into Cp (passed as the kernel's C)
+    if (N % 192 != 0 || !Cp || nt) return hipErrorInvalidValue;
+    float* cp = reinterpret_cast<float*>(Cp);
+    if (np == 2) return pp192_launch<2, PK_EPI_BIAS_PACKED>(a, w, bias, R, cp, M, N, K, group_m, st);
+    return pp192_launch<1, PK_EPI_BIAS_PACKED>(a, w, bias, R, cp, M, N, K, group_m, st);
+  }
   if (nt) {  // timing variant (ae_bench_gemm_packed diag 8): non-temporal stores
     if (np != 2 || (epi != PK_EPI_RES && epi != PK_EPI_BIAS)) return hipErrorInvalidValue;
     if (epi == PK_EPI_BIAS) return pp192_launch<2, PK_EPI_BIAS, true>(a, w, bias, R, C, M, N, K, group_m, st);
@@ -1160,8 +1222,10 @@ int cu_count() {
 }
 
 // tile width of the ping-pong GEMM for an M x N output (see ae_launch_gemm_packed)
-int pp_choose(int M, int N, int epi) {
-  if (epi == PK_EPI_GELU_PACKED || epi == PK_EPI_BIAS_PACKED) return 256;
+// packed192: the 256 x 192 kernel may take the packed-plane (QKV) epilogue too
+int pp_choose(int M, int N, int epi, bool packed192 = false) {
+  if (epi == PK_EPI_GELU_PACKED) return 256;
+  if (epi == PK_EPI_BIAS_PACKED && (N % 192 != 0 || !packed192)) return 256;
   const long tm = (M + 255) / 256, cus = cu_count();
   const long r256 = (tm * ((N + 255) / 256) + cus - 1) / cus;
   const long r192 = (tm * ((N + 191) / 192) + cus - 1) / cus;
@@ -1182,7 +1246,21 @@ extern "C" hipError_t ae_launch_gemm_packed(const unsigned short* A, const unsig
   // finishes first by rounds of CU-count tiles x per-tile time (tools/gemm_bench.py: a 256 x 192
   // round takes 0.89 of a 256 x 256 round; the 192 kernel has f32 epilogues only)
   return pp_choose(M, N, epi) == 192
-             ? pp192_dispatch(A, W, bias, R, C, M, N, K, epi, np, PK_GROUP_M, st)
+             ? pp192_dispatch(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st)
+             : pp_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
+}
+
+// ae_launch_gemm_packed with the 256 x 192 kernel also eligible for the packed-plane epilogue
+// (N % 192 == 0; the same rounds rule picks the width).  The engine's QKV launches under
+// AE_QKV192=1.  Not part of include/alert_engine.h.
+extern "C" hipError_t ae_launch_gemm_packed_qkv192(const unsigned short* A, const unsigned short* W,
+                                                   const float* bias, const float* R, float* C,
+                                                   unsigned short* Cp, int M, int N, int K, int epi,
+                                                   int np, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  if (!pk_shape_ok(M, N, K, np)) return hipErrorInvalidValue;
+  return pp_choose(M, N, epi, true) == 192
+             ? pp192_dispatch(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st)
              : pp_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
 }
 
@@ -1268,7 +1346,7 @@ extern "C" hipError_t ae_bench_gemm_packed(const unsigned short* A, const unsign
     return hipErrorInvalidValue;
   if (bn == 0) bn = pp_choose(M, N, epi) == 192 ? 192 : 512;
   if (bn == 192)  // diag 8: non-temporal stores; 21-52: grouped order of diag - 20 M-tiles
-    return pp192_dispatch(A, W, bias, R, C, M, N, K, epi, np,
+    return pp192_dispatch(A, W, bias, R, C, Cp, M, N, K, epi, np,
                           diag >= 21 && diag <= 52 ? diag - 20 : PK_GROUP_M, st, diag == 8);
   if (bn == 512 && diag >= 21 && diag <= 52)  // production kernel, grouped order of diag - 20 M-tiles
     return pp_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, diag - 20, st);

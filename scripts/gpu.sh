@@ -50,7 +50,7 @@ for S in "$@"; do
         i=$((i+1))
       done ;;
     gemm) run gemm 400 python -u tools/gemm_bench.py --shapes ${S_:-ffn1,ffn2,qkv,oproj} --variants ${V:-0} --rounds ${ROUNDS:-7} || exit $? ;;
-    attn) run attn 300 python -u tools/attn_bench.py --variants ${AV:-pp1} --rounds ${ROUNDS:-7} || exit $? ;;
+    attn) run attn 300 python -u tools/attn_bench.py --variants ${AV:-pp1} --rounds ${ROUNDS:-7} ${ATTN_EXTRA:-} || exit $? ;;
     cmd) run cmd 900 bash -c "$CMD" || exit $? ;;
     *) echo "unknown step $S"; exit 2 ;;
   esac
