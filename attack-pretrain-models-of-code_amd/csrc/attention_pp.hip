@@ -115,11 +115,12 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && NP 
   // PIPE 66: PIPE 6 with saddr DMA (per-lane offsets computed once, tiles advanced on the scalar
   // unit) and the cross-half row max by v_permlane32_swap instead of an LDS permute.
   // PIPE 67: 66 with the tile max as a 3-level tree of v_max3 (depth 3 instead of a chain of 8).
-  static_assert(PIPE == 4 || PIPE == 6 || PIPE == 66 || PIPE == 67 || PIPE == 69 || PIPE == 70,
-                "loop variants 4, 6, 66, 67, 69, 70");
+  static_assert(PIPE == 4 || PIPE == 6 || PIPE == 66 || PIPE == 67 || PIPE == 69 || PIPE == 70 ||
+                    PIPE == 72,
+                "loop variants 4, 6, 66, 67, 69, 70, 72");
   constexpr int PB = PIPE >= 60 ? 6 : PIPE;
   constexpr bool FAST = PIPE >= 60;
-  constexpr bool TREE = PIPE == 67 || (PIPE == 69 || PIPE == 70);
+  constexpr bool TREE = PIPE == 67 || (PIPE >= 69 && PIPE <= 72);
   static_assert(!(HAS_MASK && PB == 6 && !FAST),
                 "PIPE 6 has no mask path (its loop keeps no ordinary global load, so its mask "
                 "launches run PIPE 4); PIPE 66 moves the mask words by LDS-DMA");
@@ -232,6 +233,48 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && NP 
       const __bf16 h = (__bf16)p;
       ph[r >> 3][r & 7] = h;
       pl[r >> 3][r & 7] = (__bf16)(p - (float)h);
+    }
+    return psum;
+  };
+  // PIPE 72: tile kt's exp / split and tile kt+1's S MFMAs in one hand-ordered stream — per
+  // 16-d step: that step's K fragments, its 3 MFMAs, then a quarter of the exp / split (4 of the
+  // lane's 16 scores) — so one wave feeds both pipes instead of relying on another wave's phase
+  auto exp_s_fused = [&](floatx16& s, float m_new, bf16x8 (&ph)[2], bf16x8 (&pl)[2],
+                         const unsigned char* stk, floatx16& sn) {
+    float psum = 0.f;
+    const unsigned char* kr = stk + li * P::RB;
+    // the swizzled chunk offsets from an opaque row index: recomputed per tile (2 VALU per read)
+    // rather than held in 8 loop-invariant registers
+    int kli = li;
+    asm volatile("" : "+v"(kli));
+    bf16x8 kh[2], kl[2];
+    auto kread = [&](int ks, int b) {
+      const int d0 = 16 * ks + 8 * lh;
+      kh[b] = *reinterpret_cast<const bf16x8*>(kr + kpos<NP>(kli, chunk_of<NP>(0, d0)) * 16);
+      if (TERMS == 3)
+        kl[b] = *reinterpret_cast<const bf16x8*>(kr + kpos<NP>(kli, chunk_of<NP>(1, d0)) * 16);
+    };
+    kread(0, 0);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int b = ks & 1;
+      if (ks + 1 < 4) kread(ks + 1, b ^ 1);
+      if (TERMS == 3) {
+        sn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl[b], qh[ks], ks == 0 ? floatx16{} : sn, 0, 0, 0);
+        sn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh[b], ql[ks], sn, 0, 0, 0);
+        sn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh[b], qh[ks], sn, 0, 0, 0);
+      } else {
+        sn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh[b], qh[ks], ks == 0 ? floatx16{} : sn, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 4 * ks; r < 4 * ks + 4; ++r) {
+        const float pr = __builtin_amdgcn_exp2f(s[r] - m_new);
+        psum += pr;
+        const __bf16 h = (__bf16)pr;
+        ph[r >> 3][r & 7] = h;
+        pl[r >> 3][r & 7] = (__bf16)(pr - (float)h);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
     return psum;
   };
@@ -435,24 +478,29 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && NP 
       // split from tile kt+1's S MFMAs and this tile's PV (in PIPE 67 the compiler sank the exp /
       // split past the rescale branch, leaving the 12 S MFMAs back to back and the VALU chained
       // into the PV MFMAs that consume it)
-      if ((PIPE == 69 || PIPE == 70) && grow) {
+      if ((PIPE >= 69 && PIPE <= 72) && grow) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
       }
       bf16x8 ph[2], pl[2];
       __builtin_amdgcn_sched_barrier(0);
-      const float psum = exp_split(s_cur, m_new, ph, pl);
-      s_mfma(lds + KS_NEXT, s_next);
-      __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+      float psum;
+      if constexpr (PIPE == 72) {
+        psum = exp_s_fused(s_cur, m_new, ph, pl, lds + KS_NEXT, s_next);
+      } else {
+        psum = exp_split(s_cur, m_new, ph, pl);
+        s_mfma(lds + KS_NEXT, s_next);
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
 #pragma unroll
-      for (int i = 0; i < 12; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+        for (int i = 0; i < 12; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
       l_run = l_run * alpha + psum;
       m_run = m_new;
-      if ((PIPE != 69 && PIPE != 70) && grow) {
+      if ((PIPE < 69 || PIPE > 72) && grow) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
       }
@@ -673,6 +721,7 @@ extern "C" hipError_t ae_bench_attention_pp(const unsigned short* qkvp, float* o
     case 67: return app_launch<67>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
     case 69: return app_launch<69>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
     case 70: return app_launch<70>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
+    case 72: return app_launch<72>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
     default: break;
   }
   return hipErrorInvalidValue;
