@@ -744,10 +744,13 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
       // relaxed ticket, an agent-scope acquire in the last arriver — correct for any placement
       // of the partners (the tile order keeps them on one XCD, which is only faster).  No
       // co-residency is needed, so it runs beside the other half-batch stream's kernels.
+      // rows past M publish nothing: the two-stream engine's parts share one statistics array,
+      // and part 1's first rows sit where part 0's padding rows would land
       if (sn == 0 && lh == 0) {
 #pragma unroll
         for (int tm = 0; tm < 2; ++tm)
-          ln.stats[(size_t)(rb0 + 32 * tm) * 4 + tn0] = __builtin_bit_cast(uint64_t, tile[tm]);
+          if (rb0 + 32 * tm < M)
+            ln.stats[(size_t)(rb0 + 32 * tm) * 4 + tn0] = __builtin_bit_cast(uint64_t, tile[tm]);
       }
 #pragma unroll
       for (int tm = 0; tm < 2; ++tm) {
@@ -862,9 +865,10 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
     if (sn == 0 && lh == 0) {
 #pragma unroll
       for (int tm = 0; tm < 2; ++tm)
-        __hip_atomic_store(ln.stats + ((size_t)(rb0 + 32 * tm) * 4 + tn0),
-                           __builtin_bit_cast(uint64_t, tile[tm]), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        if (rb0 + 32 * tm < M)
+          __hip_atomic_store(ln.stats + ((size_t)(rb0 + 32 * tm) * 4 + tn0),
+                             __builtin_bit_cast(uint64_t, tile[tm]), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
