@@ -126,17 +126,21 @@ struct ae_engine {
   // (gemm_planes.hip PK_EPI_RES_LN); the counters are zero between launches
   uint64_t* lnst = nullptr;
   int* lnctr = nullptr;
+  size_t ctr_stride = 0;  // ints per part region of lnctr
   bool planes = false;
   int np = 1;
   // last-layer CLS attention with W_k absorbed into the query (cls_attention.hip): per-sequence
   // u = W_k^T q and p-weighted row sums [n][12][768], per-64-key-chunk partial records
   // (AE_CLS_ABSORB=0 at engine creation: the full-T QKV GEMM + one-query attention instead)
   bool cls_absorb = true;
-  // residual + LayerNorm inside the O-projection / FFN2 GEMM by the row block's last-arriving
-  // tile (gemm_planes.hip LnArgs mode 5) on both encoder forms (AE_LN_FIX=0 at engine creation:
-  // the two-stream form's separate LayerNorm kernel and the single-stream form's co-resident
-  // exchange, mode 0)
-  bool ln_fix = true;
+  // where the residual + LayerNorm after the O-projection / FFN2 runs (AE_LN_FIX at engine
+  // creation):
+  //   2 (default) the co-resident exchange inside the GEMM (gemm_planes.hip LnArgs mode 0) on
+  //     both encoder forms — each part of the two-stream form with its own counters;
+  //   1 the row block's last-arriving tile normalises the block (mode 5);
+  //   0 the round-3 forms: a separate LayerNorm kernel on the two-stream form, mode 0 on the
+  //     single-stream one.
+  int ln_kind = 2;
   // the QKV GEMM may run on 256 x 192 tiles (its packed-plane epilogue) where that finishes in
   // fewer tile rounds (AE_QKV192=1 at engine creation)
   bool qkv192 = false;
@@ -286,10 +290,11 @@ int ensure_workspace(ae_engine* e, size_t T, size_t n) {
       if ((rc = dev_alloc(e, (void**)&e->hp, nt * F * 2 * e->np))) return rc;
       const size_t blocks = (nt + 255) / 256;
       if ((rc = dev_alloc(e, (void**)&e->lnst, blocks * 256 * 4 * 8))) return rc;
-      // counters per 256-row block; a part of the two-stream encoder offsets its own by
-      // (t0 >> 8) + part, so (T >> 8) + parts + 1 slots suffice
-      if ((rc = dev_alloc(e, (void**)&e->lnctr, (2 * blocks + 8) * 4))) return rc;
-      HIPC(hipMemset(e->lnctr, 0, (2 * blocks + 8) * 4));
+      // arrival / departure counters per 256-row block, one region per part of the two-stream
+      // encoder (parts run concurrently; each launch's counters start at its region)
+      e->ctr_stride = 2 * blocks + 8;
+      if ((rc = dev_alloc(e, (void**)&e->lnctr, ae_engine::kMaxParts * e->ctr_stride * 4))) return rc;
+      HIPC(hipMemset(e->lnctr, 0, ae_engine::kMaxParts * e->ctr_stride * 4));
     }
     e->cap_T = nt;
   }
@@ -405,14 +410,21 @@ int gemm_pk(ae_engine* e, const unsigned short* A, const unsigned short* Wp, con
   return AE_OK;
 }
 
-// The O-projection / FFN2 of the split-precision path with the layer's residual add and
-// LayerNorm fused into the epilogue: x = LN(A·W^T + bias + x), written as f32 and packed planes.
+// The O-projection / FFN2 of the split-precision path over the rows [t0, t0 + M) of part `part`
+// with the layer's residual add and LayerNorm fused into the epilogue by the co-resident exchange
+// (mode 0): x = LN(A·W^T + bias + x), written as f32 and packed planes.  The 4 tiles of a row
+// block are consecutive in one XCD's in-order dispatch, so beside another stream's kernels they
+// still become co-resident (at most one partial group per launch and XCD waits for a CU, and the
+// other kernels' workgroups finish on their own); the bounded wait flags err instead of hanging.
 int gemm_pk_ln(ae_engine* e, const unsigned short* A, const unsigned short* Wp, const float* bias,
-               const float* g, const float* b, int M, int K, hipStream_t st) {
+               const float* g, const float* b, int64_t t0, int M, int K, int part,
+               hipStream_t st) {
   const int H = e->cfg.hidden;
   Prof p(e, st, e->prof_kind == AE_KIND_GEMM_ANY, 2.0 * M * H * K);
-  HIPC(ae_launch_gemm_packed_ln(A, Wp, bias, e->x, e->x, e->xp, M, H, K, e->np, g, b,
-                                e->cfg.ln_eps, e->lnst, e->lnctr, e->err, st));
+  float* x = e->x + t0 * H;
+  HIPC(ae_launch_gemm_packed_ln(A, Wp, bias, x, x, e->xp + t0 * H * e->np, M, H, K, e->np, g, b,
+                                e->cfg.ln_eps, e->lnst + t0 * 4, e->lnctr + part * e->ctr_stride,
+                                e->err, st));
   return AE_OK;
 }
 
@@ -426,7 +438,7 @@ int gemm_pk_lnfix(ae_engine* e, const unsigned short* A, const unsigned short* W
   float* x = e->x + t0 * H;
   HIPC(ae_launch_gemm_packed_ln_fix(A, Wp, bias, x, e->tmp + t0 * H, x, e->xp + t0 * H * e->np,
                                     M, H, K, e->np, g, b, e->cfg.ln_eps, e->lnst + t0 * 4,
-                                    e->lnctr + (t0 >> 8) + part, st));
+                                    e->lnctr + part * e->ctr_stride, st));
   return AE_OK;
 }
 
@@ -467,9 +479,13 @@ int layer_rows(ae_engine* e, const LayerW& w, int64_t t0, int M, int s0, int ns,
                       L, np, st));
   }
   if ((rc = done())) return rc;
-  if (e->ln_fix) {
+  if (e->ln_kind == 1) {
     if ((rc = gemm_pk_lnfix(e, e->cp + t0 * H * np, w.wo_p, w.bo, w.ln1g, w.ln1b, t0, M, H, part,
                             st)) || (rc = done()))
+      return rc;
+  } else if (e->ln_kind == 2) {
+    if ((rc = gemm_pk_ln(e, e->cp + t0 * H * np, w.wo_p, w.bo, w.ln1g, w.ln1b, t0, M, H, part,
+                         st)) || (rc = done()))
       return rc;
   } else {
     if ((rc = gemm_pk(e, e->cp + t0 * H * np, w.wo_p, w.bo, x, tmp, nullptr, M, H, H,
@@ -481,9 +497,11 @@ int layer_rows(ae_engine* e, const LayerW& w, int64_t t0, int M, int s0, int ns,
   if ((rc = gemm_pk(e, xp, w.w1_p, w.b1, nullptr, nullptr, e->hp + t0 * F * np, M, F, H,
                     EPI_BIAS_GELU, st, true)) || (rc = done()))
     return rc;
-  if (e->ln_fix)
+  if (e->ln_kind == 1)
     return gemm_pk_lnfix(e, e->hp + t0 * F * np, w.w2_p, w.b2, w.ln2g, w.ln2b, t0, M, F, part,
                          st);
+  if (e->ln_kind == 2)
+    return gemm_pk_ln(e, e->hp + t0 * F * np, w.w2_p, w.b2, w.ln2g, w.ln2b, t0, M, F, part, st);
   if ((rc = gemm_pk(e, e->hp + t0 * F * np, w.w2_p, w.b2, x, tmp, nullptr, M, H, F,
                     EPI_BIAS_RESIDUAL, st, false)) || (rc = done()))
     return rc;
@@ -584,16 +602,18 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
     }
     if (!last_cls && pl) {
       // O-proj + residual + LN1 and FFN2 + residual + LN2 each one kernel (x updated in place)
-      if ((rc = e->ln_fix ? gemm_pk_lnfix(e, e->cp, w.wo_p, w.bo, w.ln1g, w.ln1b, 0, (int)T, H,
-                                          0, st)
-                          : gemm_pk_ln(e, e->cp, w.wo_p, w.bo, w.ln1g, w.ln1b, (int)T, H, st)))
+      if ((rc = e->ln_kind == 1 ? gemm_pk_lnfix(e, e->cp, w.wo_p, w.bo, w.ln1g, w.ln1b, 0, (int)T, H,
+                                                0, st)
+                                : gemm_pk_ln(e, e->cp, w.wo_p, w.bo, w.ln1g, w.ln1b, 0, (int)T, H,
+                                             0, st)))
         return rc;
       if ((rc = gemm_pk(e, e->xp, w.w1_p, w.b1, nullptr, nullptr, e->hp, (int)T, F, H,
                         EPI_BIAS_GELU, st, true)))
         return rc;
-      if ((rc = e->ln_fix ? gemm_pk_lnfix(e, e->hp, w.w2_p, w.b2, w.ln2g, w.ln2b, 0, (int)T, F,
-                                          0, st)
-                          : gemm_pk_ln(e, e->hp, w.w2_p, w.b2, w.ln2g, w.ln2b, (int)T, F, st)))
+      if ((rc = e->ln_kind == 1 ? gemm_pk_lnfix(e, e->hp, w.w2_p, w.b2, w.ln2g, w.ln2b, 0, (int)T, F,
+                                                0, st)
+                                : gemm_pk_ln(e, e->hp, w.w2_p, w.b2, w.ln2g, w.ln2b, 0, (int)T, F,
+                                             0, st)))
         return rc;
     } else if (!last_cls) {
       if ((rc = gemm(e, e->ctx, w.wo, w.wo_h, w.wo_l, w.bo, e->x, e->tmp, (int)T, H, H, EPI_BIAS_RESIDUAL,
@@ -788,8 +808,8 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
   {
     const char* ca = std::getenv("AE_CLS_ABSORB");  // A/B runs: 0 = full-T QKV + attention
     e->cls_absorb = !(ca && ca[0] == '0');
-    const char* lf = std::getenv("AE_LN_FIX");  // A/B runs: 0 = separate LN / co-resident exchange
-    e->ln_fix = !(lf && lf[0] == '0');
+    const char* lf = std::getenv("AE_LN_FIX");  // A/B runs: 0, 1, 2 (see ln_kind)
+    if (lf && lf[0] >= '0' && lf[0] <= '2') e->ln_kind = lf[0] - '0';
     const char* q192 = std::getenv("AE_QKV192");  // A/B runs: 1 = 256 x 192 QKV tiles allowed
     e->qkv192 = q192 && q192[0] == '1';
   }

@@ -378,11 +378,17 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
       const int lr = tt * 32 + li;  // row within the half
 #pragma unroll
       for (int tn = 0; tn < 2; ++tn) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        if constexpr (PACKED) {
+          // lane half lh holds columns 8 j + 4 lh .. + 3 (4 bf16 = 8 B per plane) of every j; a
+          // v_permlane32_swap per register pair (j, j + 1) hands each half the other's 8 B, so
+          // the low half writes whole 16-B chunks j = 0, 2 and the high half j = 1, 3: 16-B
+          // writes whose 16-lane groups hit 16 distinct chunk slots (8-B writes put 32 lanes on
+          // 16 slots: 2048 bank-conflict cycles per tile, profiles/r4g_pmc_lds.json)
           const floatx16& c = acc[2 * half + tt][tn];
-          const int cc = tn * 32 + 8 * j + 4 * lh;  // column within the wave's 64
-          if (PACKED) {
+          uint32_t hw[4][2], lw[4][2];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int cc = tn * 32 + 8 * j + 4 * lh;  // column within the wave's 64
             const int col = cb0 + cc < N ? cb0 + cc : N - 4;
             const floatx4 bv = *reinterpret_cast<const floatx4*>(bias + col);
             ushortx4 h, l;
@@ -394,16 +400,39 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
               h[i] = __builtin_bit_cast(unsigned short, hv);
               l[i] = f2bf(y - (float)hv);
             }
-            // byte of column cc's hi in the packed row: block tn, element 8 j + 4 lh
-            const int hb = tn * 64 * NP + 2 * (8 * j + 4 * lh);
-            const int ch = ((hb >> 4) ^ pk_swz(lr)) & (CPR - 1);
-            *reinterpret_cast<ushortx4*>(reg + lr * RB + ch * 16 + (hb & 15)) = h;
-            if (NP == 2) {
-              const int lb = hb + 64;
-              const int cl = ((lb >> 4) ^ pk_swz(lr)) & (CPR - 1);
-              *reinterpret_cast<ushortx4*>(reg + lr * RB + cl * 16 + (lb & 15)) = l;
+            const uint2 hu = __builtin_bit_cast(uint2, h), lu = __builtin_bit_cast(uint2, l);
+            hw[j][0] = hu.x; hw[j][1] = hu.y;
+            lw[j][0] = lu.x; lw[j][1] = lu.y;
+          }
+#pragma unroll
+          for (int jp = 0; jp < 4; jp += 2) {
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+              const auto sh = __builtin_amdgcn_permlane32_swap(hw[jp][w], hw[jp + 1][w], false, false);
+              hw[jp][w] = sh[0];
+              hw[jp + 1][w] = sh[1];
+              if (NP == 2) {
+                const auto sl = __builtin_amdgcn_permlane32_swap(lw[jp][w], lw[jp + 1][w], false, false);
+                lw[jp][w] = sl[0];
+                lw[jp + 1][w] = sl[1];
+              }
             }
-          } else {
+            // this half's chunk: columns 8 (jp + lh) .. + 7 of block tn
+            const int hb = tn * 64 * NP + 16 * (jp + lh);
+            const int ch = ((hb >> 4) ^ pk_swz(lr)) & (CPR - 1);
+            *reinterpret_cast<uint4*>(reg + lr * RB + ch * 16) =
+                uint4{hw[jp][0], hw[jp][1], hw[jp + 1][0], hw[jp + 1][1]};
+            if (NP == 2) {
+              const int cl = (((hb + 64) >> 4) ^ pk_swz(lr)) & (CPR - 1);
+              *reinterpret_cast<uint4*>(reg + lr * RB + cl * 16) =
+                  uint4{lw[jp][0], lw[jp][1], lw[jp + 1][0], lw[jp + 1][1]};
+            }
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const floatx16& c = acc[2 * half + tt][tn];
+            const int cc = tn * 32 + 8 * j + 4 * lh;  // column within the wave's 64
             floatx4 v;
 #pragma unroll
             for (int i = 0; i < 4; ++i) v[i] = c[4 * j + i];
