@@ -14,13 +14,18 @@
 //
 // Kernels (all f32 arithmetic, exact-f32 MFMA products; per-sequence work only, with key chunks
 // fixed at 64 keys, so a sequence's result does not depend on the batch it is in):
-//   cls_u_kernel       u[s][h][:] = Σ_d q[s][64h+d] W_k[64h+d][:]          (VALU, tiny)
+//   cls_u_kernel       u[s][h][:] = Σ_d q[s][64h+d] W_k[64h+d][:]  (VALU; 4 sequences x 256
+//                      columns per workgroup: 576 workgroups at n = 64)
 //   cls_attn_kernel    one workgroup per (sequence, 64-key chunk): scores of 16-key tiles by
 //                      v_mfma_f32_16x16x4_f32 (16 keys x 16 head slots x 768), online softmax in
 //                      the exp2 domain, y_h += Σ p x_j by the same MFMA (16 head slots x 768) ->
-//                      per-chunk (max, sum, y[12][768])
-//   cls_combine_kernel the chunks of a sequence merged in chunk order -> ybar[s][h][:]
-//   cls_vproj_kernel   ctx[s][64h+d] = b_v[64h+d] + Σ_c W_v[64h+d][c] ybar[s][h][c]
+//                      per-chunk (max, sum, y[12][768]); the sequence's last chunk to finish
+//                      (a ticket on a per-sequence counter, agent-scope release / acquire) merges
+//                      the chunks in chunk order -> ybar[s][h][:]
+//   cls_vproj_kernel   ctx[s][64h+d] = b_v[64h+d] + Σ_c W_v[64h+d][c] ybar[s][h][c] by
+//                      v_mfma_f32_16x16x4_f32, one workgroup per (16 sequences, head, 16 d)
+// (round 4, first form: a 16-sequence u kernel, a separate combine kernel and a VALU projection
+// over 48 workgroups took 18.7 + 15.3 + 72.4 us of the ~145 us at B=64, profiles/r4g_*)
 // Masked (GraphCodeBERT) launches read row 0 of the sequence's bit-packed mask; the CLS row always
 // attends itself (special tokens see [:max_length], utils.py:555-557), so a fully masked CLS row
 // cannot occur — if it does the device error flag poisons the scores (alert_engine.h ae_score).
@@ -39,30 +44,33 @@ constexpr int REC = 32 + NH * H;    // floats per chunk record: m[16], l[16], y[
 __global__ __launch_bounds__(256) void cls_u_kernel(const float* __restrict__ q,
                                                     const float* __restrict__ wk, int n,
                                                     float* __restrict__ u) {
-  __shared__ float qs[16][DH];
-  const int h = blockIdx.y, s0 = blockIdx.x * 16, col = blockIdx.z * 256 + threadIdx.x;
-  for (int i = threadIdx.x; i < 16 * DH; i += 256) {
-    const int r = i / DH, d = i % DH;
+  constexpr int SB = 4;  // sequences per workgroup
+  __shared__ float qs[SB][DH];
+  const int h = blockIdx.y, s0 = blockIdx.x * SB, col = blockIdx.z * 256 + threadIdx.x;
+  {
+    const int r = threadIdx.x / DH, d = threadIdx.x % DH;  // 256 = SB x DH
     qs[r][d] = s0 + r < n ? q[(size_t)(s0 + r) * H + h * DH + d] : 0.f;
   }
   __syncthreads();
-  float acc[16];
+  float acc[SB];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int r = 0; r < SB; ++r) acc[r] = 0.f;
   const float* w = wk + (size_t)h * DH * H + col;
+#pragma unroll 8
   for (int d = 0; d < DH; ++d) {
     const float wv = w[(size_t)d * H];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = fmaf(qs[r][d], wv, acc[r]);
+    for (int r = 0; r < SB; ++r) acc[r] = fmaf(qs[r][d], wv, acc[r]);
   }
-  for (int r = 0; r < 16 && s0 + r < n; ++r) u[((size_t)(s0 + r) * NH + h) * H + col] = acc[r];
+  for (int r = 0; r < SB && s0 + r < n; ++r) u[((size_t)(s0 + r) * NH + h) * H + col] = acc[r];
 }
 
 // one workgroup (8 waves) per (chunk c, sequence s); LDS: u [12][XS], x tile [16][XS], partial
 // score tiles [8][256], p [16][16], alpha / running max / running sum [16] each
 __global__ __launch_bounds__(512) void cls_attn_kernel(
     const float* __restrict__ x, const float* __restrict__ u, const int* __restrict__ cu,
-    const uint32_t* __restrict__ mask, int mask_L, float scale, float* __restrict__ part) {
+    const uint32_t* __restrict__ mask, int mask_L, float scale, float* __restrict__ part,
+    int* __restrict__ ctr, float* __restrict__ ybar, int* __restrict__ err) {
   extern __shared__ float lds[];
   float* us = lds;                  // [12][XS]
   float* xs = us + NH * XS;         // [16][XS]
@@ -189,70 +197,95 @@ __global__ __launch_bounds__(512) void cls_attn_kernel(
       const int hs = 4 * l4 + i;
       if (hs < NH) rec[32 + hs * H + 96 * w + 16 * ct + l15] = acc[ct][i];
     }
-}
 
-// the chunks of sequence s merged in chunk order: ybar[s][h][:] = Σ_c 2^(m_c - M) y_c / L
-__global__ __launch_bounds__(256) void cls_combine_kernel(const float* __restrict__ part,
-                                                          const int* __restrict__ cu,
-                                                          float* __restrict__ ybar,
-                                                          int* __restrict__ err) {
-  const int s = blockIdx.x, h = blockIdx.y;
-  const int beg = cu[s], len = cu[s + 1] - beg, nc = (len + KC - 1) / KC;
-  const float* rec0 = part + ((size_t)(beg >> 6) + s) * REC;
-  float M = -INFINITY;
-  for (int c = 0; c < nc; ++c) M = fmaxf(M, rec0[(size_t)c * REC + h]);
-  float L = 0.f;
-  for (int c = 0; c < nc; ++c) {
-    const float m = rec0[(size_t)c * REC + h];
-    if (m != -INFINITY) L = fmaf(rec0[(size_t)c * REC + 16 + h], __builtin_amdgcn_exp2f(m - M), L);
-  }
-  if (!(L > 0.f)) {  // no key attended: cannot happen for a CLS row; poison the call
-    if (threadIdx.x == 0) atomicOr(err, 2);
-  }
-  const float inv = 1.f / L;
-  for (int col = threadIdx.x; col < H; col += 256) {
-    float y = 0.f;
-    for (int c = 0; c < nc; ++c) {
-      const float m = rec0[(size_t)c * REC + h];
-      if (m != -INFINITY)
-        y = fmaf(rec0[(size_t)c * REC + 32 + h * H + col], __builtin_amdgcn_exp2f(m - M), y);
+  // ---- the sequence's last chunk to finish merges them all (chunk order, so the bits do not
+  // depend on which one that is): plain record stores, every wave's vmcnt drain, the barrier, an
+  // agent-scope release before the relaxed ticket, an agent-scope acquire in the last arriver
+  // (cdna_hip_programming.md, in-launch split-K); the counter re-arms itself
+  const int nc = (len + KC - 1) / KC;
+  int* last_flag = reinterpret_cast<int*>(lrun + 16);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const int ticket = __hip_atomic_fetch_add(ctr + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = ticket == nc - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(ctr + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    ybar[((size_t)s * NH + h) * H + col] = y * inv;
+    *last_flag = last;
+  }
+  __syncthreads();
+  if (!*last_flag) return;
+  const float* rec0 = part + ((size_t)(beg >> 6) + s) * REC;
+  float* hM = sred;        // [12] the heads' maxima over the chunks
+  float* hinv = sred + 16; // [12] 1 / their normalisers
+  if (tid < NH) {
+    const int h = tid;
+    float M = -INFINITY;
+    for (int cc = 0; cc < nc; ++cc) M = fmaxf(M, rec0[(size_t)cc * REC + h]);
+    float L = 0.f;
+    for (int cc = 0; cc < nc; ++cc) {
+      const float m = rec0[(size_t)cc * REC + h];
+      if (m != -INFINITY) L = fmaf(rec0[(size_t)cc * REC + 16 + h], __builtin_amdgcn_exp2f(m - M), L);
+    }
+    if (!(L > 0.f)) atomicOr(err, 2);  // no key attended: cannot happen for a CLS row
+    hM[h] = M;
+    hinv[h] = 1.f / L;
+  }
+  __syncthreads();
+  for (int idx = tid; idx < NH * H; idx += 512) {
+    const int h = idx / H, col = idx % H;
+    const float M = hM[h];
+    float y = 0.f;
+    for (int cc = 0; cc < nc; ++cc) {
+      const float m = rec0[(size_t)cc * REC + h];
+      if (m != -INFINITY)
+        y = fmaf(rec0[(size_t)cc * REC + 32 + h * H + col], __builtin_amdgcn_exp2f(m - M), y);
+    }
+    ybar[((size_t)s * NH + h) * H + col] = y * hinv[h];
   }
 }
 
-// ctx[s][64h + d] = b_v[64h + d] + Σ_c W_v[64h + d][c] ybar[s][h][c]; 16 sequences x 64 d per block
+// ctx[s][64h + d] = b_v[64h + d] + Σ_c W_v[64h + d][c] ybar[s][h][c]: one workgroup per (16
+// sequences, head h, 16 d).  Wave w sums c in [192 w, 192 w + 192) by v_mfma_f32_16x16x4_f32: a
+// lane loads 4 consecutive c of its row as one float4 and feeds them to 4 MFMAs as their k-slot —
+// the same permutation of c on both operands, so the dot products are unchanged — and the 4
+// waves' 16 x 16 tiles are added in wave order
 __global__ __launch_bounds__(256) void cls_vproj_kernel(const float* __restrict__ ybar,
                                                         const float* __restrict__ wv,
                                                         const float* __restrict__ bv, int n,
                                                         float* __restrict__ ctx) {
-  __shared__ float ys[16][65];
-  __shared__ float ws[64][65];
-  const int h = blockIdx.y, s0 = blockIdx.x * 16, tid = threadIdx.x;
-  const int d = tid & 63, sg = tid >> 6;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int c0 = 0; c0 < H; c0 += 64) {
-    for (int i = tid; i < 16 * 64; i += 256) {
-      const int r = i >> 6, cc = i & 63;
-      ys[r][cc] = s0 + r < n ? ybar[((size_t)(s0 + r) * NH + h) * H + c0 + cc] : 0.f;
-    }
-    for (int i = tid; i < 64 * 64; i += 256) {
-      const int r = i >> 6, cc = i & 63;
-      ws[r][cc] = wv[(size_t)(h * DH + r) * H + c0 + cc];
-    }
-    __syncthreads();
-#pragma unroll 8
-    for (int cc = 0; cc < 64; ++cc) {
-      const float wvv = ws[d][cc];
+  __shared__ float red[4][256];
+  const int h = blockIdx.y, s0 = blockIdx.x * 16, d0 = blockIdx.z * 16;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i = lane & 15, kq = lane >> 4;
+  const int s = min(s0 + i, n - 1);
+  const float* a = ybar + ((size_t)s * NH + h) * H + 192 * w + 4 * kq;
+  const float* b = wv + (size_t)(h * DH + d0 + i) * H + 192 * w + 4 * kq;
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[r] = fmaf(ys[4 * sg + r][cc], wvv, acc[r]);
-    }
-    __syncthreads();
+  for (int blk = 0; blk < 12; ++blk) {
+    const float4 av = *reinterpret_cast<const float4*>(a + 16 * blk);
+    const float4 bw = *reinterpret_cast<const float4*>(b + 16 * blk);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bw.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bw.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bw.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bw.w, acc, 0, 0, 0);
   }
+  // D[sequence 4 kq + r][d i] of the wave's c range
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int sidx = s0 + 4 * sg + r;
-    if (sidx < n) ctx[(size_t)sidx * H + h * DH + d] = acc[r] + bv[h * DH + d];
+  for (int r = 0; r < 4; ++r) red[w][r * 64 + lane] = acc[r];
+  __syncthreads();
+  if (w == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int sidx = s0 + 4 * kq + r, d = d0 + i;
+      const float v = ((red[0][r * 64 + lane] + red[1][r * 64 + lane]) + red[2][r * 64 + lane]) +
+                      red[3][r * 64 + lane];
+      if (sidx < n) ctx[(size_t)sidx * H + h * DH + d] = v + bv[h * DH + d];
+    }
   }
 }
 
@@ -266,23 +299,23 @@ long ae_cls_attention_part_floats(long T, int n) { return ((T >> 6) + n + 2) * (
 // q: [n][768] CLS queries (the split modes' W_q carries log2(e)/8, so scale = 1; the exact mode's
 // does not, scale = log2(e)/8); wk, wv: [768][768] row-major K / V projection weights; bv: [768];
 // x: [T][768] layer-input rows (compacted, cu offsets); u_ws, ybar_ws: [n][12][768];
-// part_ws: ae_cls_attention_part_floats(T, n) floats; ctx: [n][768] out.
+// part_ws: ae_cls_attention_part_floats(T, n) floats; ctr_ws: n ints, zero before the first call
+// (the kernels leave them zero); ctx: [n][768] out.
 hipError_t ae_launch_cls_attention(const float* x, const float* q, const float* wk,
                                    const float* wv, const float* bv, const int* cu, int n,
                                    int max_len, const uint32_t* mask, int mask_L, float scale,
-                                   float* u_ws, float* part_ws, float* ybar_ws, float* ctx,
-                                   int* err, hipStream_t st) {
+                                   float* u_ws, float* part_ws, int* ctr_ws, float* ybar_ws,
+                                   float* ctx, int* err, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(cls_u_kernel, dim3((n + 15) / 16, NH, H / 256), dim3(256), 0, st, q, wk, n,
+  hipLaunchKernelGGL(cls_u_kernel, dim3((n + 3) / 4, NH, H / 256), dim3(256), 0, st, q, wk, n,
                      u_ws);
-  const size_t lds = (size_t)(NH * XS + KT * XS + 8 * 256 + 256 + 48) * sizeof(float);
+  const size_t lds = (size_t)(NH * XS + KT * XS + 8 * 256 + 256 + 48 + 4) * sizeof(float);
   hipError_t e = ensure_dynamic_lds((const void*)cls_attn_kernel, lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(cls_attn_kernel, dim3((max_len + KC - 1) / KC, n), dim3(512), lds, st, x,
-                     u_ws, cu, mask, mask_L, scale, part_ws);
-  hipLaunchKernelGGL(cls_combine_kernel, dim3(n, NH), dim3(256), 0, st, part_ws, cu, ybar_ws, err);
-  hipLaunchKernelGGL(cls_vproj_kernel, dim3((n + 15) / 16, NH), dim3(256), 0, st, ybar_ws, wv, bv,
-                     n, ctx);
+                     u_ws, cu, mask, mask_L, scale, part_ws, ctr_ws, ybar_ws, err);
+  hipLaunchKernelGGL(cls_vproj_kernel, dim3((n + 15) / 16, NH, DH / 16), dim3(256), 0, st, ybar_ws,
+                     wv, bv, n, ctx);
   return hipGetLastError();
 }
 

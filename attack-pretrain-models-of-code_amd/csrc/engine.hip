@@ -44,10 +44,6 @@ hipError_t ae_launch_gemm_packed_ln(const unsigned short*, const unsigned short*
                                     const float*, float*, unsigned short*, int, int, int, int,
                                     const float*, const float*, float, uint64_t*, int*, int*,
                                     hipStream_t);
-hipError_t ae_launch_gemm_packed_ln_fix(const unsigned short*, const unsigned short*,
-                                        const float*, const float*, float*, float*,
-                                        unsigned short*, int, int, int, int, const float*,
-                                        const float*, float, uint64_t*, int*, hipStream_t);
 hipError_t ae_launch_compact(const int*, const int*, const int*, int, int, int, int, int*, int*,
                              int*, int*, hipStream_t);
 hipError_t ae_launch_embed_ln(const int*, const int*, const float*, const float*, const float*,
@@ -72,7 +68,7 @@ hipError_t ae_launch_graph_mask(const int*, const int*, const int*, const int*, 
 long ae_cls_attention_part_floats(long, int);
 hipError_t ae_launch_cls_attention(const float*, const float*, const float*, const float*,
                                    const float*, const int*, int, int, const uint32_t*, int, float,
-                                   float*, float*, float*, float*, int*, hipStream_t);
+                                   float*, float*, int*, float*, float*, int*, hipStream_t);
 }
 
 namespace {
@@ -135,16 +131,19 @@ struct ae_engine {
   bool cls_absorb = true;
   // where the residual + LayerNorm after the O-projection / FFN2 runs (AE_LN_FIX at engine
   // creation):
-  //   2 (default) the co-resident exchange inside the GEMM (gemm_planes.hip LnArgs mode 0) on
-  //     both encoder forms — each part of the two-stream form with its own counters;
-  //   1 the row block's last-arriving tile normalises the block (mode 5);
-  //   0 the round-3 forms: a separate LayerNorm kernel on the two-stream form, mode 0 on the
-  //     single-stream one.
-  int ln_kind = 2;
+  //   0 (default) the two-stream form: a separate LayerNorm kernel after each part's GEMM (the
+  //     GEMM adds the residual); the single-stream form: inside the GEMM by the co-resident
+  //     exchange (gemm_planes.hip LnArgs mode 0);
+  //   2 the co-resident exchange on both forms, each part of the two-stream form with its own
+  //     counters (measured 16.06 vs 15.89 ms per B=64 x 512 step, 9.40 vs 9.28 ragged:
+  //     profiles/r4h_engine_ab.json — the fused GEMMs wait for partners beside the other part's
+  //     kernels, the separate LayerNorm overlaps them).
+  int ln_kind = 0;
   // the QKV GEMM may run on 256 x 192 tiles (its packed-plane epilogue) where that finishes in
   // fewer tile rounds (AE_QKV192=1 at engine creation)
   bool qkv192 = false;
   float *cls_u = nullptr, *cls_y = nullptr, *cls_part = nullptr;
+  int* cls_ctr = nullptr;  // per-sequence chunk tickets of the CLS attention (self-resetting)
   size_t cap_cls_part = 0;
   int *tok_ids = nullptr, *tok_pos = nullptr, *src_col = nullptr, *cu = nullptr, *one = nullptr;
   int* err = nullptr;  // device flag: some row's lens disagreed with its ids (compact_kernel)
@@ -302,9 +301,11 @@ int ensure_workspace(ae_engine* e, size_t T, size_t n) {
     size_t nn = n + n / 4 + 64;
     HIPC(hipDeviceSynchronize());
     for (void* p : {(void*)e->xc, (void*)e->cc, (void*)e->tc, (void*)e->hc, (void*)e->cu,
-                    (void*)e->cls_u, (void*)e->cls_y})
+                    (void*)e->cls_u, (void*)e->cls_y, (void*)e->cls_ctr})
       dev_free(e, p);
     int rc = 0;
+    if ((rc = dev_alloc(e, (void**)&e->cls_ctr, nn * 4))) return rc;
+    HIPC(hipMemset(e->cls_ctr, 0, nn * 4));
     if ((rc = dev_alloc(e, (void**)&e->cls_u, nn * 12 * H * 4))) return rc;
     if ((rc = dev_alloc(e, (void**)&e->cls_y, nn * 12 * H * 4))) return rc;
     if ((rc = dev_alloc(e, (void**)&e->xc, nn * H * 4))) return rc;
@@ -428,20 +429,6 @@ int gemm_pk_ln(ae_engine* e, const unsigned short* A, const unsigned short* Wp, 
   return AE_OK;
 }
 
-// The same over the rows [t0, t0 + M) of part `part` with the last-arriver LayerNorm (mode 5):
-// the pre-LayerNorm rows go to tmp, x and its planes receive the LayerNorm output.
-int gemm_pk_lnfix(ae_engine* e, const unsigned short* A, const unsigned short* Wp,
-                  const float* bias, const float* g, const float* b, int64_t t0, int M, int K,
-                  int part, hipStream_t st) {
-  const int H = e->cfg.hidden;
-  Prof p(e, st, e->prof_kind == AE_KIND_GEMM_ANY, 2.0 * M * H * K);
-  float* x = e->x + t0 * H;
-  HIPC(ae_launch_gemm_packed_ln_fix(A, Wp, bias, x, e->tmp + t0 * H, x, e->xp + t0 * H * e->np,
-                                    M, H, K, e->np, g, b, e->cfg.ln_eps, e->lnst + t0 * 4,
-                                    e->lnctr + part * e->ctr_stride, st));
-  return AE_OK;
-}
-
 // attention over packed planes: the production loop, or an experiment variant (unmasked launches)
 hipError_t attention_pp(ae_engine* e, const unsigned short* qkvp, float* out, unsigned short* op,
                         const int* cu, const int* q_rows, int max_q, int n, int heads,
@@ -479,11 +466,7 @@ int layer_rows(ae_engine* e, const LayerW& w, int64_t t0, int M, int s0, int ns,
                       L, np, st));
   }
   if ((rc = done())) return rc;
-  if (e->ln_kind == 1) {
-    if ((rc = gemm_pk_lnfix(e, e->cp + t0 * H * np, w.wo_p, w.bo, w.ln1g, w.ln1b, t0, M, H, part,
-                            st)) || (rc = done()))
-      return rc;
-  } else if (e->ln_kind == 2) {
+  if (e->ln_kind == 2) {
     if ((rc = gemm_pk_ln(e, e->cp + t0 * H * np, w.wo_p, w.bo, w.ln1g, w.ln1b, t0, M, H, part,
                          st)) || (rc = done()))
       return rc;
@@ -497,9 +480,6 @@ int layer_rows(ae_engine* e, const LayerW& w, int64_t t0, int M, int s0, int ns,
   if ((rc = gemm_pk(e, xp, w.w1_p, w.b1, nullptr, nullptr, e->hp + t0 * F * np, M, F, H,
                     EPI_BIAS_GELU, st, true)) || (rc = done()))
     return rc;
-  if (e->ln_kind == 1)
-    return gemm_pk_lnfix(e, e->hp + t0 * F * np, w.w2_p, w.b2, w.ln2g, w.ln2b, t0, M, F, part,
-                         st);
   if (e->ln_kind == 2)
     return gemm_pk_ln(e, e->hp + t0 * F * np, w.w2_p, w.b2, w.ln2g, w.ln2b, t0, M, F, part, st);
   if ((rc = gemm_pk(e, e->hp + t0 * F * np, w.w2_p, w.b2, x, tmp, nullptr, M, H, F,
@@ -578,8 +558,8 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
       const float scale = e->cfg.precision == AE_PREC_FP32 ? 0.18033688011112042f : 1.0f;
       HIPC(ae_launch_cls_attention(e->x, e->hc, w.wqkv + (size_t)H * H,
                                    w.wqkv + (size_t)2 * H * H, w.bqkv + 2 * H, e->cu, n, max_len,
-                                   mask_bits, L, scale, e->cls_u, e->cls_part, e->cls_y, e->cc,
-                                   e->err, st));
+                                   mask_bits, L, scale, e->cls_u, e->cls_part, e->cls_ctr,
+                                   e->cls_y, e->cc, e->err, st));
     } else if (pl) {
       // Q | K | V as packed planes (Q pre-scaled) straight into the attention's LDS-DMA
       if ((rc = gemm_pk(e, e->xp, w.wqkv_p, w.bqkv, nullptr, nullptr, qkvp, (int)T, 3 * H, H,
@@ -602,18 +582,12 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
     }
     if (!last_cls && pl) {
       // O-proj + residual + LN1 and FFN2 + residual + LN2 each one kernel (x updated in place)
-      if ((rc = e->ln_kind == 1 ? gemm_pk_lnfix(e, e->cp, w.wo_p, w.bo, w.ln1g, w.ln1b, 0, (int)T, H,
-                                                0, st)
-                                : gemm_pk_ln(e, e->cp, w.wo_p, w.bo, w.ln1g, w.ln1b, 0, (int)T, H,
-                                             0, st)))
+      if ((rc = gemm_pk_ln(e, e->cp, w.wo_p, w.bo, w.ln1g, w.ln1b, 0, (int)T, H, 0, st)))
         return rc;
       if ((rc = gemm_pk(e, e->xp, w.w1_p, w.b1, nullptr, nullptr, e->hp, (int)T, F, H,
                         EPI_BIAS_GELU, st, true)))
         return rc;
-      if ((rc = e->ln_kind == 1 ? gemm_pk_lnfix(e, e->hp, w.w2_p, w.b2, w.ln2g, w.ln2b, 0, (int)T, F,
-                                                0, st)
-                                : gemm_pk_ln(e, e->hp, w.w2_p, w.b2, w.ln2g, w.ln2b, 0, (int)T, F,
-                                             0, st)))
+      if ((rc = gemm_pk_ln(e, e->hp, w.w2_p, w.b2, w.ln2g, w.ln2b, 0, (int)T, F, 0, st)))
         return rc;
     } else if (!last_cls) {
       if ((rc = gemm(e, e->ctx, w.wo, w.wo_h, w.wo_l, w.bo, e->x, e->tmp, (int)T, H, H, EPI_BIAS_RESIDUAL,
@@ -808,8 +782,8 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
   {
     const char* ca = std::getenv("AE_CLS_ABSORB");  // A/B runs: 0 = full-T QKV + attention
     e->cls_absorb = !(ca && ca[0] == '0');
-    const char* lf = std::getenv("AE_LN_FIX");  // A/B runs: 0, 1, 2 (see ln_kind)
-    if (lf && lf[0] >= '0' && lf[0] <= '2') e->ln_kind = lf[0] - '0';
+    const char* lf = std::getenv("AE_LN_FIX");  // A/B runs: 0 or 2 (see ln_kind)
+    if (lf && (lf[0] == '0' || lf[0] == '2')) e->ln_kind = lf[0] - '0';
     const char* q192 = std::getenv("AE_QKV192");  // A/B runs: 1 = 256 x 192 QKV tiles allowed
     e->qkv192 = q192 && q192[0] == '1';
   }

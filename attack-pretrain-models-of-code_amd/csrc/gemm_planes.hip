@@ -55,14 +55,14 @@ struct LnArgs {
   int* arrive;       // [tiles_m] arrivals per 256-row block (self-resetting, zero between launches)
   int* depart;       // [tiles_m]
   int* err;          // set to 2 if a row block's partners never arrived (bounded wait)
-  int mode;          // 5 = production ("last arriver normalises", below); 0 = the round-3
-                     // co-resident exchange (partners wait for each other's statistics);
-                     // timing experiments (results WRONG for 1): 1 = no exchange (each tile
-                     // normalises with its own 192 columns' statistics), 2 = mode 0 in the
-                     // grouped XCD tile order of the other epilogues, 3 = row blocks interleaved
-                     // over the XCDs, 4 = mode 0 with the previous 8-B plane stores
-  float* out;        // mode 5: the LayerNorm output rows ([M][N] f32); C then receives the
-                     // pre-LayerNorm rows (bias + residual added) and R may alias out
+  int mode;          // 0 = production (the co-resident exchange: partners wait for each
+                     // other's statistics); timing experiments (results WRONG for 1): 1 = no
+                     // exchange (each tile normalises with its own 192 columns' statistics),
+                     // 2 = mode 0 in the grouped XCD tile order of the other epilogues, 3 = row
+                     // blocks interleaved over the XCDs, 4 = mode 0 with the previous 8-B plane
+                     // stores.  (A mode 5 — the row block's last-arriving tile normalising the
+                     // whole block, no co-residency — measured 1.5-3 ms per step slower and was
+                     // removed in round 4)
 };
 
 namespace {
@@ -763,134 +763,11 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
       const float d = a.mean - b.mean;
       tile[tm] = RowStat{(a.mean + b.mean) * 0.5f, (a.m2 + b.m2) + 48.f * d * d};
     }
-    if (ln.mode == 5) {
-      // ---- mode 5: no workgroup waits for another.  Every tile publishes its pre-LayerNorm
-      // rows (to C) and its (mean, M2) per row (to stats), then takes a ticket on the row
-      // block's counter; the one that draws the last ticket (all 4 tiles of the block are
-      // published) normalises the whole 256 x 768 block and re-arms the counter.  The hand-off
-      // is the in-launch split-K recipe of cdna_hip_programming.md (Projection GEMM item 2):
-      // plain stores, every wave's vmcnt drain, the barrier, an agent-scope release before the
-      // relaxed ticket, an agent-scope acquire in the last arriver — correct for any placement
-      // of the partners (the tile order keeps them on one XCD, which is only faster).  No
-      // co-residency is needed, so it runs beside the other half-batch stream's kernels.
-      // rows past M publish nothing: the two-stream engine's parts share one statistics array,
-      // and part 1's first rows sit where part 0's padding rows would land
-      if (sn == 0 && lh == 0) {
-#pragma unroll
-        for (int tm = 0; tm < 2; ++tm)
-          if (rb0 + 32 * tm < M)
-            ln.stats[(size_t)(rb0 + 32 * tm) * 4 + tn0] = __builtin_bit_cast(uint64_t, tile[tm]);
-      }
-#pragma unroll
-      for (int tm = 0; tm < 2; ++tm) {
-#pragma unroll
-        for (int tn = 0; tn < 3; ++tn)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            floatx4 v;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] = acc[tm][tn][4 * j + i];
-            *reinterpret_cast<floatx4*>(reg + li * RS + (tn * 8 + 2 * j + lh) * 16) = v;
-          }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-          const int kk = k % 3, g = k / 3;
-          const int idx = kk * 64 + lane, lr = idx / 12 + 16 * g, c8 = idx % 12;
-          const int row = prow0 + tm * 32 + lr;
-          if (row < M) {
-            const floatx4 o0 = *reinterpret_cast<const floatx4*>(reg + lr * RS + c8 * 32);
-            const floatx4 o1 = *reinterpret_cast<const floatx4*>(reg + lr * RS + c8 * 32 + 16);
-            float* const crow = C + (size_t)prow0 * N + (uint32_t)(lr + tm * 32) * (uint32_t)N;
-            *reinterpret_cast<floatx4*>(crow + cb0 + 8 * c8) = o0;
-            *reinterpret_cast<floatx4*>(crow + cb0 + 8 * c8 + 4) = o1;
-          }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's rows and stats are out
-      __syncthreads();
-      int* last_flag = reinterpret_cast<int*>(pk_smem + 8 * 32 * RS + 8 * 2 * 32 * sizeof(RowStat));
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int ticket =
-            __hip_atomic_fetch_add(ln.arrive + tm0, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = ticket == tiles_n - 1;
-        if (last) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __hip_atomic_store(ln.arrive + tm0, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        *last_flag = last;
-      }
-      __syncthreads();
-      if (!*last_flag) return;
-      // the block's 256 rows, 32 per wave: statistics merged in the mode-0 order ((0,1), (2,3),
-      // then the halves), LayerNorm over 768 columns (3 x 256, 4 per lane), x as 16-B stores,
-      // the packed planes as 8-B stores.  One workgroup moves the whole block (768 KB in, 1.5 MB
-      // out), so it is latency-bound unless many rows are in flight: each wave loads 8 rows
-      // (24 x 16 B per lane) and their 32 partial statistics before it computes any of them
-      // (r4f: 2 rows in flight per wave made the tail ~30 us per row block and the step slower
-      // than the separate LayerNorm kernel)
-      floatx4 gg[3], bb[3];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        gg[c] = *reinterpret_cast<const floatx4*>(ln.gamma + 256 * c + 4 * lane);
-        bb[c] = *reinterpret_cast<const floatx4*>(ln.beta + 256 * c + 4 * lane);
-      }
-      constexpr int RB = 8;
-      for (int r0 = 0; r0 < 32; r0 += RB) {
-        floatx4 v[RB][3];
-        uint64_t ps[RB][4];
-#pragma unroll
-        for (int rr = 0; rr < RB; ++rr) {
-          const int row = min(m0 + 32 * wave + r0 + rr, M - 1);  // clamped loads, guarded stores
-          const float* src = C + (size_t)row * N;
-#pragma unroll
-          for (int c = 0; c < 3; ++c) v[rr][c] = *reinterpret_cast<const floatx4*>(src + 256 * c + 4 * lane);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) ps[rr][q] = ln.stats[(size_t)row * 4 + q];
-        }
-#pragma unroll
-        for (int rr = 0; rr < RB; ++rr) {
-          const int row = m0 + 32 * wave + r0 + rr;
-          if (row >= M) break;
-          RowStat p[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) p[q] = __builtin_bit_cast(RowStat, ps[rr][q]);
-          const float d01 = p[0].mean - p[1].mean, d23 = p[2].mean - p[3].mean;
-          const float m01 = (p[0].mean + p[1].mean) * 0.5f, m23 = (p[2].mean + p[3].mean) * 0.5f;
-          const float q01 = (p[0].m2 + p[1].m2) + 96.f * d01 * d01;
-          const float q23 = (p[2].m2 + p[3].m2) + 96.f * d23 * d23;
-          const float dd = m01 - m23;
-          const float mu = (m01 + m23) * 0.5f;
-          const float rs = rsqrtf(((q01 + q23) + 192.f * dd * dd) * (1.f / 768.f) + ln.eps);
-          float* dst = ln.out + (size_t)row * N;
-          unsigned short* pl = reinterpret_cast<unsigned short*>(ln.xp) + (size_t)row * NP * N;
-#pragma unroll
-          for (int c = 0; c < 3; ++c) {
-            const int col = 256 * c + 4 * lane;
-            floatx4 o;
-            ushortx4 h, l;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              o[i] = (v[rr][c][i] - mu) * rs * gg[c][i] + bb[c][i];
-              h[i] = f2bf(o[i]);
-              l[i] = f2bf(o[i] - __builtin_bit_cast(float, (uint32_t)h[i] << 16));
-            }
-            *reinterpret_cast<floatx4*>(dst + col) = o;
-            unsigned short* pc = pl + (size_t)(col >> 5) * 32 * NP + (col & 31);
-            *reinterpret_cast<ushortx4*>(pc) = h;
-            if (NP == 2) *reinterpret_cast<ushortx4*>(pc + 32) = l;
-          }
-        }
-      }
-      return;
-    }
     // (4) publish this tile's (mean, M2) of its 256 rows; one lane signals for the workgroup
     // after every wave's stores have completed (agent-scope 8-B stores / loads, L2-coherent:
     // the partners share this XCD's L2, and the loads skip the CU's L1)
+    // (rows past M publish nothing: the two-stream engine's parts share one statistics array,
+    // and a part's first rows sit where the previous part's padding rows would land)
     if (sn == 0 && lh == 0) {
 #pragma unroll
       for (int tm = 0; tm < 2; ++tm)
@@ -903,7 +780,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
     __syncthreads();
     if (tid == 0 && ln.mode != 1) {
       // release / acquire at agent scope around the exchange (the workgroup's statistics stores
-      // are ordered before the arrival, the partners' after the wait), as mode 5's hand-off
+      // are ordered before the arrival, the partners' after the wait)
       __hip_atomic_fetch_add(ln.arrive + tm0, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       // bounded wait (~1 s): a partner that never arrives flags the engine instead of hanging
       int ok = 0;
@@ -1319,29 +1196,6 @@ hipError_t packed_ln(const unsigned short* A, const unsigned short* W, const flo
   return pp192_launch<1, PK_EPI_RES_LN>(a, w, bias, R, C, M, N, K, PK_GROUP_M, st, ln);
 }
 }  // namespace
-
-// The same with the last-arriver LayerNorm (LnArgs mode 5): C receives the pre-LayerNorm rows
-// (a scratch [M][768] f32 buffer), out the LayerNorm output (R may alias out), Cp its packed
-// planes; stats: [M][4] 8-B words; ctr: (M + 255) / 256 ints, zero on the first call (the last
-// arriver of every row block re-arms its counter).  No workgroup waits for another.
-extern "C" hipError_t ae_launch_gemm_packed_ln_fix(const unsigned short* A, const unsigned short* W,
-                                                   const float* bias, const float* R, float* C,
-                                                   float* out, unsigned short* Cp, int M, int N,
-                                                   int K, int np, const float* gamma,
-                                                   const float* beta, float eps, uint64_t* stats,
-                                                   int* ctr, hipStream_t st) {
-  if (M <= 0) return hipSuccess;
-  if (N != 768 || K % 64 != 0 || (np != 1 && np != 2) || !bias || !R || !C || !out || !Cp ||
-      !gamma || !beta || !stats || !ctr || C == R || C == out)
-    return hipErrorInvalidValue;
-  const int tiles_m = (M + 255) / 256;
-  LnArgs ln{gamma, beta, eps, reinterpret_cast<__bf16*>(Cp), stats, ctr, ctr + tiles_m, nullptr,
-            5, out};
-  auto a = reinterpret_cast<const __bf16*>(A);
-  auto w = reinterpret_cast<const __bf16*>(W);
-  if (np == 2) return pp192_launch<2, PK_EPI_RES_LN>(a, w, bias, R, C, M, N, K, PK_GROUP_M, st, ln);
-  return pp192_launch<1, PK_EPI_RES_LN>(a, w, bias, R, C, M, N, K, PK_GROUP_M, st, ln);
-}
 
 extern "C" hipError_t ae_launch_gemm_packed_ln(const unsigned short* A, const unsigned short* W,
                                                const float* bias, const float* R, float* C,
