@@ -19,13 +19,16 @@
 //   cls_attn_kernel    one workgroup per (sequence, 64-key chunk): scores of 16-key tiles by
 //                      v_mfma_f32_16x16x4_f32 (16 keys x 16 head slots x 768), online softmax in
 //                      the exp2 domain, y_h += Σ p x_j by the same MFMA (16 head slots x 768) ->
-//                      per-chunk (max, sum, y[12][768]); the sequence's last chunk to finish
-//                      (a ticket on a per-sequence counter, agent-scope release / acquire) merges
-//                      the chunks in chunk order -> ybar[s][h][:]
+//                      per-chunk (max, sum, y[12][768])
+//   cls_combine_kernel the chunks of a sequence merged in chunk order -> ybar[s][h][:], one
+//                      workgroup per (sequence, head, 256 columns)
 //   cls_vproj_kernel   ctx[s][64h+d] = b_v[64h+d] + Σ_c W_v[64h+d][c] ybar[s][h][c] by
 //                      v_mfma_f32_16x16x4_f32, one workgroup per (16 sequences, head, 16 d)
-// (round 4, first form: a 16-sequence u kernel, a separate combine kernel and a VALU projection
-// over 48 workgroups took 18.7 + 15.3 + 72.4 us of the ~145 us at B=64, profiles/r4g_*)
+// (round 4, first form: a 16-sequence u kernel, a combine over (sequence, head) and a VALU
+// projection over 48 workgroups took 18.7 + 15.3 + 72.4 us of the ~145 us at B=64,
+// profiles/r4g_*; merging the chunks in the sequence's last-arriving chunk workgroup instead of a
+// combine kernel made the attention kernel 36 -> 163-204 us: one workgroup then reads all of a
+// sequence's records, r4i)
 // Masked (GraphCodeBERT) launches read row 0 of the sequence's bit-packed mask; the CLS row always
 // attends itself (special tokens see [:max_length], utils.py:555-557), so a fully masked CLS row
 // cannot occur — if it does the device error flag poisons the scores (alert_engine.h ae_score).
@@ -69,8 +72,7 @@ __global__ __launch_bounds__(256) void cls_u_kernel(const float* __restrict__ q,
 // score tiles [8][256], p [16][16], alpha / running max / running sum [16] each
 __global__ __launch_bounds__(512) void cls_attn_kernel(
     const float* __restrict__ x, const float* __restrict__ u, const int* __restrict__ cu,
-    const uint32_t* __restrict__ mask, int mask_L, float scale, float* __restrict__ part,
-    int* __restrict__ ctr, float* __restrict__ ybar, int* __restrict__ err) {
+    const uint32_t* __restrict__ mask, int mask_L, float scale, float* __restrict__ part) {
   extern __shared__ float lds[];
   float* us = lds;                  // [12][XS]
   float* xs = us + NH * XS;         // [16][XS]
@@ -198,54 +200,31 @@ __global__ __launch_bounds__(512) void cls_attn_kernel(
       if (hs < NH) rec[32 + hs * H + 96 * w + 16 * ct + l15] = acc[ct][i];
     }
 
-  // ---- the sequence's last chunk to finish merges them all (chunk order, so the bits do not
-  // depend on which one that is): plain record stores, every wave's vmcnt drain, the barrier, an
-  // agent-scope release before the relaxed ticket, an agent-scope acquire in the last arriver
-  // (cdna_hip_programming.md, in-launch split-K); the counter re-arms itself
-  const int nc = (len + KC - 1) / KC;
-  int* last_flag = reinterpret_cast<int*>(lrun + 16);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    const int ticket = __hip_atomic_fetch_add(ctr + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = ticket == nc - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      __hip_atomic_store(ctr + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    *last_flag = last;
-  }
-  __syncthreads();
-  if (!*last_flag) return;
+}
+
+// the chunks of sequence s merged in chunk order: ybar[s][h][c] = Σ_k 2^(m_k - M) y_k[h][c] / L
+__global__ __launch_bounds__(256) void cls_combine_kernel(const float* __restrict__ part,
+                                                          const int* __restrict__ cu,
+                                                          float* __restrict__ ybar,
+                                                          int* __restrict__ err) {
+  const int s = blockIdx.x, h = blockIdx.y, col = blockIdx.z * 256 + threadIdx.x;
+  const int beg = cu[s], len = cu[s + 1] - beg, nc = (len + KC - 1) / KC;
   const float* rec0 = part + ((size_t)(beg >> 6) + s) * REC;
-  float* hM = sred;        // [12] the heads' maxima over the chunks
-  float* hinv = sred + 16; // [12] 1 / their normalisers
-  if (tid < NH) {
-    const int h = tid;
-    float M = -INFINITY;
-    for (int cc = 0; cc < nc; ++cc) M = fmaxf(M, rec0[(size_t)cc * REC + h]);
-    float L = 0.f;
-    for (int cc = 0; cc < nc; ++cc) {
-      const float m = rec0[(size_t)cc * REC + h];
-      if (m != -INFINITY) L = fmaf(rec0[(size_t)cc * REC + 16 + h], __builtin_amdgcn_exp2f(m - M), L);
+  float M = -INFINITY;
+  for (int c = 0; c < nc; ++c) M = fmaxf(M, rec0[(size_t)c * REC + h]);
+  float L = 0.f, y = 0.f;
+  for (int c = 0; c < nc; ++c) {
+    const float m = rec0[(size_t)c * REC + h];
+    if (m != -INFINITY) {
+      const float e = __builtin_amdgcn_exp2f(m - M);
+      L = fmaf(rec0[(size_t)c * REC + 16 + h], e, L);
+      y = fmaf(rec0[(size_t)c * REC + 32 + h * H + col], e, y);
     }
-    if (!(L > 0.f)) atomicOr(err, 2);  // no key attended: cannot happen for a CLS row
-    hM[h] = M;
-    hinv[h] = 1.f / L;
   }
-  __syncthreads();
-  for (int idx = tid; idx < NH * H; idx += 512) {
-    const int h = idx / H, col = idx % H;
-    const float M = hM[h];
-    float y = 0.f;
-    for (int cc = 0; cc < nc; ++cc) {
-      const float m = rec0[(size_t)cc * REC + h];
-      if (m != -INFINITY)
-        y = fmaf(rec0[(size_t)cc * REC + 32 + h * H + col], __builtin_amdgcn_exp2f(m - M), y);
-    }
-    ybar[((size_t)s * NH + h) * H + col] = y * hinv[h];
+  if (!(L > 0.f)) {  // no key attended: cannot happen for a CLS row; poison the call
+    if (threadIdx.x == 0 && blockIdx.z == 0) atomicOr(err, 2);
   }
+  ybar[((size_t)s * NH + h) * H + col] = y * (1.f / L);
 }
 
 // ctx[s][64h + d] = b_v[64h + d] + Σ_c W_v[64h + d][c] ybar[s][h][c]: one workgroup per (16
@@ -299,21 +278,22 @@ long ae_cls_attention_part_floats(long T, int n) { return ((T >> 6) + n + 2) * (
 // q: [n][768] CLS queries (the split modes' W_q carries log2(e)/8, so scale = 1; the exact mode's
 // does not, scale = log2(e)/8); wk, wv: [768][768] row-major K / V projection weights; bv: [768];
 // x: [T][768] layer-input rows (compacted, cu offsets); u_ws, ybar_ws: [n][12][768];
-// part_ws: ae_cls_attention_part_floats(T, n) floats; ctr_ws: n ints, zero before the first call
-// (the kernels leave them zero); ctx: [n][768] out.
+// part_ws: ae_cls_attention_part_floats(T, n) floats; ctx: [n][768] out.
 hipError_t ae_launch_cls_attention(const float* x, const float* q, const float* wk,
                                    const float* wv, const float* bv, const int* cu, int n,
                                    int max_len, const uint32_t* mask, int mask_L, float scale,
-                                   float* u_ws, float* part_ws, int* ctr_ws, float* ybar_ws,
-                                   float* ctx, int* err, hipStream_t st) {
+                                   float* u_ws, float* part_ws, float* ybar_ws, float* ctx,
+                                   int* err, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(cls_u_kernel, dim3((n + 3) / 4, NH, H / 256), dim3(256), 0, st, q, wk, n,
                      u_ws);
-  const size_t lds = (size_t)(NH * XS + KT * XS + 8 * 256 + 256 + 48 + 4) * sizeof(float);
+  const size_t lds = (size_t)(NH * XS + KT * XS + 8 * 256 + 256 + 48) * sizeof(float);
   hipError_t e = ensure_dynamic_lds((const void*)cls_attn_kernel, lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(cls_attn_kernel, dim3((max_len + KC - 1) / KC, n), dim3(512), lds, st, x,
-                     u_ws, cu, mask, mask_L, scale, part_ws, ctr_ws, ybar_ws, err);
+                     u_ws, cu, mask, mask_L, scale, part_ws);
+  hipLaunchKernelGGL(cls_combine_kernel, dim3(n, NH, H / 256), dim3(256), 0, st, part_ws, cu,
+                     ybar_ws, err);
   hipLaunchKernelGGL(cls_vproj_kernel, dim3((n + 15) / 16, NH, DH / 16), dim3(256), 0, st, ybar_ws,
                      wv, bv, n, ctx);
   return hipGetLastError();

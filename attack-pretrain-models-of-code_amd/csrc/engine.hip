@@ -68,7 +68,7 @@ hipError_t ae_launch_graph_mask(const int*, const int*, const int*, const int*, 
 long ae_cls_attention_part_floats(long, int);
 hipError_t ae_launch_cls_attention(const float*, const float*, const float*, const float*,
                                    const float*, const int*, int, int, const uint32_t*, int, float,
-                                   float*, float*, int*, float*, float*, int*, hipStream_t);
+                                   float*, float*, float*, float*, int*, hipStream_t);
 }
 
 namespace {
@@ -143,7 +143,6 @@ struct ae_engine {
   // fewer tile rounds (AE_QKV192=1 at engine creation)
   bool qkv192 = false;
   float *cls_u = nullptr, *cls_y = nullptr, *cls_part = nullptr;
-  int* cls_ctr = nullptr;  // per-sequence chunk tickets of the CLS attention (self-resetting)
   size_t cap_cls_part = 0;
   int *tok_ids = nullptr, *tok_pos = nullptr, *src_col = nullptr, *cu = nullptr, *one = nullptr;
   int* err = nullptr;  // device flag: some row's lens disagreed with its ids (compact_kernel)
@@ -301,11 +300,9 @@ int ensure_workspace(ae_engine* e, size_t T, size_t n) {
     size_t nn = n + n / 4 + 64;
     HIPC(hipDeviceSynchronize());
     for (void* p : {(void*)e->xc, (void*)e->cc, (void*)e->tc, (void*)e->hc, (void*)e->cu,
-                    (void*)e->cls_u, (void*)e->cls_y, (void*)e->cls_ctr})
+                    (void*)e->cls_u, (void*)e->cls_y})
       dev_free(e, p);
     int rc = 0;
-    if ((rc = dev_alloc(e, (void**)&e->cls_ctr, nn * 4))) return rc;
-    HIPC(hipMemset(e->cls_ctr, 0, nn * 4));
     if ((rc = dev_alloc(e, (void**)&e->cls_u, nn * 12 * H * 4))) return rc;
     if ((rc = dev_alloc(e, (void**)&e->cls_y, nn * 12 * H * 4))) return rc;
     if ((rc = dev_alloc(e, (void**)&e->xc, nn * H * 4))) return rc;
@@ -558,8 +555,8 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
       const float scale = e->cfg.precision == AE_PREC_FP32 ? 0.18033688011112042f : 1.0f;
       HIPC(ae_launch_cls_attention(e->x, e->hc, w.wqkv + (size_t)H * H,
                                    w.wqkv + (size_t)2 * H * H, w.bqkv + 2 * H, e->cu, n, max_len,
-                                   mask_bits, L, scale, e->cls_u, e->cls_part, e->cls_ctr,
-                                   e->cls_y, e->cc, e->err, st));
+                                   mask_bits, L, scale, e->cls_u, e->cls_part, e->cls_y, e->cc,
+                                   e->err, st));
     } else if (pl) {
       // Q | K | V as packed planes (Q pre-scaled) straight into the attention's LDS-DMA
       if ((rc = gemm_pk(e, e->xp, w.wqkv_p, w.bqkv, nullptr, nullptr, qkvp, (int)T, 3 * H, H,
