@@ -61,8 +61,9 @@ def parse_args():
                     help="CPU scoring microbenchmark budget (cpu_baseline)")
     ap.add_argument("--cpu-e2e-seconds", type=float, default=60.0,
                     help="cap (s) of the CPU config-1 greedy attack (config1.cpu); all 16 "
-                         "functions take ~15 min (tools/config1_cpu_full.py ran them once: "
-                         "profiles/r3_config1_cpu_full.json, compared as config1.cpu_full_run)")
+                         "functions take ~9 min on 16 threads (tools/config1_cpu_full.py ran "
+                         "them once on the GPU box's host: profiles/r4_config1_cpu_full.json, "
+                         "compared as config1.cpu_full_run)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--attack-examples", type=int, default=400,
                     help="examples of test_subs_0_400 in the config-2 GA attack leg (0 disables)")
@@ -327,9 +328,10 @@ def config1_leg(dev, precision, threads, cpu_seconds):
         from tools.config1_cpu_full import record_key
         rec = json.load(open(full[-1]))
         mine = [record_key(r) for r in g["records"]]
-        res["cpu_full_run"] = {k: rec[k] for k in ("kind", "cores", "cpu_count", "examples_completed",
-                                                   "complete", "queries", "successes", "wall_s",
-                                                   "victim_queries_per_s")}
+        res["cpu_full_run"] = {k: rec[k] for k in ("kind", "cores", "host", "cpu_count",
+                                                   "examples_completed", "complete", "queries",
+                                                   "successes", "wall_s", "victim_queries_per_s")
+                               if k in rec}
         res["cpu_full_run"]["record"] = "profiles/" + pathlib.Path(full[-1]).name
         res["cpu_full_run"]["same_outcome_as_gpu"] = sum(a == b for a, b in zip(mine, rec["records"]))
     if cpu_seconds > 0:
