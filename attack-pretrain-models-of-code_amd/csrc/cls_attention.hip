@@ -68,16 +68,16 @@ __global__ __launch_bounds__(256) void cls_u_kernel(const float* __restrict__ q,
   for (int r = 0; r < SB && s0 + r < n; ++r) u[((size_t)(s0 + r) * NH + h) * H + col] = acc[r];
 }
 
-// one workgroup (8 waves) per (chunk c, sequence s); LDS: x tile [16][XS], partial score tiles
-// [8][256], p [16][16], alpha / running max / running sum [16] each (59 KiB: two workgroups per
-// CU).  u stays in registers: wave w contracts dims [96w, 96w + 96), so lane (head slot l15,
-// k-slot l4) only ever needs u[l15][96w + 4kk + l4], kk < 24 — 24 values loaded once (u in LDS
-// made the workgroup 96 KiB, one per CU: 41 us at B=64, profiles/r4j)
-__global__ __launch_bounds__(512, 4) void cls_attn_kernel(
+// one workgroup (8 waves) per (chunk c, sequence s); LDS: u [12][XS], x tile [16][XS], partial
+// score tiles [8][256], p [16][16], alpha / running max / running sum [16] each.  (u held in 24
+// registers per lane instead, for 59 KiB of LDS and two workgroups per CU: 63 vs 41 us at B=64,
+// profiles/r4o — slower, not kept.)
+__global__ __launch_bounds__(512) void cls_attn_kernel(
     const float* __restrict__ x, const float* __restrict__ u, const int* __restrict__ cu,
     const uint32_t* __restrict__ mask, int mask_L, float scale, float* __restrict__ part) {
   extern __shared__ float lds[];
-  float* xs = lds;                  // [16][XS]
+  float* us = lds;                  // [12][XS]
+  float* xs = us + NH * XS;         // [16][XS]
   float* sred = xs + KT * XS;       // [8][256]
   float* pt = sred + 8 * 256;       // [16 keys][16 heads]
   float* alpha = pt + 256;          // [16]
@@ -91,13 +91,11 @@ __global__ __launch_bounds__(512, 4) void cls_attn_kernel(
   const int l15 = lane & 15, l4 = lane >> 4;
   const uint32_t* mrow = mask ? mask + (size_t)s * mask_L * (mask_L / 32) : nullptr;
 
-  // this lane's u values (the B operand of the score MFMAs for its head slot and k-slot)
-  float ureg[24];
-  {
-    const float* ur = u + ((size_t)s * NH + (l15 < NH ? l15 : 0)) * H + 96 * w + l4;
-    const float live = l15 < NH ? 1.f : 0.f;  // head slots 12-15 contract with zeros
-#pragma unroll
-    for (int kk = 0; kk < 24; ++kk) ureg[kk] = ur[4 * kk] * live;
+  // u of this sequence -> LDS (12 x 192 float4)
+  const float4* u4 = reinterpret_cast<const float4*>(u + (size_t)s * NH * H);
+  for (int i = tid; i < NH * (H / 4); i += 512) {
+    const int r = i / (H / 4), c4 = i % (H / 4);
+    *reinterpret_cast<float4*>(us + r * XS + 4 * c4) = u4[i];
   }
   if (tid < 16) {
     mrun[tid] = -INFINITY;
@@ -111,13 +109,11 @@ __global__ __launch_bounds__(512, 4) void cls_attn_kernel(
   float4 pre[6];  // the next x tile, 16 rows x 192 float4 over 512 threads
   auto load_tile = [&](int t) {
     const int r0 = k0 + t * KT;
-    // rows past the sequence re-read its last row: their scores are -inf, so p = 0 and the
-    // finite values add nothing to y
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       const int f = tid + 512 * j, r = f / (H / 4), c4 = f % (H / 4);
-      const int row = min(r0 + r, len - 1);
-      pre[j] = reinterpret_cast<const float4*>(x + (size_t)(beg + row) * H)[c4];
+      pre[j] = r0 + r < len ? reinterpret_cast<const float4*>(x + (size_t)(beg + r0 + r) * H)[c4]
+                            : float4{0.f, 0.f, 0.f, 0.f};
     }
   };
   load_tile(0);
@@ -133,9 +129,12 @@ __global__ __launch_bounds__(512, 4) void cls_attn_kernel(
     // scores: wave w contracts dims [96w, 96w + 96) -> D[key = 4*l4 + i][head slot = l15]
     floatx4 d = floatx4{0.f, 0.f, 0.f, 0.f};
     const float* xa = xs + l15 * XS + 96 * w + l4;
+    const float* ub = us + (l15 < NH ? l15 : 0) * XS + 96 * w + l4;
 #pragma unroll
-    for (int kk = 0; kk < 24; ++kk)
-      d = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[4 * kk], ureg[kk], d, 0, 0, 0);
+    for (int kk = 0; kk < 24; ++kk) {
+      const float b = l15 < NH ? ub[4 * kk] : 0.f;
+      d = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[4 * kk], b, d, 0, 0, 0);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) sred[w * 256 + (4 * l4 + i) * 16 + l15] = d[i];
     __syncthreads();
@@ -290,7 +289,7 @@ hipError_t ae_launch_cls_attention(const float* x, const float* q, const float* 
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(cls_u_kernel, dim3((n + 3) / 4, NH, H / 256), dim3(256), 0, st, q, wk, n,
                      u_ws);
-  const size_t lds = (size_t)(KT * XS + 8 * 256 + 256 + 48) * sizeof(float);
+  const size_t lds = (size_t)(NH * XS + KT * XS + 8 * 256 + 256 + 48) * sizeof(float);
   hipError_t e = ensure_dynamic_lds((const void*)cls_attn_kernel, lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(cls_attn_kernel, dim3((max_len + KC - 1) / KC, n), dim3(512), lds, st, x,
