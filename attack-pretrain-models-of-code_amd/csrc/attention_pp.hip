@@ -654,7 +654,7 @@ hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op
   if (np != 1 && np != 2) return hipErrorInvalidValue;
   dim3 grid((max_q + QPB - 1) / QPB, heads, n), block(256);
 #define APP_LAUNCH(N, M, PL)                                                                 \
-  hipLaunchKernelGGL((attn_pp_kernel<N, M, PL, M ? (PIPE >= 60 ? 66 : 4) : PIPE>), grid, block, 0, \
+  hipLaunchKernelGGL((attn_pp_kernel<N, M, PL, M ? (PIPE == 72 ? 72 : PIPE >= 60 ? 66 : 4) : PIPE>), grid, block, 0, \
                      stream, qkvp, out, op, cu,                                                 \
                      q_rows, mask, mask_L)
 #define APP_MP(N)                                                      \

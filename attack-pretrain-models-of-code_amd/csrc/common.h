@@ -69,6 +69,25 @@ __device__ __forceinline__ float gelu_erfc_fast(float x) {
   return fmaf(-au, (p * t) * e, u + au);
 }
 
+// gelu_erfc_fast on a pair, written on 2-wide vectors so every non-transcendental step is one
+// packed-f32 instruction (v_pk_fma / v_pk_mul / v_pk_add: the same IEEE operation per element,
+// so the results equal two gelu_erfc_fast calls bit for bit); the rcp and exp2 stay scalar.
+typedef float gelu_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ gelu_f2 gelu_erfc_fast2(gelu_f2 x) {
+  const gelu_f2 u = x * 0.5f;
+  const gelu_f2 au = {fabsf(u.x), fabsf(u.y)};
+  const gelu_f2 d = __builtin_elementwise_fma(gelu_f2(0.46328380415598320f), au, gelu_f2(1.0f));
+  const gelu_f2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  gelu_f2 p = gelu_f2(1.061405429f);
+  p = __builtin_elementwise_fma(p, t, gelu_f2(-1.453152027f));
+  p = __builtin_elementwise_fma(p, t, gelu_f2(1.421413741f));
+  p = __builtin_elementwise_fma(p, t, gelu_f2(-0.284496736f));
+  p = __builtin_elementwise_fma(p, t, gelu_f2(0.254829592f));
+  const gelu_f2 a = u * (-2.88539008177792680f * u);
+  const gelu_f2 e = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+  return __builtin_elementwise_fma(-au, (p * t) * e, u + au);
+}
+
 // bf16 round-to-nearest-even of an f32 (NaN-preserving cast lowered to v_cvt_pk_bf16_f32).
 __device__ __forceinline__ unsigned short f2bf(float f) {
   __bf16 b = (__bf16)f;

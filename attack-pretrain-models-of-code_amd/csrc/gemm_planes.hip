@@ -391,11 +391,18 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
             const int cc = tn * 32 + 8 * j + 4 * lh;  // column within the wave's 64
             const int col = cb0 + cc < N ? cb0 + cc : N - 4;
             const floatx4 bv = *reinterpret_cast<const floatx4*>(bias + col);
+            float yv[4];
+#pragma unroll
+            for (int i = 0; i < 4; i += 2) {
+              const gelu_f2 z = gelu_f2{c[4 * j + i], c[4 * j + i + 1]} + gelu_f2{bv[i], bv[i + 1]};
+              const gelu_f2 y = EPI == PK_EPI_GELU_PACKED ? gelu_erfc_fast2(z) : z;
+              yv[i] = y.x;
+              yv[i + 1] = y.y;
+            }
             ushortx4 h, l;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              const float y = EPI == PK_EPI_GELU_PACKED ? gelu_erfc_fast(c[4 * j + i] + bv[i])
-                                                        : c[4 * j + i] + bv[i];
+              const float y = yv[i];
               const __bf16 hv = (__bf16)y;
               h[i] = __builtin_bit_cast(unsigned short, hv);
               l[i] = f2bf(y - (float)hv);
