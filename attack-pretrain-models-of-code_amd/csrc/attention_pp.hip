@@ -116,8 +116,14 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && NP 
   // unit) and the cross-half row max by v_permlane32_swap instead of an LDS permute.
   // PIPE 67: 66 with the tile max as a 3-level tree of v_max3 (depth 3 instead of a chain of 8).
   static_assert(PIPE == 4 || PIPE == 6 || PIPE == 66 || PIPE == 67 || PIPE == 69 || PIPE == 70 ||
-                    PIPE == 72,
-                "loop variants 4, 6, 66, 67, 69, 70, 72");
+                    PIPE == 72 || PIPE == 73,
+                "loop variants 4, 6, 66, 67, 69, 70, 72, 73");
+  // PIPE 73: 66 whose masked launches skip every key tile that no query of the wave attends
+  // (the tile's MFMAs, max, exp and PV; its DMA and barriers stay) when each of the wave's query
+  // rows attends some key — bit-identical, since such a tile adds exp2(-FLT_MAX - m) = 0 (and a
+  // leading one is erased by the first real tile's rescale by exactly 0); a row that attends
+  // nothing keeps the reference's uniform attention over all keys (no skipping in its wave)
+  constexpr bool SKIP = HAS_MASK && PIPE == 73;
   constexpr int PB = PIPE >= 60 ? 6 : PIPE;
   constexpr bool FAST = PIPE >= 60;
   constexpr bool TREE = PIPE == 67 || (PIPE >= 69 && PIPE <= 72);
@@ -391,6 +397,20 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && NP 
       if constexpr (HAS_MASK)
         dma4s(moff, mbase + j, lds0 + MASK_OFF + (uint32_t)((j % 3) * 1024 + wave * 256));
     };
+    // PIPE 73: does every query row of the wave attend some key of the sequence?  (plain loads,
+    // consumed here, before the first counted DMA)
+    bool rows_live = false;
+    if constexpr (SKIP) {
+      const int nw = (len + 31) >> 5;
+      uint32_t any = 0;
+      for (int j = 0; j < nw; ++j) {
+        uint32_t wd = mrow[j];
+        if (j == nw - 1 && (len & 31)) wd &= (1u << (len & 31)) - 1u;
+        any |= wd;
+      }
+      rows_live = __all(any != 0u);
+    }
+    bool skip_c = false;  // PIPE 73: the current tile is skipped
     // prologue: K0 V0 M0 K1 V1 M1 K2 (as many as exist; M = mask words, masked launches only)
     issue(0, false, lds0 + kslot(0));
     issue(0, true, lds0 + vslot(0));
@@ -429,6 +449,26 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && NP 
       if (kt + 3 < nkt) {
         issue(kt + 3, false, lds0 + KS_ISS);
         n_iss += DM;
+      }
+      // PIPE 73: tile kt+1's mask words landed last iteration; skip it when no query of the wave
+      // attends any of its keys
+      bool skip_n = false;
+      if constexpr (SKIP) {
+        if (rows_live && kt + 1 < nkt) {
+          uint32_t mb = *reinterpret_cast<const uint32_t*>(lds + MASK_OFF + ((R + 1) % 3) * 1024 +
+                                                            wave * 256 + 4 * li);
+          const int rem = len - (kt + 1) * KT;
+          if (rem < KT) mb &= (1u << rem) - 1u;
+          skip_n = !__any(mb != 0u);
+        }
+        if (skip_c) {
+          if (!skip_n) s_mfma(lds + KS_NEXT, s_next);
+          skip_c = skip_n;
+          wait_vm(n_iss);
+          barrier();
+          return;
+        }
+        skip_c = skip_n;
       }
       // deferred rescale (cdna_hip_programming.md T13): keep the running max unless some row's
       // tile max exceeds it by more than 8 (log2 domain), so P <= 2^8 and the O rescale runs only
@@ -654,7 +694,7 @@ hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op
   if (np != 1 && np != 2) return hipErrorInvalidValue;
   dim3 grid((max_q + QPB - 1) / QPB, heads, n), block(256);
 #define APP_LAUNCH(N, M, PL)                                                                 \
-  hipLaunchKernelGGL((attn_pp_kernel<N, M, PL, M ? (PIPE == 72 ? 72 : PIPE >= 60 ? 66 : 4) : PIPE>), grid, block, 0, \
+  hipLaunchKernelGGL((attn_pp_kernel<N, M, PL, M ? (PIPE == 72 || PIPE == 73 ? PIPE : PIPE >= 60 ? 66 : 4) : (PIPE == 73 ? 67 : PIPE)>), grid, block, 0, \
                      stream, qkvp, out, op, cu,                                                 \
                      q_rows, mask, mask_L)
 #define APP_MP(N)                                                      \
@@ -722,6 +762,7 @@ extern "C" hipError_t ae_bench_attention_pp(const unsigned short* qkvp, float* o
     case 69: return app_launch<69>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
     case 70: return app_launch<70>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
     case 72: return app_launch<72>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
+    case 73: return app_launch<73>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
     default: break;
   }
   return hipErrorInvalidValue;

@@ -52,6 +52,13 @@ def main():
     ap.add_argument("--terms", type=int, default=3)
     ap.add_argument("--ragged", action="store_true")
     ap.add_argument("--mask", action="store_true")
+    ap.add_argument("--mask-gcb", action="store_true",
+                    help="with --mask: GraphCodeBERT's mask structure (utils.py:547-570) instead "
+                         "of random bits — the last 128 positions data-flow nodes over 1-3 code "
+                         "tokens and 1-2 edges each, code rows attending all code rows")
+    ap.add_argument("--mask-density", type=float, default=0.6,
+                    help="fraction of keys each query keeps under --mask (1.0: the mask path "
+                         "with nothing excluded)")
     ap.add_argument("--planes", action="store_true",
                     help="packed-plane context output (the engine's launch) instead of f32")
     ap.add_argument("--rounds", type=int, default=7)
@@ -86,8 +93,24 @@ def main():
     cs = min(args.check_seqs, n)
     dense, dmask = None, None
     if args.mask:
-        dense = torch.rand(n, L, L, generator=g) < 0.6
-        dense[:, :, 0] = True
+        if args.mask_gcb:
+            nodes = min(128, L // 5)
+            ncode = L - nodes
+            dense = torch.zeros(n, L, L, dtype=torch.bool)
+            dense[:, :ncode, :ncode] = True
+            dense[:, 0, :] = True
+            dense[:, ncode - 1, :] = True
+            for s_ in range(n):
+                for i in range(nodes):
+                    a = int(torch.randint(1, ncode - 3, (1,), generator=g))
+                    b = a + int(torch.randint(1, 4, (1,), generator=g))
+                    dense[s_, ncode + i, a:b] = True
+                    dense[s_, a:b, ncode + i] = True
+                    for _ in range(int(torch.randint(1, 3, (1,), generator=g))):
+                        dense[s_, ncode + i, ncode + int(torch.randint(0, nodes, (1,), generator=g))] = True
+        else:
+            dense = torch.rand(n, L, L, generator=g) < args.mask_density
+            dense[:, :, 0] = True
         words = (dense.view(n, L, L // 32, 32).long() << torch.arange(32)).sum(-1)
         dmask = (words - (words >= 2 ** 31).long() * 2 ** 32).to(torch.int32).to(dev)
     ref = reference(qkv[:int(cu[cs])], cu, cs, dense)
