@@ -103,7 +103,7 @@ __device__ __forceinline__ int vpos(int r, int x) {
 // instructions).  Kept only as the mask path of the PIPE 6 reference (bench variant 6).
 // PIPE 6 / 66 / 67: below (67 is the production loop).
 template <int NP, bool HAS_MASK, bool PLANES, int PIPE>
-__global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && NP == 2)) ? 3 : 2) void attn_pp_kernel(const unsigned short* __restrict__ qkvp,
+__global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && (NP == 2 || PIPE == 73))) ? 3 : 2) void attn_pp_kernel(const unsigned short* __restrict__ qkvp,
                                                          float* __restrict__ out,
                                                          unsigned short* __restrict__ op,
                                                          const int* __restrict__ cu,
@@ -461,15 +461,10 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && NP 
           if (rem < KT) mb &= (1u << rem) - 1u;
           skip_n = !__any(mb != 0u);
         }
-        if (skip_c) {
-          if (!skip_n) s_mfma(lds + KS_NEXT, s_next);
-          skip_c = skip_n;
-          wait_vm(n_iss);
-          barrier();
-          return;
-        }
-        skip_c = skip_n;
       }
+      if (SKIP && skip_c) {  // this tile adds nothing: only the next tile's S
+        s_mfma(lds + KS_NEXT, s_next);
+      } else {
       // deferred rescale (cdna_hip_programming.md T13): keep the running max unless some row's
       // tile max exceeds it by more than 8 (log2 domain), so P <= 2^8 and the O rescale runs only
       // on the tiles that move a max by that much — the same softmax with another reference max
@@ -545,6 +540,8 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && NP 
         for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
       }
       pv_mfma(lds + VS_CUR, ph, pl);
+      }
+      if constexpr (SKIP) skip_c = skip_n;
       wait_vm(n_iss);  // V_{kt+1}, K_{kt+2} landed; this iteration's DMA stays in flight
       barrier();
     };
