@@ -410,7 +410,6 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && (NP
       }
       rows_live = __all(any != 0u);
     }
-    bool skip_c = false;  // PIPE 73: the current tile is skipped
     // prologue: K0 V0 M0 K1 V1 M1 K2 (as many as exist; M = mask words, masked launches only)
     issue(0, false, lds0 + kslot(0));
     issue(0, true, lds0 + vslot(0));
@@ -450,16 +449,16 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && (NP
         issue(kt + 3, false, lds0 + KS_ISS);
         n_iss += DM;
       }
-      // PIPE 73: tile kt+1's mask words landed last iteration; skip it when no query of the wave
-      // attends any of its keys
-      bool skip_n = false;
+      // PIPE 73: this tile's mask words (issued two iterations ago, landed at the last wait):
+      // skip its work when no query of the wave attends any of its keys (tile 0 never)
+      bool skip_c = false;
       if constexpr (SKIP) {
-        if (rows_live && kt + 1 < nkt) {
-          uint32_t mb = *reinterpret_cast<const uint32_t*>(lds + MASK_OFF + ((R + 1) % 3) * 1024 +
+        if (rows_live && kt > 0) {
+          uint32_t mb = *reinterpret_cast<const uint32_t*>(lds + MASK_OFF + (R % 3) * 1024 +
                                                             wave * 256 + 4 * li);
-          const int rem = len - (kt + 1) * KT;
+          const int rem = len - kt * KT;
           if (rem < KT) mb &= (1u << rem) - 1u;
-          skip_n = !__any(mb != 0u);
+          skip_c = !__any(mb != 0u);
         }
       }
       if (SKIP && skip_c) {  // this tile adds nothing: only the next tile's S
@@ -541,7 +540,6 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && (NP
       }
       pv_mfma(lds + VS_CUR, ph, pl);
       }
-      if constexpr (SKIP) skip_c = skip_n;
       wait_vm(n_iss);  // V_{kt+1}, K_{kt+2} landed; this iteration's DMA stays in flight
       barrier();
     };
