@@ -103,7 +103,7 @@ __device__ __forceinline__ int vpos(int r, int x) {
 // instructions).  Kept only as the mask path of the PIPE 6 reference (bench variant 6).
 // PIPE 6 / 66 / 67: below (67 is the production loop).
 template <int NP, bool HAS_MASK, bool PLANES, int PIPE>
-__global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && (NP == 2 || PIPE == 73))) ? 3 : 2) void attn_pp_kernel(const unsigned short* __restrict__ qkvp,
+__global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && NP == 2)) ? 3 : 2) void attn_pp_kernel(const unsigned short* __restrict__ qkvp,
                                                          float* __restrict__ out,
                                                          unsigned short* __restrict__ op,
                                                          const int* __restrict__ cu,
@@ -116,14 +116,8 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && (NP
   // unit) and the cross-half row max by v_permlane32_swap instead of an LDS permute.
   // PIPE 67: 66 with the tile max as a 3-level tree of v_max3 (depth 3 instead of a chain of 8).
   static_assert(PIPE == 4 || PIPE == 6 || PIPE == 66 || PIPE == 67 || PIPE == 69 || PIPE == 70 ||
-                    PIPE == 72 || PIPE == 73,
-                "loop variants 4, 6, 66, 67, 69, 70, 72, 73");
-  // PIPE 73: 66 whose masked launches skip every key tile that no query of the wave attends
-  // (the tile's MFMAs, max, exp and PV; its DMA and barriers stay) when each of the wave's query
-  // rows attends some key — bit-identical, since such a tile adds exp2(-FLT_MAX - m) = 0 (and a
-  // leading one is erased by the first real tile's rescale by exactly 0); a row that attends
-  // nothing keeps the reference's uniform attention over all keys (no skipping in its wave)
-  constexpr bool SKIP = HAS_MASK && PIPE == 73;
+                    PIPE == 72,
+                "loop variants 4, 6, 66, 67, 69, 70, 72");
   constexpr int PB = PIPE >= 60 ? 6 : PIPE;
   constexpr bool FAST = PIPE >= 60;
   constexpr bool TREE = PIPE == 67 || (PIPE >= 69 && PIPE <= 72);
@@ -397,19 +391,6 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && (NP
       if constexpr (HAS_MASK)
         dma4s(moff, mbase + j, lds0 + MASK_OFF + (uint32_t)((j % 3) * 1024 + wave * 256));
     };
-    // PIPE 73: does every query row of the wave attend some key of the sequence?  (plain loads,
-    // consumed here, before the first counted DMA)
-    bool rows_live = false;
-    if constexpr (SKIP) {
-      const int nw = (len + 31) >> 5;
-      uint32_t any = 0;
-      for (int j = 0; j < nw; ++j) {
-        uint32_t wd = mrow[j];
-        if (j == nw - 1 && (len & 31)) wd &= (1u << (len & 31)) - 1u;
-        any |= wd;
-      }
-      rows_live = __all(any != 0u);
-    }
     // prologue: K0 V0 M0 K1 V1 M1 K2 (as many as exist; M = mask words, masked launches only)
     issue(0, false, lds0 + kslot(0));
     issue(0, true, lds0 + vslot(0));
@@ -449,21 +430,6 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && (NP
         issue(kt + 3, false, lds0 + KS_ISS);
         n_iss += DM;
       }
-      // PIPE 73: this tile's mask words (issued two iterations ago, landed at the last wait):
-      // skip its work when no query of the wave attends any of its keys (tile 0 never)
-      bool skip_c = false;
-      if constexpr (SKIP) {
-        if (rows_live && kt > 0) {
-          uint32_t mb = *reinterpret_cast<const uint32_t*>(lds + MASK_OFF + (R % 3) * 1024 +
-                                                            wave * 256 + 4 * li);
-          const int rem = len - kt * KT;
-          if (rem < KT) mb &= (1u << rem) - 1u;
-          skip_c = !__any(mb != 0u);
-        }
-      }
-      if (SKIP && skip_c) {  // this tile adds nothing: only the next tile's S
-        s_mfma(lds + KS_NEXT, s_next);
-      } else {
       // deferred rescale (cdna_hip_programming.md T13): keep the running max unless some row's
       // tile max exceeds it by more than 8 (log2 domain), so P <= 2^8 and the O rescale runs only
       // on the tiles that move a max by that much — the same softmax with another reference max
@@ -539,7 +505,6 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && (NP
         for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
       }
       pv_mfma(lds + VS_CUR, ph, pl);
-      }
       wait_vm(n_iss);  // V_{kt+1}, K_{kt+2} landed; this iteration's DMA stays in flight
       barrier();
     };
@@ -689,7 +654,7 @@ hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op
   if (np != 1 && np != 2) return hipErrorInvalidValue;
   dim3 grid((max_q + QPB - 1) / QPB, heads, n), block(256);
 #define APP_LAUNCH(N, M, PL)                                                                 \
-  hipLaunchKernelGGL((attn_pp_kernel<N, M, PL, M ? (PIPE == 72 || PIPE == 73 ? PIPE : PIPE >= 60 ? 66 : 4) : (PIPE == 73 ? 67 : PIPE)>), grid, block, 0, \
+  hipLaunchKernelGGL((attn_pp_kernel<N, M, PL, M ? (PIPE == 72 ? 72 : PIPE >= 60 ? 66 : 4) : PIPE>), grid, block, 0, \
                      stream, qkvp, out, op, cu,                                                 \
                      q_rows, mask, mask_L)
 #define APP_MP(N)                                                      \
@@ -727,7 +692,11 @@ hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op
 // add chain) 188.5 / 188.2 vs 187.3 / 188.7 (profiles/r3ao_attn_psum2_ab.jsonl), and other
 // interleaves of the next S MFMAs with the exp / split (8 or 3 vector instructions per MFMA, or
 // the compiler's own order: 181.2 / 181.6 / 183.7 vs 179.8 / 179.5 us,
-// profiles/r3as_attn_interleave_ab.jsonl): not kept.
+// profiles/r3as_attn_interleave_ab.jsonl): not kept.  Round 4: loop 73 — masked launches
+// skipping key tiles no query of the wave attends (bit-identical to 66 when every row of the
+// wave attends some key) — measured 347 vs 324 us on GraphCodeBERT-shaped masks and 352 vs 325
+// on random ones at B=64 x L=640 (the if / else around the tile's work costs 38 registers and
+// the schedule more than the skipped tiles return; tools/attn_bench.py --mask --mask-gcb): removed.
 constexpr int APP_PIPE = 67;
 }  // namespace
 
@@ -757,7 +726,6 @@ extern "C" hipError_t ae_bench_attention_pp(const unsigned short* qkvp, float* o
     case 69: return app_launch<69>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
     case 70: return app_launch<70>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
     case 72: return app_launch<72>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
-    case 73: return app_launch<73>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
     default: break;
   }
   return hipErrorInvalidValue;

@@ -209,7 +209,7 @@ def _qkv_planes(qkv, np_):
     return _pack(hi, lo, np_)
 
 
-@pytest.mark.parametrize("variant", [6, 66, 67, 69, 70, 72, 73])
+@pytest.mark.parametrize("variant", [6, 66, 67, 69, 70, 72])
 @pytest.mark.parametrize("np_", [2, 1])
 @pytest.mark.parametrize("case", ["ragged", "mask", "cls", "planes", "grow"])
 def test_attention_pp_matches_f64(gpu, np_, case, variant):
@@ -315,76 +315,6 @@ def test_attention_pp_restructured_loops_bit_identical(gpu, case):
     assert torch.equal(outs[69], outs[6])  # the O rescale before the exp / S region
     assert torch.equal(outs[70], outs[6])  # the same at two workgroups per CU
     assert torch.equal(outs[72], outs[6])  # exp / split and the next S MFMAs hand-interleaved
-
-
-def _gcb_dense(g, n, L, lens, nodes, dead=()):
-    """GraphCodeBERT-shaped masks (utils.py:547-570): the last `nodes` positions of a sequence
-    are data-flow nodes attending 1-3 code tokens (which attend them back) and 1-2 other nodes;
-    code rows attend every code row; rows 0 and ncode-1 (special tokens) attend everything.
-    `dead`: (sequence, node) pairs whose row attends nothing (a truncated node)."""
-    dense = torch.zeros(n, L, L, dtype=torch.bool)
-    for s_, ln in enumerate(lens):
-        nd = min(nodes, ln // 4)
-        nc = ln - nd
-        dense[s_, :nc, :nc] = True
-        dense[s_, 0, :ln] = True
-        dense[s_, nc - 1, :ln] = True
-        for i in range(nd):
-            a = int(torch.randint(1, max(2, nc - 3), (1,), generator=g))
-            b = a + int(torch.randint(1, 4, (1,), generator=g))
-            dense[s_, nc + i, a:b] = True
-            dense[s_, a:b, nc + i] = True
-            for _ in range(int(torch.randint(1, 3, (1,), generator=g))):
-                dense[s_, nc + i, nc + int(torch.randint(0, nd, (1,), generator=g))] = True
-    for s_, i in dead:
-        nc = lens[s_] - min(nodes, lens[s_] // 4)
-        dense[s_, nc + i, :] = False
-    return dense
-
-
-@pytest.mark.parametrize("np_", [2, 1])
-@pytest.mark.parametrize("kind", ["gcb", "gcb_dead", "random"])
-def test_attention_pp_masked_tile_skip_bit_identical(gpu, np_, kind):
-    """Loop 73 skips every key tile that no query of a wave attends (GraphCodeBERT node rows see a
-    few code tokens; code rows see few nodes) when each of the wave's rows attends something: its
-    packed-plane context must equal loop 66's bit for bit — GraphCodeBERT-shaped masks over
-    ragged lengths, the same with rows that attend nothing (their waves skip nothing: uniform
-    attention over all keys, as HF's finfo.min mask), and random masks."""
-    lib = _lib()
-    vp, i32 = ctypes.c_void_p, ctypes.c_int32
-    lib.ae_bench_attention_pp.argtypes = [vp] * 5 + [i32] * 3 + [vp, i32, i32, i32, vp]
-    lib.ae_bench_attention_pp.restype = ctypes.c_int
-    g = torch.Generator().manual_seed(73 + np_)
-    L = 640
-    lens = [640, 333, 97, 512, 40]
-    n = len(lens)
-    if kind == "random":
-        dense = torch.rand(n, L, L, generator=g) < 0.3
-    else:
-        dead = ((0, 3), (0, 60), (3, 100)) if kind == "gcb_dead" else ()
-        dense = _gcb_dense(g, n, L, lens, 128, dead)
-    words = (dense.view(n, L, L // 32, 32).long() << torch.arange(32)).sum(-1)
-    dmask = (words - (words >= 2 ** 31).long() * 2 ** 32).to(torch.int32).cuda()
-    cu = torch.zeros(n + 1, dtype=torch.int32)
-    cu[1:] = torch.cumsum(torch.tensor(lens), 0)
-    T = int(cu[-1])
-    qkv = torch.randn(T, 3 * 768, generator=g)
-    dq, dcu = _qkv_planes(qkv, np_).cuda(), cu.cuda()
-    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    outs = {}
-    for v in (66, 73):
-        op = torch.zeros((T, np_ * 768), dtype=torch.int16, device="cuda")
-        assert lib.ae_bench_attention_pp(_p(dq), None, _p(op), _p(dcu), None, max(lens), n, 12,
-                                         _p(dmask), L, np_, v, st) == 0
-        outs[v] = op
-    torch.cuda.synchronize()
-    assert torch.equal(outs[73], outs[66])
-    if kind == "gcb_dead":  # the dead rows attended every key uniformly
-        ref = _attn_ref(qkv, cu, n, words, L)
-        got = _unpack(outs[73].view(torch.bfloat16).cpu(), np_, 768)
-        row = int(cu[0]) + lens[0] - 128 + 3
-        tol = 2e-4 if np_ == 2 else 2e-2
-        assert (got[row] - ref[row]).abs().max() <= tol
 
 
 @pytest.mark.parametrize("M,K,np_", [(300, 768, 2), (512, 3072, 2), (1000, 768, 1), (37, 768, 2),
