@@ -103,7 +103,7 @@ __device__ __forceinline__ int vpos(int r, int x) {
 // instructions).  Kept only as the mask path of the PIPE 6 reference (bench variant 6).
 // PIPE 6 / 66 / 67: below (67 is the production loop).
 template <int NP, bool HAS_MASK, bool PLANES, int PIPE>
-__global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && NP == 2)) ? 3 : 2) void attn_pp_kernel(const unsigned short* __restrict__ qkvp,
+__global__ __launch_bounds__(256, (PIPE >= 60 && !(HAS_MASK && NP == 2)) ? 3 : 2) void attn_pp_kernel(const unsigned short* __restrict__ qkvp,
                                                          float* __restrict__ out,
                                                          unsigned short* __restrict__ op,
                                                          const int* __restrict__ cu,
@@ -115,12 +115,11 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && NP 
   // PIPE 66: PIPE 6 with saddr DMA (per-lane offsets computed once, tiles advanced on the scalar
   // unit) and the cross-half row max by v_permlane32_swap instead of an LDS permute.
   // PIPE 67: 66 with the tile max as a 3-level tree of v_max3 (depth 3 instead of a chain of 8).
-  static_assert(PIPE == 4 || PIPE == 6 || PIPE == 66 || PIPE == 67 || PIPE == 69 || PIPE == 70 ||
-                    PIPE == 72,
-                "loop variants 4, 6, 66, 67, 69, 70, 72");
+  static_assert(PIPE == 4 || PIPE == 6 || PIPE == 66 || PIPE == 67 || PIPE == 72,
+                "loop variants 4, 6, 66, 67, 72");
   constexpr int PB = PIPE >= 60 ? 6 : PIPE;
   constexpr bool FAST = PIPE >= 60;
-  constexpr bool TREE = PIPE == 67 || (PIPE >= 69 && PIPE <= 72);
+  constexpr bool TREE = PIPE == 67 || PIPE == 72;
   static_assert(!(HAS_MASK && PB == 6 && !FAST),
                 "PIPE 6 has no mask path (its loop keeps no ordinary global load, so its mask "
                 "launches run PIPE 4); PIPE 66 moves the mask words by LDS-DMA");
@@ -474,11 +473,12 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && NP 
         m_new = grow ? fmaxf(m_run, mt) : m_run;
         alpha = __builtin_amdgcn_exp2f(m_run - m_new);  // 1 when m_new == m_run; 0 from -inf
       }
-      // PIPE 69: the rare O rescale BEFORE the region, so no branch separates tile kt's exp /
-      // split from tile kt+1's S MFMAs and this tile's PV (in PIPE 67 the compiler sank the exp /
+      // PIPE 72: the rare O rescale BEFORE the region, so no branch separates tile kt's exp /
+      // split from tile kt+1's S MFMAs and this tile's PV (in PIPE 67 the compiler sinks the exp /
       // split past the rescale branch, leaving the 12 S MFMAs back to back and the VALU chained
-      // into the PV MFMAs that consume it)
-      if ((PIPE >= 69 && PIPE <= 72) && grow) {
+      // into the PV MFMAs that consume it; that reorder alone, round-4 loop 69, measured 225.8 vs
+      // 184.9 us, and at two workgroups per CU, loop 70, 190.9: profiles/r4g_attn_ab.jsonl)
+      if (PIPE == 72 && grow) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
       }
@@ -500,7 +500,7 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && PIPE != 70 && !(HAS_MASK && NP 
       __builtin_amdgcn_sched_barrier(0);
       l_run = l_run * alpha + psum;
       m_run = m_new;
-      if ((PIPE < 69 || PIPE > 72) && grow) {
+      if (PIPE != 72 && grow) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
       }
@@ -723,8 +723,6 @@ extern "C" hipError_t ae_bench_attention_pp(const unsigned short* qkvp, float* o
     case 6: return app_launch<6>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
     case 66: return app_launch<66>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
     case 67: return app_launch<67>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
-    case 69: return app_launch<69>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
-    case 70: return app_launch<70>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
     case 72: return app_launch<72>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
     default: break;
   }

@@ -791,12 +791,12 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
     e->split = !(sp && sp[0] == '0');
     const char* lag = std::getenv("AE_SPLIT_LAG");  // experiments: 1 (QKV) .. 7 (whole layer 0)
     if (lag && lag[0] >= '1' && lag[0] <= '7') e->split_lag = lag[0] - '0';
-    const char* av = std::getenv("AE_ATTN_VARIANT");  // A/B runs: 6, 66, 69, 70, 72 (67 = production)
+    const char* av = std::getenv("AE_ATTN_VARIANT");  // A/B runs: 6, 66, 72 (67 = production)
     if (av) {
       const int v = std::atoi(av);
-      if (v != 0 && v != 6 && v != 66 && v != 67 && v != 69 && v != 70 && v != 72) {
+      if (v != 0 && v != 6 && v != 66 && v != 67 && v != 72) {
         ae_destroy(e);
-        return fail(AE_EINVAL, "AE_ATTN_VARIANT must be 6, 66, 67, 69, 70 or 72 (the exact loops)");
+        return fail(AE_EINVAL, "AE_ATTN_VARIANT must be 6, 66, 67 or 72 (the exact loops)");
       }
       e->attn_variant = v == 67 ? 0 : v;
     }

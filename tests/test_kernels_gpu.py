@@ -209,7 +209,7 @@ def _qkv_planes(qkv, np_):
     return _pack(hi, lo, np_)
 
 
-@pytest.mark.parametrize("variant", [6, 66, 67, 69, 70, 72])
+@pytest.mark.parametrize("variant", [6, 66, 67, 72])
 @pytest.mark.parametrize("np_", [2, 1])
 @pytest.mark.parametrize("case", ["ragged", "mask", "cls", "planes", "grow"])
 def test_attention_pp_matches_f64(gpu, np_, case, variant):
@@ -304,7 +304,7 @@ def test_attention_pp_restructured_loops_bit_identical(gpu, case):
     dq, dcu = _qkv_planes(qkv, 2).cuda(), cu.cuda()
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     outs = {}
-    for v in (6, 66, 67, 69, 70, 72):
+    for v in (6, 66, 67, 72):
         op = torch.zeros((T, 2 * 768), dtype=torch.int16, device="cuda")
         assert lib.ae_bench_attention_pp(_p(dq), None, _p(op), _p(dcu), None, max(lens), n, 12,
                                          None, 0, 2, v, st) == 0
@@ -312,8 +312,6 @@ def test_attention_pp_restructured_loops_bit_identical(gpu, case):
     torch.cuda.synchronize()
     assert torch.equal(outs[66], outs[6])
     assert torch.equal(outs[67], outs[6])
-    assert torch.equal(outs[69], outs[6])  # the O rescale before the exp / S region
-    assert torch.equal(outs[70], outs[6])  # the same at two workgroups per CU
     assert torch.equal(outs[72], outs[6])  # exp / split and the next S MFMAs hand-interleaved
 
 
