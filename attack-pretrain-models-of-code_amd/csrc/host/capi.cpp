@@ -1,4 +1,5 @@
 // capi.cpp — extern "C" surface of libalert_host.so (include/alert_host.h).
+#include <algorithm>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -35,6 +36,11 @@ struct ah_example {
   std::unordered_map<std::string, int32_t> word_id[2];
   std::vector<int32_t> word_tok;
   std::vector<int32_t> word_off{0};
+  // the word ids of every line of the original text (its first word in the "first" BPE form
+  // when it is the text's first word), so a mutant re-splits only the lines its edits touch;
+  // first_line: the first line that has words (-2: not built yet)
+  std::vector<std::vector<int32_t>> line_ids;
+  int32_t first_line = -2;
 };
 
 namespace {
@@ -281,33 +287,102 @@ int32_t ah_example_mutants(ah_example* e, ah_tokenizer* t, int32_t mode, int32_t
   return n_mut;
 }
 
+namespace {
+// id of (word, first) in the example's word table, added with its token run on first sight
+int32_t word_lookup(ah_example* e, ah_tokenizer* t, const std::string& w, int first) {
+  auto it = e->word_id[first].find(w);
+  if (it != e->word_id[first].end()) return it->second;
+  const std::vector<int32_t>& run = t->t.word_ids(w, first);
+  const int32_t id = (int32_t)e->word_off.size() - 1;
+  e->word_tok.insert(e->word_tok.end(), run.begin(), run.end());
+  e->word_off.push_back((int32_t)e->word_tok.size());
+  e->word_id[first].emplace(w, id);
+  return id;
+}
+
+// the words of one line: py_split of its text (lines are joined by '\n', so the text's split is
+// the concatenation of its lines' splits), each word assembled in one reused buffer
+void line_words(ah_example* e, ah_tokenizer* t, const std::vector<uint32_t>& cps, int32_t line,
+                std::vector<int32_t>& out) {
+  thread_local std::string w;
+  w.clear();
+  int first = line == e->first_line ? 1 : 0;
+  for (uint32_t cp : cps) {
+    if (ah::py_isspace(cp)) {
+      if (!w.empty()) {
+        out.push_back(word_lookup(e, t, w, first));
+        first = 0;
+        w.clear();
+      }
+    } else {
+      ah::utf8_append(w, cp);
+    }
+  }
+  if (!w.empty()) out.push_back(word_lookup(e, t, w, first));
+}
+
+void ensure_line_ids(ah_example* e, ah_tokenizer* t) {
+  if (e->first_line != -2) return;
+  const auto& lines = e->ex.lines_cp;
+  e->first_line = -1;
+  for (size_t i = 0; i < lines.size() && e->first_line < 0; ++i)
+    if (!ah::py_split(ah::utf8_encode(lines[i], 0, lines[i].size())).empty())
+      e->first_line = (int32_t)i;
+  e->line_ids.assign(lines.size(), {});
+  for (size_t i = 0; i < lines.size(); ++i) line_words(e, t, lines[i], (int32_t)i, e->line_ids[i]);
+}
+
+// a substitute that cannot change which line holds the text's first word: non-empty, no
+// whitespace (py_isspace over the ASCII and the common Unicode spaces, conservatively)
+bool plain_sub(const char* s) {
+  if (!s || !*s) return false;
+  for (const unsigned char* p = (const unsigned char*)s; *p; ++p)
+    if (*p <= 0x20 || *p == 0x7f || *p >= 0x80) return false;
+  return true;
+}
+}  // namespace
+
 int32_t ah_example_mutant_words(ah_example* e, ah_tokenizer* t, int32_t mode, int32_t n_mut,
                                 const int32_t* pair_off, const char* const* tgts,
                                 const char* const* subs, int32_t L, int32_t* mut_words,
                                 int32_t cap_words, int32_t* mut_off, int32_t* lens_out) {
   if (!e || !t || !pair_off || !mut_off || !lens_out || L < 2) return fail("bad argument");
+  ensure_line_ids(e, t);
   std::string code;
   std::vector<int32_t> seq;
+  std::vector<std::string> tv, sv;
   mut_off[0] = 0;
   for (int32_t m = 0; m < n_mut; ++m) {
-    if (!build_mutant(e, mode, pair_off[m], pair_off[m + 1], tgts, subs, code))
-      return fail("single mode needs 1 pair per mutant");
-    const std::vector<std::string> words = ah::py_split(code);
-    int32_t ntok = 0, pads = 0;
-    for (size_t w = 0; w < words.size(); ++w) {
-      const int first = w == 0 ? 1 : 0;
-      auto it = e->word_id[first].find(words[w]);
-      int32_t id;
-      if (it == e->word_id[first].end()) {
-        const std::vector<int32_t>& run = t->t.word_ids(words[w], first);
-        id = (int32_t)e->word_off.size() - 1;
-        e->word_tok.insert(e->word_tok.end(), run.begin(), run.end());
-        e->word_off.push_back((int32_t)e->word_tok.size());
-        e->word_id[first].emplace(words[w], id);
-      } else {
-        id = it->second;
+    const size_t seq0 = seq.size();
+    const int32_t b = pair_off[m], end = pair_off[m + 1];
+    if (mode == AH_MODE_SINGLE && end - b != 1) return fail("single mode needs 1 pair per mutant");
+    bool plain = true;
+    for (int32_t k = b; k < end && plain; ++k) plain = plain_sub(subs[k]);
+    if (plain) {
+      // only the lines the edits touch are re-split (ASCII identifiers in, so the text's first
+      // word stays on first_line); the others reuse the original's word ids
+      tv.assign(tgts + b, tgts + end);
+      sv.assign(subs + b, subs + end);
+      auto edited = ah::edit_lines(e->ex, tv, sv);  // in line order
+      size_t q = 0;
+      for (int32_t i = 0; i < (int32_t)e->line_ids.size(); ++i) {
+        if (q < edited.size() && edited[q].first == i) {
+          line_words(e, t, edited[q].second, i, seq);
+          ++q;
+        } else {
+          seq.insert(seq.end(), e->line_ids[i].begin(), e->line_ids[i].end());
+        }
       }
-      seq.push_back(id);
+    } else {
+      if (!build_mutant(e, mode, b, end, tgts, subs, code))
+        return fail("single mode needs 1 pair per mutant");
+      const std::vector<std::string> words = ah::py_split(code);
+      for (size_t w = 0; w < words.size(); ++w)
+        seq.push_back(word_lookup(e, t, words[w], w == 0 ? 1 : 0));
+    }
+    int32_t ntok = 0, pads = 0;
+    for (size_t w = seq0; w < seq.size(); ++w) {
+      const int32_t id = seq[w];
       for (int32_t k = e->word_off[id]; k < e->word_off[id + 1]; ++k, ++ntok)
         if (ntok < L - 2 && e->word_tok[k] == t->t.pad_id) ++pads;  // literal "<pad>" text
     }

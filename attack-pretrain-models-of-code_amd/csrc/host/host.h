@@ -80,6 +80,10 @@ struct Example {
   std::vector<Leaf> leaves;        // lex(rcode): the leaves get_example(_batch) edits
   std::vector<Leaf> id_leaves;     // lex(remove_comments(rcode)): get_identifiers code tokens
   std::vector<std::vector<uint32_t>> lines_cp;  // rcode.split('\n') as code points
+  // leaf text -> indices into leaves, in leaf order (the edits get_example(_batch) makes for a
+  // name, without scanning every leaf per name)
+  std::unordered_map<std::string, std::vector<int>> leaf_index;
+  std::vector<std::vector<int>> line_leaves;  // leaf indices by start line, in leaf order
 };
 
 void example_init(Example& ex, const std::string& code, Lang lang);
@@ -89,6 +93,11 @@ std::string get_example(const Example& ex, const std::string& tgt, const std::st
 // get_example_batch (chromosome in dict order, run_parser.py:242-266)
 std::string get_example_batch(const Example& ex, const std::vector<std::string>& tgts,
                               const std::vector<std::string>& subs);
+// the lines either of them changes, in line order, with their new code points (every other
+// line of ex.lines_cp is unchanged); both are this plus a join
+std::vector<std::pair<int, std::vector<uint32_t>>> edit_lines(const Example& ex,
+                                                              const std::vector<std::string>& tgts,
+                                                              const std::vector<std::string>& subs);
 
 // ------------------------------------------------------------------------------------ DFG
 // One DFG_c entry (python_parser/parser_folder/DFG_c.py): (code, idx, 'comesFrom' |

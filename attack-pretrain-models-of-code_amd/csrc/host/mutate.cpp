@@ -10,6 +10,7 @@
 // code-point indices; lines are therefore kept as code-point arrays and indexed with byte columns.
 // get_example shifts the k-th same-line occurrence by k*diff; get_example_batch applies a line's
 // edits in chromosome-key order with a running diff (the documented offset quirk).
+#include <algorithm>
 #include "host.h"
 
 namespace ah {
@@ -134,60 +135,87 @@ void example_init(Example& ex, const std::string& code, Lang lang) {
   ex.id_leaves = lang == LANG_PYTHON ? ex.leaves : lex(remove_comments(ex.rcode), lang);
   ex.lines_cp.clear();
   for (auto& l : split_lines(ex.rcode)) ex.lines_cp.push_back(utf8_decode(l));
+  ex.leaf_index.clear();
+  ex.line_leaves.assign(ex.lines_cp.size(), {});
+  for (size_t i = 0; i < ex.leaves.size(); ++i) {
+    ex.leaf_index[ex.leaves[i].text].push_back((int)i);
+    if (ex.leaves[i].sl >= 0 && ex.leaves[i].sl < (int)ex.line_leaves.size())
+      ex.line_leaves[ex.leaves[i].sl].push_back((int)i);
+  }
 }
 
-std::string get_example(const Example& ex, const std::string& tgt, const std::string& sub) {
-  // replace_pos: line -> [(start_col, end_col)], dict insertion order
-  std::vector<int> line_order;
-  std::vector<std::vector<std::pair<int, int>>> pos_by_line(ex.lines_cp.size());
-  for (const Leaf& lf : ex.leaves) {
-    if (lf.text == tgt) {
-      if (pos_by_line[lf.sl].empty()) line_order.push_back(lf.sl);
-      pos_by_line[lf.sl].push_back({lf.sc, lf.ec});
-    }
+std::vector<std::pair<int, std::vector<uint32_t>>> edit_lines(const Example& ex,
+                                                              const std::vector<std::string>& tgts,
+                                                              const std::vector<std::string>& subs) {
+  // get_example(_batch) edits, per line, every occurrence of every chromosome name — names in
+  // chromosome order, a name's occurrences in leaf order — each shifted by the diffs applied
+  // before it on that line.  A line changes iff one of its edits changes the text: a name mapped
+  // to itself splices its own text back with diff 0, which alters nothing on a line where every
+  // edit is such, but after a real edit on the same line it lands shifted (the reference's
+  // offset quirk), so it is applied there like any other.
+  const size_t n = tgts.size();
+  std::unordered_map<std::string, int> name_k;
+  name_k.reserve(n * 2);
+  for (size_t k = 0; k < n; ++k) name_k.emplace(tgts[k], (int)k);
+  std::vector<int> touched;
+  for (size_t k = 0; k < n; ++k) {
+    if (tgts[k] == subs[k]) continue;
+    auto hit = ex.leaf_index.find(tgts[k]);
+    if (hit == ex.leaf_index.end()) continue;
+    for (int li : hit->second) touched.push_back(ex.leaves[li].sl);
   }
-  const std::vector<uint32_t> subcp = utf8_decode(sub);
-  const long diff = (long)subcp.size() - (long)utf8_decode(tgt).size();
+  std::sort(touched.begin(), touched.end());
+  touched.erase(std::unique(touched.begin(), touched.end()), touched.end());
+  std::vector<std::vector<uint32_t>> subcps(n);
+  std::vector<long> diffs(n, 0);
+  std::vector<char> decoded(n, 0);
+  struct Edit {
+    int k, li;
+  };
+  std::vector<Edit> edits;
+  std::vector<std::pair<int, std::vector<uint32_t>>> out;
+  out.reserve(touched.size());
+  for (int line : touched) {
+    edits.clear();
+    for (int li : ex.line_leaves[line]) {
+      auto it = name_k.find(ex.leaves[li].text);
+      if (it != name_k.end()) edits.push_back({it->second, li});
+    }
+    std::sort(edits.begin(), edits.end(),
+              [](const Edit& a, const Edit& b) { return a.k != b.k ? a.k < b.k : a.li < b.li; });
+    std::vector<uint32_t> l = ex.lines_cp[line];
+    long shift = 0;
+    for (const Edit& e : edits) {
+      if (!decoded[e.k]) {
+        subcps[e.k] = utf8_decode(subs[e.k]);
+        diffs[e.k] = (long)subcps[e.k].size() - (long)utf8_decode(tgts[e.k]).size();
+        decoded[e.k] = 1;
+      }
+      const Leaf& lf = ex.leaves[e.li];
+      splice_line(l, lf.sc + shift, lf.ec + shift, subcps[e.k]);
+      shift += diffs[e.k];
+    }
+    out.emplace_back(line, std::move(l));
+  }
+  return out;
+}
+
+namespace {
+std::string apply_edits(const Example& ex,
+                        std::vector<std::pair<int, std::vector<uint32_t>>>&& edited) {
   std::vector<std::vector<uint32_t>> lines = ex.lines_cp;
-  for (int line : line_order) {
-    long index = 0;
-    for (auto& p : pos_by_line[line]) {
-      splice_line(lines[line], p.first + index * diff, p.second + index * diff, subcp);
-      ++index;
-    }
-  }
+  for (auto& e : edited) lines[e.first] = std::move(e.second);
   return lines_to_string(lines);
+}
+}  // namespace
+
+std::string get_example(const Example& ex, const std::string& tgt, const std::string& sub) {
+  return apply_edits(ex, edit_lines(ex, {tgt}, {sub}));
 }
 
 std::string get_example_batch(const Example& ex, const std::vector<std::string>& tgts,
                               const std::vector<std::string>& subs) {
-  struct Edit {
-    const std::vector<uint32_t>* sub;
-    long diff;
-    int sc, ec;
-  };
-  std::vector<int> line_order;
-  std::vector<std::vector<Edit>> edits(ex.lines_cp.size());
-  std::vector<std::vector<uint32_t>> subcps(tgts.size());
-  for (size_t k = 0; k < tgts.size(); ++k) {
-    subcps[k] = utf8_decode(subs[k]);
-    const long diff = (long)subcps[k].size() - (long)utf8_decode(tgts[k]).size();
-    for (const Leaf& lf : ex.leaves) {
-      if (lf.text == tgts[k]) {
-        if (edits[lf.sl].empty()) line_order.push_back(lf.sl);
-        edits[lf.sl].push_back({&subcps[k], diff, lf.sc, lf.ec});
-      }
-    }
-  }
-  std::vector<std::vector<uint32_t>> lines = ex.lines_cp;
-  for (int line : line_order) {
-    long diff = 0;
-    for (auto& e : edits[line]) {
-      splice_line(lines[line], e.sc + diff, e.ec + diff, *e.sub);
-      diff += e.diff;
-    }
-  }
-  return lines_to_string(lines);
+  return apply_edits(ex, edit_lines(ex, tgts, subs));
 }
 
 std::vector<std::string> py_split(const std::string& s) {

@@ -152,16 +152,26 @@ def test_offset_quirk_reproduced():
     assert Example(code).mutant_text(list(chrom.items())) == exp
 
 
-def test_mutant_words_feed_the_same_ids(devign_small, tok):
-    from apmc_amd.host import Example
+@pytest.mark.parametrize("single", [False, True])
+def test_mutant_words_feed_the_same_ids(devign_small, tok, single):
+    """The device-splice inputs (word table + per-mutant word ids; only the lines a mutant's
+    edits touch are re-split, the others reuse the original's ids) give exactly the ids of the
+    text path (get_example(_batch) -> ' '.join(split()) -> BPE), in both edit modes, incl.
+    substitutes with spaces or non-ASCII text (the fallback that re-splits the whole text)."""
+    from apmc_amd.host import MODE_SINGLE, Example
     rng = random.Random(1)
-    for js in devign_small[:20]:
+    odd = ["a b", "ü", "x\ty", "<pad>"]
+    for js in devign_small[:40]:
         if not js["substitutes"]:
             continue
         ex = Example(js["func"])
         pops = [list(c.items()) for c in _random_chromosomes(js, rng, 5)]
-        ids, lens = ex.mutant_ids(tok, pops, 512)
-        word_tok, word_off, mut_words, mut_off, lens2 = ex.mutant_words(tok, pops, 512)
+        if single:
+            pops = [[p[0]] for p in pops if p]
+        pops.append([(pops[0][0][0], odd[rng.randrange(len(odd))])])
+        kw = {"mode": MODE_SINGLE} if single else {}
+        ids, lens = ex.mutant_ids(tok, pops, 512, **kw)
+        word_tok, word_off, mut_words, mut_off, lens2 = ex.mutant_words(tok, pops, 512, **kw)
         assert (lens == lens2).all()
         for m in range(len(pops)):
             ws = mut_words[mut_off[m]:mut_off[m + 1]]
