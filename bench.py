@@ -169,7 +169,39 @@ def host_cores():
 
 
 # ------------------------------------------------------------------------------------------ legs
-def time_steps(eng, ids_dev, lens, out, steps, warmup, dev, dist, profile):
+def single_stream_engine(sd, precision, dev):
+    """An engine with the encoder on one stream (AE_SPLIT_STREAMS=0 at creation): the kernels
+    a profiled pass times then run with nothing beside them."""
+    from apmc_amd.engine import Engine
+
+    prev = os.environ.get("AE_SPLIT_STREAMS")
+    os.environ["AE_SPLIT_STREAMS"] = "0"
+    try:
+        return Engine(sd, head="sigmoid1", num_labels=1, precision=precision, device=dev.index)
+    finally:  # the user's own setting stays in force for the later legs
+        if prev is None:
+            os.environ.pop("AE_SPLIT_STREAMS")
+        else:
+            os.environ["AE_SPLIT_STREAMS"] = prev
+
+
+def attention_summary(a_ms, a_n, steps, B, L, peak, where):
+    """Attention of the 11 full-length layers (4·L²·64 FLOP per (sequence, head): S = QKᵀ and
+    PV) over the time of every attention launch of the step, the CLS-only last layer's included
+    (conservative)."""
+    if not a_n:
+        return None
+    per_layer_flop = 4.0 * L * L * 64 * 12 * B
+    attn_ms = a_ms / steps
+    tf = 11 * per_layer_flop / attn_ms / 1e9
+    return {"ms_per_step": round(attn_ms, 4), "launches_per_step": a_n // steps,
+            "full_layer_algorithmic_gflop": round(per_layer_flop / 1e9, 2),
+            "algorithmic_tflops": round(tf, 2), "frac_of_peak": round(tf / peak, 4),
+            "timing": "HIP events on the launch stream around every attention launch (11 full "
+                      "layers + the CLS-only last layer), " + where}
+
+
+def time_steps(eng, ids_dev, lens, out, steps, warmup, dev, dist, profile, kind="gemm_ffn1"):
     import torch
 
     stream = torch.cuda.current_stream(dev)
@@ -178,7 +210,7 @@ def time_steps(eng, ids_dev, lens, out, steps, warmup, dev, dist, profile):
     torch.cuda.synchronize(dev)
     if profile:
         eng.kernel_time()  # drop anything recorded so far
-        eng.set_profiling("gemm_ffn1", True)  # events are created here, before the timed region
+        eng.set_profiling(kind, True)  # events are created here, before the timed region
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -191,7 +223,7 @@ def time_steps(eng, ids_dev, lens, out, steps, warmup, dev, dist, profile):
     elapsed = time.perf_counter() - t0
     kt = None
     if profile:
-        eng.set_profiling("gemm_ffn1", False)
+        eng.set_profiling(kind, False)
         kt = eng.kernel_time()
     return elapsed, kt
 
@@ -658,17 +690,18 @@ def microbench_leg(dev, precision, steps, warmup, world):
 
     peak = {"fp32": FP32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS,
             "f32x3": BF16_MFMA_PEAK_TFLOPS / 3}[precision]
-    eng = Engine(synthetic_state_dict(seed=0, head="sigmoid1"), head="sigmoid1", num_labels=1,
-                 precision=precision, device=dev.index)
+    sd = synthetic_state_dict(seed=0, head="sigmoid1")
+    eng = Engine(sd, head="sigmoid1", num_labels=1, precision=precision, device=dev.index)
     out = {}
 
-    def timed(fn, n_steps, kind=None):
+    def timed(fn, n_steps, kind=None, on=None):
+        on = on or eng
         for _ in range(warmup):
             fn()
         torch.cuda.synchronize(dev)
         if kind:
-            eng.kernel_time()
-            eng.set_profiling(kind, True)
+            on.kernel_time()
+            on.set_profiling(kind, True)
         t0 = time.perf_counter()
         for _ in range(n_steps):
             fn()
@@ -676,8 +709,8 @@ def microbench_leg(dev, precision, steps, warmup, world):
         el = time.perf_counter() - t0
         kt = None
         if kind:
-            eng.set_profiling(kind, False)
-            kt = eng.kernel_time()
+            on.set_profiling(kind, False)
+            kt = on.kernel_time()
         return el, kt
 
     def summary(rows_flop, rows, el, n_steps, what):
@@ -726,22 +759,21 @@ def microbench_leg(dev, precision, steps, warmup, world):
     gi, gp, gb = synthetic_gcb_batch(64)
     gi_d, gp_d, gb_d = (torch.from_numpy(a).to(dev) for a in (gi, gp, gb))
     glens = np.full((64,), 640, np.int32)
-    el, (a_ms, a_n, _) = timed(lambda: eng.score_graph(gi_d, glens, gp_d, gb_d, out=ov), steps,
-                               kind="attention")
+    el, _ = timed(lambda: eng.score_graph(gi_d, glens, gp_d, gb_d, out=ov), steps)
     res = summary(flops_per_query(640) * 64, 64, el, steps,
                   "GraphCodeBERT step: B = 64 x L = 640 (512 code + 128 data-flow nodes, 1-3 code "
                   "tokens and 1-2 edges per node, seed 0), bit-packed mask, node averaging")
-    # attention of the 11 full-length masked layers (4·L²·64 per (sequence, head)) over the time
-    # of every attention launch of the step (the CLS-only last layer's included: conservative)
-    per_layer_flop = 4.0 * 640 * 640 * 64 * 12 * 64
-    if a_n:
-        attn_ms = a_ms / steps
-        res["attention"] = {"ms_per_step": round(attn_ms, 4), "launches_per_step": a_n // steps,
-                            "full_layer_algorithmic_gflop": round(per_layer_flop / 1e9, 2),
-                            "algorithmic_tflops": round(11 * per_layer_flop / attn_ms / 1e9, 2),
-                            "frac_of_peak": round(11 * per_layer_flop / attn_ms / 1e9 / peak, 4),
-                            "timing": "HIP events on the engine stream around every attention "
-                                      "launch (11 masked full layers + the CLS-only last layer)"}
+    # the masked attention kernels timed where nothing runs beside them (in the two-stream engine
+    # a launch's events also span the other half's kernels sharing the CUs)
+    eng_s = single_stream_engine(sd, precision, dev)
+    ov_s = torch.empty_like(ov)
+    _, (a_ms, a_n, _) = timed(lambda: eng_s.score_graph(gi_d, glens, gp_d, gb_d, out=ov_s), steps,
+                              kind="attention", on=eng_s)
+    eng_s.close()
+    att = attention_summary(a_ms, a_n, steps, 64, 640, peak,
+                            f"single-stream engine, the same batch, {steps} steps")
+    if att:
+        res["attention"] = att
     out["gcb640"] = res
     log(f"microbench gcb640: {res['victim_queries_per_s']} q/s")
     eng.close()
@@ -806,18 +838,20 @@ def main():
     # streams (engine.hip run_encoder), so its FFN1 launches share the CUs with the other half's
     # kernels; FFN1 is timed (HIP events on its launch stream) on a single-stream engine over the
     # same batch, where nothing else runs beside it
-    prev_split = os.environ.get("AE_SPLIT_STREAMS")
-    os.environ["AE_SPLIT_STREAMS"] = "0"
-    eng1 = Engine(sd, head="sigmoid1", num_labels=1, precision=args.precision, device=dev.index)
-    if prev_split is None:  # the user's own setting stays in force for the later legs
-        os.environ.pop("AE_SPLIT_STREAMS")
-    else:
-        os.environ["AE_SPLIT_STREAMS"] = prev_split
+    eng1 = single_stream_engine(sd, args.precision, dev)
     out1 = torch.empty_like(out)
     n1 = max(5, args.steps // 2)
     el1, (k_ms, k_n, k_flop) = time_steps(eng1, ids_dev, lens, out1, n1, args.warmup, dev, dist,
                                           profile=True)
+    # the attention kernels of the same single-stream steps (11 full layers + the CLS-only last
+    # layer), HIP events on their launch stream
+    _, (at_ms, at_n, _) = time_steps(eng1, ids_dev, lens, out1, n1, args.warmup, dev, dist,
+                                     profile=True, kind="attention")
     eng1.close()
+    if dist is not None:
+        t = torch.tensor([at_ms], dtype=torch.float64, device=COLL_DEV)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        at_ms = float(t.item())
     if dist is not None:
         t = torch.tensor([elapsed, el1], dtype=torch.float64, device=COLL_DEV)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -836,6 +870,8 @@ def main():
     # 3 bf16 MFMAs per product, so its ceiling in algorithmic FLOP/s is the bf16 peak / 3
     peak = {"fp32": FP32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS,
             "f32x3": BF16_MFMA_PEAK_TFLOPS / 3}[args.precision]
+    attention = attention_summary(at_ms, at_n, n1, B, L, peak,
+                                  f"single-stream engine, the same batch, {n1} steps")
     fp32_mode = bf16_mode = None
     if args.precision != "fp32" and not args.no_fp32_mode:
         # the exact-fp32 mode of the same step, and the split / bf16 parity on this very batch
@@ -913,6 +949,7 @@ def main():
                            "the CUs with the other half's kernels",
             "two_stream_avg_launch_us": round(1e3 * s_ms / max(s_n, 1), 2) if s_n else None,
         },
+        "attention": attention,
         "whole_step_executed_tflops": round(executed, 3),
         "whole_step_frac_of_peak": round(executed / world / peak, 4),
         "probs_checksum": float(np.round(probs.astype(np.float64).sum(), 6)),
