@@ -64,10 +64,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--check-seqs", type=int, default=8)
+    ap.add_argument("--lib", default=None, help="engine library to load (A/B of kernel sources)")
     args = ap.parse_args()
 
     from apmc_amd.engine import load_library
-    lib = load_library()
+    lib = load_library(args.lib)
     vp, i32 = ctypes.c_void_p, ctypes.c_int32
     fn = lib.ae_bench_attention_x3
     fn.argtypes = [vp] * 5 + [i32] * 3 + [vp, i32, i32, i32, vp]
