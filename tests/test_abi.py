@@ -53,3 +53,75 @@ def test_libraries_built_from_this_tree():
     host = ctypes.CDLL(str(HOSTLIB_PATH))
     host.ah_source_hash.restype = ctypes.c_char_p
     assert host.ah_source_hash().decode() == source_hash("host")
+
+
+def _lib():
+    from apmc_amd.engine import load_library
+    return load_library()
+
+
+def _err(lib):
+    lib.ae_last_error.restype = ctypes.c_char_p
+    return lib.ae_last_error().decode()
+
+
+def test_argument_errors_before_any_device_call():
+    """Every entry point validates its arguments before the first HIP call and reports
+    AE_EINVAL (-22) with a message in ae_last_error() — the error contract include/alert_engine.h
+    states; these calls never reach the device, so they run here without a GPU."""
+    from apmc_amd.engine import AE_HEAD, AE_PREC, AeConfig
+    lib = _lib()
+    EINVAL = -22
+    buf = (ctypes.c_int32 * 64)()
+    fbuf = (ctypes.c_float * 64)()
+    p = ctypes.cast(buf, ctypes.c_void_p)
+    fp = ctypes.cast(fbuf, ctypes.c_void_p)
+
+    def cfg(**kw):
+        c = dict(layers=12, hidden=768, heads=12, ffn=3072, vocab=50265, max_pos=514, type_vocab=1,
+                 num_labels=1, head_kind=AE_HEAD["sigmoid1"], precision=AE_PREC["f32x3"], pad_id=1,
+                 with_mlm=0, ln_eps=1e-5)
+        c.update(kw)
+        return AeConfig(**c)
+
+    out = ctypes.c_void_p()
+    for bad, msg in ((dict(hidden=1024), "hidden=768"), (dict(heads=16), "hidden=768"),
+                     (dict(ffn=3000), "ffn"), (dict(layers=0), "ffn/layers"),
+                     (dict(num_labels=0), "num_labels"), (dict(num_labels=2), "sigmoid head"),
+                     (dict(head_kind=AE_HEAD["pair2"]), "pair head"),
+                     (dict(precision=7), "precision")):
+        c = cfg(**bad)
+        assert lib.ae_create(ctypes.byref(c), None, 0, 0, ctypes.byref(out)) == EINVAL, bad
+        assert msg in _err(lib), (bad, _err(lib))
+    c = cfg()
+    assert lib.ae_create(None, None, 0, 0, ctypes.byref(out)) == EINVAL
+    assert lib.ae_create(ctypes.byref(c), None, 3, 0, ctypes.byref(out)) == EINVAL
+    assert "null argument" in _err(lib)
+    # scoring / encoding on a null engine, null inputs, bad shapes
+    assert lib.ae_score(None, p, p, None, None, 4, 512, fp, None) == EINVAL
+    assert "null engine" in _err(lib)
+    assert lib.ae_score_graph(None, p, p, None, None, 4, 640, fp, None) == EINVAL
+    assert "pos and mask_bits" in _err(lib)
+    assert lib.ae_encode_ex(None, p, p, 4, 512, 0, 0, 1, fp, None) == EINVAL
+    assert lib.ae_set_profiling(None, 0, 1) == EINVAL
+    # standalone kernels: shapes checked before launch
+    assert lib.ae_topk(fp, 1, 10, 0, fp, p, None) == EINVAL and "bad shape" in _err(lib)
+    assert lib.ae_topk(fp, 1, 10, 11, fp, p, None) == EINVAL
+    assert lib.ae_topk(fp, 1, 1000, 257, fp, p, None) == EINVAL
+    assert lib.ae_topk(None, 1, 10, 5, fp, p, None) == EINVAL and "null" in _err(lib)
+    assert lib.ae_splice(p, p, p, p, 4, 1, 0, 2, 1, p, p, None) == EINVAL
+    assert lib.ae_splice(p, None, p, p, 4, 512, 0, 2, 1, p, p, None) == EINVAL
+    assert lib.ae_graph_mask(p, p, p, p, 2, 100, 4, p, None) == EINVAL  # L % 32
+    assert lib.ae_graph_mask(p, p, p, p, 2, 2048, 4, p, None) == EINVAL  # L > 1024
+    assert lib.ae_graph_mask(p, p, p, p, 2, 640, 0, p, None) == EINVAL  # e_cap < 1
+    assert lib.ae_cosine_rank(fp, fp, 4, 0, 768, ctypes.c_float(1e-8), fp, None) == EINVAL
+
+
+def test_engine_refuses_to_run_without_a_gpu():
+    """The product path fails loudly when there is no device: no CPU fallback."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from apmc_amd.engine import Engine
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        Engine({}, head="sigmoid1", num_labels=1, precision="f32x3")
