@@ -361,3 +361,23 @@ def test_qkv192_tiles_bit_identical(gpu, monkeypatch, split):
         assert np.array_equal(_score(engines["1"], ids), _score(engines["0"], ids))
     for e in engines.values():
         e.close()
+
+
+def test_bench_size_batch_properties(gpu):
+    """At the bench's full sizes (config-2 rows of L = 512; the batch-1024 microbenchmark), the
+    properties that do not need the oracle to run the whole batch: one 1024-row call equals
+    sixteen 64-row calls bit for bit (the two-stream parts, tile rounds and split-K forms change
+    with the batch, the arithmetic per row does not), every row of the f32x3 step is within the
+    north-star tolerance of the exact-fp32 mode, and the first and last rows match the oracle."""
+    rng = np.random.default_rng(0)
+    n, L = 1024, 512
+    ids = rng.integers(4, 50264, size=(n, L)).astype(np.int32)  # bench.py's id recipe
+    ids[:, 0], ids[:, -1] = 0, 2
+    eng = _engine(0, "sigmoid1", precision="f32x3")
+    big = _score(eng, ids)
+    chunks = np.concatenate([_score(eng, ids[i:i + 64]) for i in range(0, n, 64)])
+    assert np.array_equal(big, chunks), np.abs(big - chunks).max()
+    exact = _score(_engine(0, "sigmoid1", precision="fp32"), ids)
+    np.testing.assert_allclose(big, exact, atol=PROB_TOL, rtol=0)
+    ref = ora.score(synthetic_sd(0, "sigmoid1"), ids[[0, n - 1]], "sigmoid1")
+    np.testing.assert_allclose(big[[0, n - 1]], ref, atol=PROB_TOL, rtol=0)
