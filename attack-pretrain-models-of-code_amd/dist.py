@@ -193,11 +193,18 @@ def merge_csv_shards(dist, rank, world, path):
         header, rows = None, []
         for r in range(world):
             shard = f"{path}.rank{r}"
+            if not os.path.exists(shard):  # a rank that never opened its Recorder
+                continue
             with open(shard, newline="") as f:
                 rd = csv.reader(f)
-                header = next(rd)
-                rows.extend(rd)
+                head = next(rd, None)
+                if head is not None:
+                    header = head
+                    rows.extend(rd)
             os.remove(shard)
+        if header is None:
+            from .utils import Recorder
+            header = Recorder.HEADER
         rows.sort(key=lambda row: int(row[0]))
         with open(path, "w", newline="") as f:
             w = csv.writer(f)
@@ -231,12 +238,13 @@ def run_sharded_gi_batched(model, codes, subs, labels, args, max_inflight=64, de
     return merge_records(recs), tot
 
 
-def run_sharded_mhm(model, codes, subs, labels, args, n_candi=30, max_iter=100, prob_threshold=1,
+def run_sharded_mhm(model, codes, subs, labels, args, n_candi=30, max_iter=None, prob_threshold=1,
                     original=False, max_inflight=64, device=None, n: int | None = None,
                     key: str = "apmc_mhm_queue"):
     """run_mhm_attack (cross-example batched MHM-NS chains) over all ranks with one dynamic
     queue over examples [0, n) — per-example MCMC cost is as skewed as GA's (a success after one
-    round vs 100 rounds of 31 candidates).  Returns (merged records, job totals)."""
+    round vs 100 rounds of 31 candidates).  max_iter None = the task driver's own count
+    (drivers.MHM_MAX_ITER).  Returns (merged records, job totals)."""
     from .drivers import run_mhm_attack
 
     dist, rank, world = _rank_world()

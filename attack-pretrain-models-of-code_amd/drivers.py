@@ -198,6 +198,10 @@ class _InOrderWriter:
     def records(self):
         return [self.rows[i] for i in sorted(self.rows)]
 
+    def close(self):
+        if self.recorder is not None:
+            self.recorder.close()
+
 
 def _source(order, queue, writer):
     pos = 0
@@ -244,7 +248,10 @@ def run_gi_attack_batched(model, codes, subs, labels, args: AttackArgs, indices=
             log(_record(index, res, attack_type, queries, dt, None))
         writer.finish(index, lambda rec: _record(index, res, attack_type, queries, dt, rec))
 
-    run_requests(model, _source(order, queue, writer), start, on_done, max_inflight, pipeline)
+    try:
+        run_requests(model, _source(order, queue, writer), start, on_done, max_inflight, pipeline)
+    finally:
+        writer.close()
     return _totals(writer.records(), time.time() - t0)
 
 
@@ -261,25 +268,30 @@ def run_gi_attack(model, codes, subs, labels, args: AttackArgs, indices=None, to
     records = []
     t0 = time.time()
     pos = 0
-    while True:
-        if queue is not None:
-            index = queue()
-            if index is None:
-                break
-        else:
-            if pos >= len(order):
-                break
-            index = order[pos]
-            pos += 1
-        if args.rng == "per_example":
-            random.seed(args.seed + index)
-        q0 = model.query
-        ts = time.time()
-        res, attack_type = attack_one(attacker, tok, codes[index], subs[index], labels[index], args)
-        records.append(_record(index, res, attack_type, model.query - q0, (time.time() - ts) / 60,
-                               recorder))
-        if log:
-            log(records[-1])
+    try:
+        while True:
+            if queue is not None:
+                index = queue()
+                if index is None:
+                    break
+            else:
+                if pos >= len(order):
+                    break
+                index = order[pos]
+                pos += 1
+            if args.rng == "per_example":
+                random.seed(args.seed + index)
+            q0 = model.query
+            ts = time.time()
+            res, attack_type = attack_one(attacker, tok, codes[index], subs[index], labels[index],
+                                          args)
+            records.append(_record(index, res, attack_type, model.query - q0,
+                                   (time.time() - ts) / 60, recorder))
+            if log:
+                log(records[-1])
+    finally:
+        if recorder is not None:
+            recorder.close()
     return _totals(records, time.time() - t0)
 
 
@@ -308,6 +320,14 @@ def make_mhm_attacker(args, model, tok, codes):
     return MHM_ATTACKERS[task](args, model, None, tok, token2id, id2token)
 
 
+def _record_key_error(args, task):
+    """on_error = "record" turns a chain's KeyError into is_success -5 for the one copy that is
+    documented to raise it (GraphCloneMHM_Attacker: GraphCodeBERT/clonedetection/code/
+    attacker.py never skips a candidate naming a variable); any other task's KeyError is a bug
+    and propagates."""
+    return getattr(args, "on_error", "raise") == "record" and task == "gcb_clone"
+
+
 def mhm_one_gen(attacker, tok, code, subs, label, args, n_candi, max_iter, prob_threshold,
                 original, rng):
     """One example of mhm_attack.py:188-230 (Authorship mhm.py:192-233, clone mhm_attack.py:
@@ -322,7 +342,7 @@ def mhm_one_gen(attacker, tok, code, subs, label, args, n_candi, max_iter, prob_
         res = yield from attacker.chain_gen(tok, subs, code, label, example, n_candi, max_iter,
                                             prob_threshold, original, rng)
     except KeyError as e:
-        if getattr(args, "on_error", "raise") != "record":
+        if not _record_key_error(args, task):
             raise
         return -5, {"error": f"KeyError: {e}"}
     return (1 if res["succ"] else (-1 if res["succ"] is not None else -3)), res
@@ -340,7 +360,31 @@ def _mhm_call(attacker, task, tok, code, subs, label, example, n_candi, max_iter
     return fn(tok, subs, code=code, _label=label, **kw)
 
 
-def _mhm_record(index, code, task, res, label, queries, dt_min, recorder):
+# the task drivers whose writemhm call passes " ".join(_res['tokens']) — a string there, so every
+# character comes out space-separated (CodeXGLUE/Clone-detection-BigCloneBench/code/
+# mhm_attack.py:231, GraphCodeBERT/clonedetection/code/mhm_attack.py:221,
+# GraphCodeBERT/Authorship-Attribution/code/mhm_attack.py:229); the other three pass it as is
+MHM_JOINED_TOKENS = ("clone", "gcb_clone", "gcb_authorship")
+
+
+def writemhm_columns(task, code, tokens, last_code=None):
+    """(Original Code, Adversarial Code) of a writemhm row, with each task driver's own quirks:
+    CodeXGLUE clone writes "CODE1: ... ||CODE2: ..." of the example's pair (mhm_attack.py:231);
+    GraphCodeBERT clonedetection writes its leftover loop variable `code` — the LAST pair of
+    source_codes (mhm_attack.py:162 then :221; the pickled pair's element type is not in the
+    repository, a list is assumed: str(list(pair))); the rest write the example's code."""
+    if task == "clone":
+        text = ("CODE1: " + code[2].replace("\n", " ") + " ||CODE2: "
+                + code[3].replace("\n", " "))
+    elif task == "gcb_clone":
+        text = str(list(last_code if last_code is not None else code))
+    else:
+        text = code
+    adv = " ".join(tokens) if task in MHM_JOINED_TOKENS else tokens
+    return text, adv
+
+
+def _mhm_record(index, code, task, res, label, queries, dt_min, recorder, last_code=None):
     """One mhm_attack.py row (recoder.writemhm, :229) of a finished chain; res None: the
     example was skipped (-4 misclassified, or {'succ': None}: no substitutable name)."""
     if res is not None and "error" in res:
@@ -352,11 +396,8 @@ def _mhm_record(index, code, task, res, label, queries, dt_min, recorder):
                    replace_info=res["replace_info"], nb_changed_var=res["nb_changed_var"],
                    nb_changed_pos=res["nb_changed_pos"])
         if recorder is not None:
-            text = code
-            if _is_clone(task):  # Clone mhm_attack.py:229
-                text = ("CODE1: " + code[2].replace("\n", " ") + " ||CODE2: "
-                        + code[3].replace("\n", " "))
-            recorder.writemhm(index, text, res["prog_length"], res["tokens"], label,
+            text, adv = writemhm_columns(task, code, res["tokens"], last_code)
+            recorder.writemhm(index, text, res["prog_length"], adv, label,
                               res.get("orig_label", label), res["new_pred"], res["is_success"],
                               res["old_uid"], res["score_info"], res["nb_changed_var"],
                               res["nb_changed_pos"], res["replace_info"], res["attack_type"],
@@ -386,6 +427,23 @@ def run_mhm_attack(model, codes, subs, labels, args: AttackArgs, indices=None, t
     attacker = make_mhm_attacker(args, model, tok, codes)
     recorder = Recorder(args.csv_store_path) if args.csv_store_path else None
     order = list(range(len(codes))) if indices is None else list(indices)
+    try:
+        records, t0 = _run_mhm_loop(model, codes, subs, labels, args, attacker, tok, task, order,
+                                    recorder, n_candi, max_iter, prob_threshold, original,
+                                    max_inflight, queue)
+    finally:
+        if recorder is not None:
+            recorder.close()
+    correct = sum(r["is_success"] >= -1 for r in records)
+    succ = sum(r["is_success"] == 1 for r in records)
+    return dict(records=records, examples=len(records), total_cnt=correct, success=succ,
+                success_rate=(succ / correct) if correct else 0.0,
+                errors=sum(r["is_success"] == -5 for r in records),
+                queries=sum(r["queries"] for r in records), wall_s=time.time() - t0)
+
+
+def _run_mhm_loop(model, codes, subs, labels, args, attacker, tok, task, order, recorder, n_candi,
+                  max_iter, prob_threshold, original, max_inflight, queue):
     records, t0 = [], time.time()
     if max_inflight > 1 or queue is not None:
         from .batching import run_requests
@@ -400,7 +458,8 @@ def run_mhm_attack(model, codes, subs, labels, args: AttackArgs, indices=None, t
         def on_done(index, value, queries, ts):
             dt = (time.time() - ts) / 60
             writer.finish(index, lambda rec: _mhm_record(index, codes[index], task, value[1],
-                                                         labels[index], queries, dt, rec))
+                                                         labels[index], queries, dt, rec,
+                                                         codes[-1]))
 
         run_requests(model, _source(order, queue, writer), start, on_done, max(2, max_inflight))
         records = writer.records()
@@ -418,14 +477,10 @@ def run_mhm_attack(model, codes, subs, labels, args: AttackArgs, indices=None, t
             res = _mhm_call(attacker, task, tok, codes[index], subs[index], labels[index],
                             example, n_candi, max_iter, prob_threshold, original)
         except KeyError as e:
-            if args.on_error != "record":
+            if not _record_key_error(args, task):
                 raise
             res = {"error": f"KeyError: {e}"}
         records.append(_mhm_record(index, codes[index], task, res, labels[index],
-                                   model.query - q0, (time.time() - ts) / 60, recorder))
-    correct = sum(r["is_success"] >= -1 for r in records)
-    succ = sum(r["is_success"] == 1 for r in records)
-    return dict(records=records, examples=len(records), total_cnt=correct, success=succ,
-                success_rate=(succ / correct) if correct else 0.0,
-                errors=sum(r["is_success"] == -5 for r in records),
-                queries=sum(r["queries"] for r in records), wall_s=time.time() - t0)
+                                   model.query - q0, (time.time() - ts) / 60, recorder,
+                                   codes[-1]))
+    return records, t0

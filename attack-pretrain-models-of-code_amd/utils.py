@@ -283,6 +283,17 @@ class Recorder:
         self.f = open(file_path, "w")
         self.writer = csv.writer(self.f)
         self.writer.writerow(self.HEADER)
+        self.f.flush()  # a rank that writes no row still leaves a readable shard
+
+    def close(self) -> None:
+        if not self.f.closed:
+            self.f.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
     def write(self, index, code, prog_length, adv_code, true_label, orig_label, temp_label,
               is_success, variable_names, score_info, nb_changed_var, nb_changed_pos,

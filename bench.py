@@ -531,7 +531,7 @@ def aa_leg(dev, n_examples, n_gcb, rank, world, precision):
                                   f"programs [0, {len(gcodes)}), L = 640 with the data-flow mask")
         log("authorship leg: GraphCodeBERT MHM-NS")
         margs = AttackArgs(block_size=512, eval_batch_size=64, seed=123456, task="gcb_authorship",
-                           code_length=512, data_flow_length=128, on_error="record")
+                           code_length=512, data_flow_length=128)
         _, t = run_sharded_mhm(gmodel, gcodes, gsubs, glabels, margs, max_iter=100,
                                prob_threshold=1, max_inflight=128, device=dev,
                                key="bench_aa_gcb_mhm_queue")

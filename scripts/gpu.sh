@@ -34,7 +34,13 @@ for S in "$@"; do
            run pytest_gpu 1100 python -u -m pytest ${TESTS:-tests} -m gpu $XF -v --timeout 300 --timeout-method thread ${PYTEST_EXTRA:-} ${K:+-k "$K"}
            rc=$?
            # KEEPGOING=1: test FAILURES (pytest rc 1) do not end the call; a crash, abort or
-           # time limit (any other non-zero rc) still does
+           # time limit (any other non-zero rc) still does.  pytest-timeout's thread method ends
+           # a hung test with os._exit(1), so rc 1 counts as failures only when no timeout banner
+           # is in the log and pytest reached its final summary line.
+           if [ $rc -eq 1 ] && { grep -q '+++ Timeout +++' "$OUT/pytest_gpu.log" || \
+                                 ! grep -Eq '^=+ .*(failed|passed).* in [0-9.]+s' "$OUT/pytest_gpu.log"; }; then
+             echo "pytest_gpu: timeout or no final summary: not a plain test failure"; exit 124
+           fi
            if [ $rc -ne 0 ] && ! { [ "${KEEPGOING:-0}" = 1 ] && [ $rc -eq 1 ]; }; then exit $rc; fi ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench) run bench 1000 python -u bench.py ${BENCH_FULL_ARGS:-} || exit $? ;;

@@ -35,3 +35,10 @@ def gpu():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+@functools.lru_cache(maxsize=None)
+def golden512():
+    """transformers goldens at the attacks' block size (tests/golden/make_golden_encoder_512.py)."""
+    import numpy as np
+    return dict(np.load(ROOT / "tests" / "golden" / "encoder_golden_512.npz"))

@@ -60,6 +60,21 @@ def test_clone_pair_matches_golden(gpu):
     np.testing.assert_allclose(p, g["clone_probs"], atol=PROB_TOL, rtol=0)
 
 
+@pytest.mark.parametrize("precision", ["fp32", "f32x3"])
+@pytest.mark.parametrize("seed,head,num_labels,key", [(0, "sigmoid1", 1, "devign"),
+                                                      (1, "softmaxN", 66, "aa"),
+                                                      (2, "pair2", 2, "clone")])
+def test_heads_match_golden_at_block_512(gpu, precision, seed, head, num_labels, key):
+    """The headline config's length pinned to transformers directly (not only through the oracle):
+    rows of 512, 510, 300, 129 tokens, one with literal <pad> ids inside, for every head
+    (tests/golden/make_golden_encoder_512.py; ref CodeXGLUE/Defect-detection/code/model.py:24-34,
+    gi_attack.py:129-131)."""
+    from conftest import golden512
+    g = golden512()
+    p = _score(_engine(seed, head, num_labels, precision=precision), g[f"{key}_ids"])
+    np.testing.assert_allclose(p, g[f"{key}_probs"], atol=PROB_TOL, rtol=0)
+
+
 @pytest.mark.parametrize("L,lens", [(128, [128, 1 + 2, 77, 31, 128, 64, 100, 2, 33, 97]),
                                     (512, [512, 300, 511, 129])])
 def test_varlen_batch_matches_oracle(gpu, L, lens):

@@ -392,3 +392,50 @@ def test_dfg_python_known_answers():
     assert _names("for i in a:\n    k = i", "python") == ["i", "k"]
     # lambda parameters are not definitions (default parameters are)
     assert _names("g = lambda u, w=1: u", "python") == ["g", "w"]
+
+
+def _leaf_spans(code, leaves):
+    """(line, column) start / end of every leaf, found left to right in the code text — the
+    tree_to_token_index points (run_parser.py:199-204) of a lexer whose leaves are the text's."""
+    lines, spans, ln, col = code.split("\n"), [], 0, 0
+    for t in leaves:
+        while True:
+            c = lines[ln].find(t, col)
+            if c >= 0:
+                break
+            ln, col = ln + 1, 0
+        spans.append(((ln, c), (ln, c + len(t))))
+        col = c + len(t)
+    return spans
+
+
+def test_python_junda_known_answer():
+    """The reference's one known answer for the Python leaf lexer, python_parser/junda_test.md:1-18:
+    for its snippet, the occurrences of c, d, e, f are leaves c -> [5, 12], d -> [10, 17, 22],
+    e -> [15], f -> [20] at exactly the (line, column) spans listed there.  The same page's
+    name set includes the typed parameter `c: int`; DFG_python.py:19-27 defines a parameter
+    only when the identifier's parent is `parameters` (a `typed_parameter` is not), so
+    get_identifiers (run_parser.py:272-281) of the snippet is [d, e, f] — our graph says the
+    same (test_dfg_python_known_answers: typed parameters do not define)."""
+    from apmc_amd.host import Example
+    code = "import a\ndef b(c: int):\n    d = c + 10\n    e = d + 10\n    f = d + 20"
+    want = {
+        "c": ([5, 12], [((1, 6), (1, 7)), ((2, 8), (2, 9))]),
+        "d": ([10, 17, 22], [((2, 4), (2, 5)), ((3, 8), (3, 9)), ((4, 8), (4, 9))]),
+        "e": ([15], [((3, 4), (3, 5))]),
+        "f": ([20], [((4, 4), (4, 5))]),
+    }
+    ex = Example(code, "python")
+    for which in (0, 1):  # get_example's leaves and get_identifiers' (comment-stripped) leaves
+        leaves = ex.leaves(identifiers=bool(which))
+        spans = _leaf_spans(code, leaves)
+        for name, (idx, pos) in want.items():
+            got = [i for i, t in enumerate(leaves) if t == name]
+            assert got == idx, (name, got)
+            assert [spans[i] for i in got] == pos, (name, [spans[i] for i in got])
+    # every data-flow entry sits on one of those occurrences
+    leaves = ex.leaves(identifiers=True)
+    names = ex.dfg_names()
+    assert names == ["d", "e", "f"]
+    for i, _, _ in ex.dfg():
+        assert i in want[leaves[i]][0]

@@ -203,6 +203,16 @@ def test_mhm_variant_driver_batched_equals_sequential(task, tmp_path):
     rows = list(csv.reader(open(tmp_path / "bat.csv")))
     attacked = [r for r in seq if r["is_success"] in (1, -1)]
     assert len(rows) == 1 + len(attacked)
+    from apmc_amd.drivers import MHM_JOINED_TOKENS
     for row, r in zip(rows[1:], attacked):
         assert int(row[0]) == r["index"] and row[13] == r["attack_type"]
         assert int(row[14]) == r["queries"]
+        # each task driver's own writemhm columns (drivers.writemhm_columns)
+        adv = r["adv_code"]
+        assert row[3] == (" ".join(adv) if task in MHM_JOINED_TOKENS else adv)
+        if task == "clone":
+            assert row[1].startswith("CODE1: ") and " ||CODE2: " in row[1]
+        elif task == "gcb_clone":
+            assert row[1] == str(list(codes[-1]))
+        else:
+            assert row[1] == codes[r["index"]]

@@ -54,3 +54,19 @@ def test_pad_rows_do_not_change_cls():
 
 def test_flop_model():
     assert ora.flops_per_query(512, C=0) - 2 * 768 * 768 == 12 * (2 * 512 * 7077888 + 4 * 512 * 512 * 768)
+
+
+def test_heads_match_hf_at_block_512():
+    """The oracle at the headline config's own length (L = 512: full, 510, ragged 300 / 129, a row
+    with literal <pad> ids inside it) against transformers (make_golden_encoder_512.py)."""
+    from conftest import golden512
+    g = golden512()
+    sd = synthetic_sd(0, "sigmoid1")
+    h = ora.encoder_forward(sd, g["devign_ids"])
+    np.testing.assert_allclose(h[:, 0, :].numpy(), g["devign_cls"], atol=5e-5, rtol=0)
+    np.testing.assert_allclose(ora.head_forward(sd, h, "sigmoid1").numpy(), g["devign_probs"],
+                               atol=2e-6, rtol=0)
+    p = ora.score(synthetic_sd(1, "softmaxN", 66), g["aa_ids"], "softmaxN")
+    np.testing.assert_allclose(p, g["aa_probs"], atol=2e-6, rtol=0)
+    p = ora.score(synthetic_sd(2, "pair2", 2), g["clone_ids"], "pair2")
+    np.testing.assert_allclose(p, g["clone_probs"], atol=2e-6, rtol=0)
