@@ -9,6 +9,8 @@ import pathlib
 
 PKG_DIR = pathlib.Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "lib" / "libalert_engine.so"
+# the same sources built with -DAE_TOOLS: timing / A-B entry points (ae_bench_*) and AE_* knobs
+TOOLS_LIB_PATH = PKG_DIR / "lib" / "libalert_engine_tools.so"
 HOSTLIB_PATH = PKG_DIR / "lib" / "libalert_host.so"
 DATA_DIR = PKG_DIR.parent / "data"
 

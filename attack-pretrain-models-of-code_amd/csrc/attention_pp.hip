@@ -708,6 +708,8 @@ extern "C" hipError_t ae_launch_attention_pp(const unsigned short* qkvp, float* 
                               stream);
 }
 
+#ifdef AE_TOOLS
+// Tools library only (-DAE_TOOLS, lib/libalert_engine_tools.so).
 // Kernel experiments (tools/attn_bench.py, tests): 67 = the production loop, 66 = the same
 // without the tree row max, 6 = the round-3 loop both restructure bit-identically (its mask
 // launches run PIPE 4).  Earlier loops (0-5), the 8-wave ping-pong (7), 4 waves x 64 queries (8),
@@ -728,3 +730,4 @@ extern "C" hipError_t ae_bench_attention_pp(const unsigned short* qkvp, float* o
   }
   return hipErrorInvalidValue;
 }
+#endif  // AE_TOOLS

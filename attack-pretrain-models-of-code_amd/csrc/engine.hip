@@ -29,11 +29,11 @@ hipError_t ae_launch_attention_f32(const float*, float*, const int*, const int*,
                                    const uint32_t*, int, hipStream_t);
 hipError_t ae_launch_attention_pp(const unsigned short*, float*, unsigned short*, const int*,
                                   const int*, int, int, int, const uint32_t*, int, int, hipStream_t);
+#ifdef AE_TOOLS
 hipError_t ae_bench_attention_pp(const unsigned short*, float*, unsigned short*, const int*,
                                  const int*, int, int, int, const uint32_t*, int, int, int,
                                  hipStream_t);
-hipError_t ae_launch_attention_x3(const float*, float*, unsigned short*, const int*, const int*,
-                                  int, int, int, const uint32_t*, int, int, hipStream_t);
+#endif
 hipError_t ae_launch_gemm_packed(const unsigned short*, const unsigned short*, const float*,
                                  const float*, float*, unsigned short*, int, int, int, int, int,
                                  hipStream_t);
@@ -430,9 +430,11 @@ int gemm_pk_ln(ae_engine* e, const unsigned short* A, const unsigned short* Wp, 
 hipError_t attention_pp(ae_engine* e, const unsigned short* qkvp, float* out, unsigned short* op,
                         const int* cu, const int* q_rows, int max_q, int n, int heads,
                         const uint32_t* mask, int mask_L, int np, hipStream_t st) {
+#ifdef AE_TOOLS
   if (e->attn_variant && !mask)
     return ae_bench_attention_pp(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np,
                                  e->attn_variant, st);
+#endif
   return ae_launch_attention_pp(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, st);
 }
 
@@ -642,6 +644,8 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
     return fail(AE_EINVAL, "pair head needs num_labels=2");
   if (cfg->precision < AE_PREC_FP32 || cfg->precision > AE_PREC_F32X3)
     return fail(AE_EINVAL, "precision must be AE_PREC_FP32, AE_PREC_BF16 or AE_PREC_F32X3");
+  if (cfg->streams != AE_STREAMS_TWO && cfg->streams != AE_STREAMS_ONE)
+    return fail(AE_EINVAL, "streams must be AE_STREAMS_TWO or AE_STREAMS_ONE");
   HIPC(hipSetDevice(device));
   ae_engine* e = new ae_engine();
   e->cfg = *cfg;
@@ -776,6 +780,9 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
   HIPC(hipMemcpy(e->one, one_host, 16, hipMemcpyHostToDevice));
   HIPC(hipEventCreateWithFlags(&e->pinned_ready, hipEventDisableTiming));
   HIPC(hipEventRecord(e->pinned_ready, nullptr));
+#ifdef AE_TOOLS
+  // A/B knobs of the tools library (lib/libalert_engine_tools.so, tools/engine_ab.py and the
+  // alternative-form parity tests); the product library has the defaults compiled in
   {
     const char* ca = std::getenv("AE_CLS_ABSORB");  // A/B runs: 0 = full-T QKV + attention
     e->cls_absorb = !(ca && ca[0] == '0');
@@ -784,11 +791,15 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
     const char* q192 = std::getenv("AE_QKV192");  // A/B runs: 1 = 256 x 192 QKV tiles allowed
     e->qkv192 = q192 && q192[0] == '1';
   }
+#endif
   if (e->planes) {
-    // on unless AE_SPLIT_STREAMS=0 (tools/split_ab.py, profiles/r3s_split_streams_ab.json:
-    // B=64 x L=512 16.58 -> 16.35 ms per step, ragged lens 40..512 11.36 -> 9.53 ms)
+    // two streams unless cfg.streams == AE_STREAMS_ONE (tools/split_ab.py,
+    // profiles/r3s_split_streams_ab.json: B=64 x L=512 16.58 -> 16.35 ms per step, ragged lens
+    // 40..512 11.36 -> 9.53 ms)
+    e->split = e->cfg.streams != AE_STREAMS_ONE;
+#ifdef AE_TOOLS
     const char* sp = std::getenv("AE_SPLIT_STREAMS");
-    e->split = !(sp && sp[0] == '0');
+    if (sp && sp[0] == '0') e->split = false;
     const char* lag = std::getenv("AE_SPLIT_LAG");  // experiments: 1 (QKV) .. 7 (whole layer 0)
     if (lag && lag[0] >= '1' && lag[0] <= '7') e->split_lag = lag[0] - '0';
     const char* av = std::getenv("AE_ATTN_VARIANT");  // A/B runs: 6, 66, 72 (67 = production)
@@ -802,6 +813,7 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
     }
     const char* parts = std::getenv("AE_SPLIT_PARTS");  // experiments: 2 (default) .. 4
     if (parts && parts[0] >= '2' && parts[0] <= '4') e->split_parts = parts[0] - '0';
+#endif
     if (e->split) {
       HIPC(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
       for (int p = 0; p < ae_engine::kMaxParts; ++p) {

@@ -65,6 +65,14 @@ struct LnArgs {
                      // removed in round 4)
 };
 
+// The LayerNorm timing modes 1-4 exist only in the tools library (built with -DAE_TOOLS from
+// these sources, lib/libalert_engine_tools.so); the product library compiles mode 0 alone.
+#ifdef AE_TOOLS
+#define LN_MODE(a) ((a).mode)
+#else
+#define LN_MODE(a) 0
+#endif
+
 namespace {
 constexpr int PK_ROWB = 128;
 
@@ -526,7 +534,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
   const int tiles_n = (N + BN - 1) / BN;
   const int tiles_m = (M + BM - 1) / BM;
   int tm0, tn0;
-  if (EPI == PK_EPI_RES_LN && ln.mode != 2) {
+  if (EPI == PK_EPI_RES_LN && LN_MODE(ln) != 2) {
     // The 4 N-tiles of a 256-row block exchange row statistics, so they must be co-resident:
     // blocks b, b+8, b+16, b+24 (one XCD, consecutive in its in-order dispatch) take the row
     // block's 4 tiles; XCD x owns the contiguous row blocks [x * per, x * per + per) (mode 3:
@@ -534,7 +542,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
     // leave before any exchange (all four partners of one do).
     const int k = blockIdx.x >> 3, per = (tiles_m + 7) / 8;
     tn0 = k & 3;
-    tm0 = ln.mode == 3 ? (k >> 2) * 8 + (blockIdx.x & 7) : (blockIdx.x & 7) * per + (k >> 2);
+    tm0 = LN_MODE(ln) == 3 ? (k >> 2) * 8 + (blockIdx.x & 7) : (blockIdx.x & 7) * per + (k >> 2);
     if (tm0 >= tiles_m) return;
   } else {
     if (EPI == PK_EPI_RES_LN && (int)blockIdx.x >= tiles_m * tiles_n) return;
@@ -785,7 +793,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0 && ln.mode != 1) {
+    if (tid == 0 && LN_MODE(ln) != 1) {
       // release / acquire at agent scope around the exchange (the workgroup's statistics stores
       // are ordered before the arrival, the partners' after the wait)
       __hip_atomic_fetch_add(ln.arrive + tm0, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -810,7 +818,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
       RowStat p[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        p[q] = ln.mode == 1 ? tile[tm]
+        p[q] = LN_MODE(ln) == 1 ? tile[tm]
                             : __builtin_bit_cast(RowStat, __hip_atomic_load(
                                   ln.stats + (size_t)(rb0 + 32 * tm) * 4 + q, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT));
@@ -824,7 +832,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
       rstd[tm] = rsqrtf(var + ln.eps);
     }
     __syncthreads();  // every wave has read the statistics
-    if (tid == 0 && ln.mode != 1) {
+    if (tid == 0 && LN_MODE(ln) != 1) {
       // the last of the 4 partners to leave re-arms the counters for the next launch
       if (__hip_atomic_fetch_add(ln.depart + tm0, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
           tiles_n - 1) {
@@ -849,7 +857,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
           *reinterpret_cast<floatx4*>(reg + li * RS + (tn * 8 + 2 * j + lh) * 16) = o;
         }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (ln.mode == 4) {  // timing A/B only: the previous 4-column form (8-B plane stores)
+      if (LN_MODE(ln) == 4) {  // timing A/B only: the previous 4-column form (8-B plane stores)
 #pragma unroll
         for (int k = 0; k < 12; ++k) {
           const int idx = k * 64 + lane, lr = idx / 24, c = idx % 24;
@@ -1069,7 +1077,7 @@ hipError_t pp192_launch(const __bf16* A, const __bf16* W, const float* bias, con
   if (hipError_t e = ensure_dynamic_lds((const void*)gemm_pp192_kernel<NP, EPI, NT>, lds); e != hipSuccess)
     return e;
   const int tiles_m = (M + 255) / 256;
-  const int tiles = EPI == PK_EPI_RES_LN && ln.mode != 2 ? 32 * ((tiles_m + 7) / 8)
+  const int tiles = EPI == PK_EPI_RES_LN && LN_MODE(ln) != 2 ? 32 * ((tiles_m + 7) / 8)
                                                         : tiles_m * ((N + 191) / 192);
   hipLaunchKernelGGL((gemm_pp192_kernel<NP, EPI, NT>), dim3(tiles), dim3(512), lds, st, A, W, bias, R,
                      C, M, N, K, group_m, ln);
@@ -1090,9 +1098,13 @@ hipError_t pp192_dispatch(const unsigned short* A, const unsigned short* W, cons
     return pp192_launch<1, PK_EPI_BIAS_PACKED>(a, w, bias, R, cp, M, N, K, group_m, st);
   }
   if (nt) {  // timing variant (ae_bench_gemm_packed diag 8): non-temporal stores
+#ifdef AE_TOOLS
     if (np != 2 || (epi != PK_EPI_RES && epi != PK_EPI_BIAS)) return hipErrorInvalidValue;
     if (epi == PK_EPI_BIAS) return pp192_launch<2, PK_EPI_BIAS, true>(a, w, bias, R, C, M, N, K, group_m, st);
     return pp192_launch<2, PK_EPI_RES, true>(a, w, bias, R, C, M, N, K, group_m, st);
+#else
+    return hipErrorInvalidValue;
+#endif
   }
   if (np == 2) {
     if (epi == PK_EPI_BIAS) return pp192_launch<2, PK_EPI_BIAS>(a, w, bias, R, C, M, N, K, group_m, st);
@@ -1213,6 +1225,10 @@ extern "C" hipError_t ae_launch_gemm_packed_ln(const unsigned short* A, const un
   return packed_ln(A, W, bias, R, C, Cp, M, N, K, np, gamma, beta, eps, stats, ctr, err, 0, st);
 }
 
+#ifdef AE_TOOLS
+// ---- tools library only (lib/libalert_engine_tools.so, -DAE_TOOLS): timing experiments whose
+// variants give WRONG results on purpose; the product library exports none of this.
+
 // Timing experiments of the fused residual + LayerNorm GEMM (tools/gemm_bench.py): `mode` as
 // LnArgs::mode.  Not part of include/alert_engine.h.
 extern "C" hipError_t ae_bench_gemm_packed_ln(const unsigned short* A, const unsigned short* W,
@@ -1261,3 +1277,4 @@ extern "C" hipError_t ae_bench_gemm_packed(const unsigned short* A, const unsign
   }
   return hipErrorInvalidValue;
 }
+#endif  // AE_TOOLS

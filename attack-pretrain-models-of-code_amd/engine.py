@@ -11,7 +11,7 @@ import os
 
 import numpy as np
 
-from . import LIB_PATH
+from . import LIB_PATH, TOOLS_LIB_PATH
 from .weights import CODEBERT, RobertaShape
 
 AE_HEAD = {"sigmoid1": 0, "softmaxN": 1, "pair2": 2, "none": 3}
@@ -25,7 +25,10 @@ class AeConfig(ctypes.Structure):
                 ("type_vocab", ctypes.c_int32), ("num_labels", ctypes.c_int32),
                 ("head_kind", ctypes.c_int32), ("precision", ctypes.c_int32),
                 ("pad_id", ctypes.c_int32), ("with_mlm", ctypes.c_int32),
-                ("ln_eps", ctypes.c_float)]
+                ("ln_eps", ctypes.c_float), ("streams", ctypes.c_int32)]
+
+
+AE_STREAMS = {"two": 0, "one": 1}
 
 
 class AeWeightView(ctypes.Structure):
@@ -39,18 +42,21 @@ EXPORTS = ("ae_create", "ae_destroy", "ae_score", "ae_score_graph", "ae_graph_ma
            "ae_topk", "ae_cosine_rank", "ae_set_profiling", "ae_kernel_time", "ae_last_error",
            "ae_version", "ae_source_hash")
 
-_LIB = None
+_LIBS: dict[str, ctypes.CDLL] = {}
 
 
-def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
-    """Load (once) the engine library.  torch must be imported first so that the library binds to
-    the HIP runtime torch already loaded (one runtime per process: shared streams and pointers)."""
-    global _LIB
-    if _LIB is not None:
-        return _LIB
+def load_library(path: str | os.PathLike | None = None, tools: bool = False) -> ctypes.CDLL:
+    """Load (once) the engine library: the product library lib/libalert_engine.so, or with
+    tools=True the tools library lib/libalert_engine_tools.so (the same sources built with
+    -DAE_TOOLS: the product plus the timing / A-B entry points ae_bench_* and the engine's AE_*
+    knobs).  torch must be imported first so that the library binds to the HIP runtime torch
+    already loaded (one runtime per process: shared streams and pointers)."""
+    key = str(path) if path else ("tools" if tools else "product")
+    if key in _LIBS:
+        return _LIBS[key]
     import torch  # noqa: F401  (HIP runtime first)
 
-    p = str(path or LIB_PATH)
+    p = str(path or (TOOLS_LIB_PATH if tools else LIB_PATH))
     if not os.path.exists(p):
         raise RuntimeError(f"HIP engine library not built: {p} is missing (run `make` or "
                            f"__graft_entry__.build()); there is no CPU fallback")
@@ -85,13 +91,14 @@ def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     for name in EXPORTS:
         if name not in ("ae_last_error", "ae_version", "ae_source_hash"):
             getattr(lib, name).restype = ctypes.c_int
-    _LIB = lib
+    _LIBS[key] = lib
     return lib
 
 
-def _check(rc: int, what: str):
+def _check(rc: int, what: str, lib: ctypes.CDLL | None = None):
     if rc != 0:
-        msg = _LIB.ae_last_error().decode(errors="replace") if _LIB is not None else ""
+        lib = lib if lib is not None else _LIBS.get("product")
+        msg = lib.ae_last_error().decode(errors="replace") if lib is not None else ""
         raise RuntimeError(f"{what} failed ({rc}): {msg}")
 
 
@@ -111,10 +118,17 @@ class Engine:
 
     def __init__(self, state_dict: dict[str, np.ndarray], head: str = "sigmoid1",
                  num_labels: int = 1, precision: str = "fp32", device: int = 0,
-                 with_mlm: bool = False, shape: RobertaShape = CODEBERT):
+                 with_mlm: bool = False, shape: RobertaShape = CODEBERT, streams: str = "two",
+                 tools: bool = False):
+        """streams: "two" (default: the split-precision encoder as two half-batch HIP streams)
+        or "one" (every kernel on the caller's stream).  tools=True builds the engine from the
+        tools library (lib/libalert_engine_tools.so, the same sources with -DAE_TOOLS), whose
+        engine also reads the A/B knobs AE_ATTN_VARIANT, AE_SPLIT_STREAMS / _PARTS / _LAG,
+        AE_LN_FIX, AE_QKV192, AE_CLS_ABSORB at creation (tools/engine_ab.py, alternative-form
+        parity tests); the product library reads no environment."""
         import torch
 
-        self.lib = load_library()
+        self.lib = load_library(tools=tools)
         if not torch.cuda.is_available():
             raise RuntimeError("apmc_amd.Engine needs a ROCm GPU (torch.cuda.is_available() is "
                                "False); there is no CPU fallback")
@@ -125,7 +139,8 @@ class Engine:
         self.pad_id = shape.pad_id
         cfg = AeConfig(shape.layers, shape.hidden, shape.heads, shape.ffn, shape.vocab,
                        shape.max_pos, shape.type_vocab, num_labels, AE_HEAD[head],
-                       AE_PREC[precision], shape.pad_id, int(with_mlm), shape.ln_eps)
+                       AE_PREC[precision], shape.pad_id, int(with_mlm), shape.ln_eps,
+                       AE_STREAMS[streams])
         keep = []
         views = (AeWeightView * len(state_dict))()
         for i, (k, v) in enumerate(state_dict.items()):
@@ -135,7 +150,7 @@ class Engine:
         handle = ctypes.c_void_p()
         torch.cuda.set_device(device)
         _check(self.lib.ae_create(ctypes.byref(cfg), views, len(state_dict), device,
-                                  ctypes.byref(handle)), "ae_create")
+                                  ctypes.byref(handle)), "ae_create", self.lib)
         self.handle = handle
         self.out_cols = 1 if head == "sigmoid1" else num_labels
 
@@ -165,7 +180,7 @@ class Engine:
             out = torch.empty((n_out, self.out_cols), dtype=torch.float32, device=ids.device)
         _check(self.lib.ae_score(self.handle, _ptr(ids), ctypes.c_void_p(lens.ctypes.data),
                                  _ptr(pos), _ptr(mask_bits), n, L, _ptr(out), _stream(stream)),
-               "ae_score")
+               "ae_score", self.lib)
         return out
 
     def score_graph(self, ids, lens: np.ndarray, pos, mask_bits, out=None, stream=None):
@@ -186,7 +201,7 @@ class Engine:
             out = torch.empty((n_out, self.out_cols), dtype=torch.float32, device=ids.device)
         _check(self.lib.ae_score_graph(self.handle, _ptr(ids), ctypes.c_void_p(lens.ctypes.data),
                                        _ptr(pos), _ptr(mask_bits), n, L, _ptr(out),
-                                       _stream(stream)), "ae_score_graph")
+                                       _stream(stream)), "ae_score_graph", self.lib)
         return out
 
     def graph_mask(self, ids, meta, spans, edges, out=None, stream=None):
@@ -203,7 +218,7 @@ class Engine:
             out = torch.empty((n, L, L // 32), dtype=torch.int32, device=ids.device)
         _check(self.lib.ae_graph_mask(_ptr(ids), _ptr(meta), _ptr(spans), _ptr(edges), n, L,
                                       edges.shape[1], _ptr(out), _stream(stream)),
-               "ae_graph_mask")
+               "ae_graph_mask", self.lib)
         return out
 
     def encode(self, ids, lens: np.ndarray, attend_pad: bool = False, row0: int = 0,
@@ -220,7 +235,7 @@ class Engine:
         out = torch.zeros((n, nrows, self.shape.hidden), dtype=torch.float32, device=ids.device)
         _check(self.lib.ae_encode_ex(self.handle, _ptr(ids), ctypes.c_void_p(lens.ctypes.data),
                                      n, L, 1 if attend_pad else 0, row0, nrows, _ptr(out),
-                                     _stream(stream)), "ae_encode_ex")
+                                     _stream(stream)), "ae_encode_ex", self.lib)
         return out
 
     def mlm_nll(self, ids, stream=None):
@@ -231,7 +246,7 @@ class Engine:
         assert ids.dtype == torch.int32 and ids.is_cuda and ids.is_contiguous()
         out = torch.empty((n, L), dtype=torch.float32, device=ids.device)
         _check(self.lib.ae_mlm_nll(self.handle, _ptr(ids), n, L, _ptr(out), _stream(stream)),
-               "ae_mlm_nll")
+               "ae_mlm_nll", self.lib)
         return out
 
     def mlm_topk(self, ids, k: int, stream=None):
@@ -241,17 +256,17 @@ class Engine:
         scores = torch.empty((L, k), dtype=torch.float32, device=ids.device)
         idx = torch.empty((L, k), dtype=torch.int32, device=ids.device)
         _check(self.lib.ae_mlm_topk(self.handle, _ptr(ids), L, k, _ptr(scores), _ptr(idx),
-                                    _stream(stream)), "ae_mlm_topk")
+                                    _stream(stream)), "ae_mlm_topk", self.lib)
         return scores, idx
 
     def set_profiling(self, kind: str, enabled: bool = True):
         _check(self.lib.ae_set_profiling(self.handle, AE_KIND[kind], int(enabled)),
-               "ae_set_profiling")
+               "ae_set_profiling", self.lib)
 
     def kernel_time(self):
         ms, cnt, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
         _check(self.lib.ae_kernel_time(self.handle, ctypes.byref(ms), ctypes.byref(cnt),
-                                       ctypes.byref(fl)), "ae_kernel_time")
+                                       ctypes.byref(fl)), "ae_kernel_time", self.lib)
         return ms.value, cnt.value, fl.value
 
 

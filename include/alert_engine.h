@@ -74,6 +74,12 @@ extern "C" {
 #define AE_PREC_F32X3 2 /* GEMMs as split-bf16 (hi*hi + hi*lo + lo*hi) on bf16 MFMA:
                            f32-class accuracy (probabilities within 1e-4) at 3 bf16 MFMAs  */
 
+/* Encoder schedule of the split-precision modes (ignored by AE_PREC_FP32). */
+#define AE_STREAMS_TWO 0 /* default: the batch as two halves on two HIP streams, one kernel apart
+                            (one half's memory-bound phases beside the other's MFMA loops)   */
+#define AE_STREAMS_ONE 1 /* every kernel on the caller's stream (the fused residual +
+                            LayerNorm GEMM epilogue; what the bench's roofline pass times)    */
+
 typedef struct ae_config {
   int32_t layers;      /* 12 */
   int32_t hidden;      /* 768 (kernels are specialised for 768) */
@@ -88,6 +94,7 @@ typedef struct ae_config {
   int32_t pad_id;      /* 1 */
   int32_t with_mlm;    /* 1: also upload the lm_head (MLM paths) */
   float ln_eps;        /* 1e-5 */
+  int32_t streams;     /* AE_STREAMS_*: how the split-precision encoder is scheduled */
 } ae_config;
 
 /* One named host tensor (fp32, row-major, HF state_dict naming). */

@@ -34,6 +34,42 @@ def test_library_exports_every_declared_symbol():
     assert b"gfx950" in lib.ae_version()
 
 
+def _dynamic_symbols(path):
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", str(path)], capture_output=True, text=True,
+                         check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+def test_product_library_has_no_experiment_entry_points():
+    """The product library exports the engine and the launchers it runs, nothing else: the
+    timing / A-B entry points (ae_bench_*: kernel variants and DIAG builds whose results are
+    wrong on purpose) and the engine's AE_* knobs live only in the tools library built from the
+    same sources with -DAE_TOOLS."""
+    from apmc_amd import LIB_PATH, TOOLS_LIB_PATH
+    prod = _dynamic_symbols(LIB_PATH)
+    assert not [s for s in prod if s.startswith("ae_bench")], sorted(prod)
+    assert b"AE_ATTN_VARIANT" not in LIB_PATH.read_bytes()
+    assert b"AE_SPLIT_STREAMS" not in LIB_PATH.read_bytes()
+    tools = _dynamic_symbols(TOOLS_LIB_PATH)
+    for s in ("ae_bench_gemm_packed", "ae_bench_gemm_packed_ln", "ae_bench_attention_pp",
+              "ae_bench_attention_x3"):
+        assert s in tools, s
+    assert set(declared_symbols()) <= tools
+
+
+def test_streams_config_validated():
+    """ae_config.streams (AE_STREAMS_TWO / AE_STREAMS_ONE) is checked before any device call."""
+    from apmc_amd.engine import AE_HEAD, AE_PREC, AeConfig
+    lib = _lib()
+    c = AeConfig(layers=12, hidden=768, heads=12, ffn=3072, vocab=50265, max_pos=514,
+                 type_vocab=1, num_labels=1, head_kind=AE_HEAD["sigmoid1"],
+                 precision=AE_PREC["f32x3"], pad_id=1, with_mlm=0, ln_eps=1e-5, streams=2)
+    out = ctypes.c_void_p()
+    assert lib.ae_create(ctypes.byref(c), None, 0, 0, ctypes.byref(out)) == -22
+    assert "streams" in _err(lib)
+
+
 def test_library_has_gfx950_code_object():
     from apmc_amd import LIB_PATH
     data = LIB_PATH.read_bytes()
@@ -44,12 +80,13 @@ def test_libraries_built_from_this_tree():
     """Both libraries embed the hash of the sources they were built from (buildinfo.py); the
     loaders refuse a library left over from other sources, so the tests and the bench can only
     run binaries built from exactly this tree."""
-    from apmc_amd import HOSTLIB_PATH, LIB_PATH
+    from apmc_amd import HOSTLIB_PATH, LIB_PATH, TOOLS_LIB_PATH
     from apmc_amd.buildinfo import source_hash
     import torch  # noqa: F401
-    eng = ctypes.CDLL(str(LIB_PATH))
-    eng.ae_source_hash.restype = ctypes.c_char_p
-    assert eng.ae_source_hash().decode() == source_hash("engine")
+    for path in (LIB_PATH, TOOLS_LIB_PATH):
+        eng = ctypes.CDLL(str(path))
+        eng.ae_source_hash.restype = ctypes.c_char_p
+        assert eng.ae_source_hash().decode() == source_hash("engine"), path
     host = ctypes.CDLL(str(HOSTLIB_PATH))
     host.ah_source_hash.restype = ctypes.c_char_p
     assert host.ah_source_hash().decode() == source_hash("host")

@@ -27,27 +27,25 @@ def test_attention_summary_counts_the_eleven_full_layers():
     assert bench.attention_summary(0.0, 0, steps, B, L, peak, "here") is None
 
 
-def test_single_stream_engine_restores_the_callers_setting(monkeypatch):
-    """The roofline / attention passes build their engine with AE_SPLIT_STREAMS=0 and leave the
-    caller's own setting (set or unset) in force for the later legs."""
+def test_single_stream_engine_is_a_config_not_the_environment(monkeypatch):
+    """The roofline / attention passes build their engine with ae_config.streams = one stream
+    (the product library reads no AE_* environment) and leave the environment untouched."""
     import apmc_amd.engine as eng_mod
     seen = []
 
     class FakeEngine:
         def __init__(self, *a, **kw):
-            seen.append(os.environ.get("AE_SPLIT_STREAMS"))
+            seen.append(kw)
 
     monkeypatch.setattr(eng_mod, "Engine", FakeEngine)
 
     class Dev:
         index = 0
 
-    monkeypatch.delenv("AE_SPLIT_STREAMS", raising=False)
+    before = dict(os.environ)
     bench.single_stream_engine({}, "f32x3", Dev())
-    assert seen[-1] == "0" and "AE_SPLIT_STREAMS" not in os.environ
-    monkeypatch.setenv("AE_SPLIT_STREAMS", "1")
-    bench.single_stream_engine({}, "f32x3", Dev())
-    assert seen[-1] == "0" and os.environ["AE_SPLIT_STREAMS"] == "1"
+    assert seen[-1]["streams"] == "one" and not seen[-1].get("tools")
+    assert dict(os.environ) == before
 
 
 def test_pmc_traffic_comes_from_the_newest_round():

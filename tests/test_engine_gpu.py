@@ -283,9 +283,9 @@ def test_two_stream_encoder_matches_single_stream(gpu, monkeypatch, precision, n
     from apmc_amd.engine import Engine
     sd = synthetic_sd(6, "softmaxN", 5)
     engines = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("AE_SPLIT_STREAMS", mode)
-        engines[mode] = Engine(sd, head="softmaxN", num_labels=5, precision=precision)
+    for mode, streams in (("1", "two"), ("0", "one")):  # ae_config.streams
+        engines[mode] = Engine(sd, head="softmaxN", num_labels=5, precision=precision,
+                               streams=streams)
     rng = np.random.default_rng(30 + n)
     L = 384
     ids = _rand_ids(rng, n, L, rng.integers(3, L + 1, n))
@@ -307,8 +307,9 @@ def test_cls_absorbed_attention_matches_full_path(gpu, monkeypatch, precision, t
     sd = synthetic_sd(7, "softmaxN", 66)
     engines = {}
     for mode in ("1", "0"):
-        monkeypatch.setenv("AE_CLS_ABSORB", mode)
-        engines[mode] = Engine(sd, head="softmaxN", num_labels=66, precision=precision)
+        monkeypatch.setenv("AE_CLS_ABSORB", mode)  # a knob of the tools library's engine
+        engines[mode] = Engine(sd, head="softmaxN", num_labels=66, precision=precision,
+                               tools=mode == "0")
     rng = np.random.default_rng(40)
     L = 640
     lens = np.array([640, 2, 3, 17, 63, 64, 65, 130, 511, 512, 333, 600], np.int32)
@@ -341,11 +342,11 @@ def test_fused_layernorm_forms_match(gpu, monkeypatch, split):
     boundaries; LayerNorm rounding only, and bit-identical when re-run (counters re-armed)."""
     from apmc_amd.engine import Engine
     sd = synthetic_sd(6, "softmaxN", 5)
-    monkeypatch.setenv("AE_SPLIT_STREAMS", split)
     engines = {}
     for mode in ("2", "0"):
-        monkeypatch.setenv("AE_LN_FIX", mode)
-        engines[mode] = Engine(sd, head="softmaxN", num_labels=5, precision="f32x3")
+        monkeypatch.setenv("AE_LN_FIX", mode)  # a knob of the tools library's engine
+        engines[mode] = Engine(sd, head="softmaxN", num_labels=5, precision="f32x3",
+                               streams="two" if split == "1" else "one", tools=mode == "2")
     rng = np.random.default_rng(50)
     for n, L in ((64, 384), (5, 300), (1, 77)):
         ids = _rand_ids(rng, n, L, rng.integers(3, L + 1, n))
@@ -364,11 +365,11 @@ def test_qkv192_tiles_bit_identical(gpu, monkeypatch, split):
     encoder forms."""
     from apmc_amd.engine import Engine
     sd = synthetic_sd(7, "sigmoid1", 1)
-    monkeypatch.setenv("AE_SPLIT_STREAMS", split)
     engines = {}
     for mode in ("1", "0"):
-        monkeypatch.setenv("AE_QKV192", mode)
-        engines[mode] = Engine(sd, head="sigmoid1", num_labels=1, precision="f32x3")
+        monkeypatch.setenv("AE_QKV192", mode)  # a knob of the tools library's engine
+        engines[mode] = Engine(sd, head="sigmoid1", num_labels=1, precision="f32x3",
+                               streams="two" if split == "1" else "one", tools=mode == "1")
     rng = np.random.default_rng(51)
     for n, L in ((64, 512), (33, 300), (2, 77)):
         lens = np.full(n, L) if n == 64 else rng.integers(3, L + 1, n)

@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 
 def _lib():
     from apmc_amd.engine import load_library
-    lib = load_library()
+    lib = load_library(tools=True)  # the ae_bench_* entry points live in the tools library
     vp, i32 = ctypes.c_void_p, ctypes.c_int32
     lib.ae_launch_gemm_packed.argtypes = [vp] * 6 + [i32] * 5 + [vp]
     lib.ae_launch_gemm_packed.restype = ctypes.c_int

@@ -68,7 +68,7 @@ def main():
     args = ap.parse_args()
 
     from apmc_amd.engine import load_library
-    lib = load_library(args.lib)
+    lib = load_library(args.lib, tools=True)
     vp, i32 = ctypes.c_void_p, ctypes.c_int32
     fn = lib.ae_bench_attention_x3
     fn.argtypes = [vp] * 5 + [i32] * 3 + [vp, i32, i32, i32, vp]

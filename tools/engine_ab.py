@@ -45,7 +45,7 @@ def main():
         for item in filter(None, kv.split(",")):
             k, _, v = item.partition("=")
             os.environ[k] = v
-        engines[name] = Engine(sd, head="sigmoid1", num_labels=1, precision=args.precision, device=0)
+        engines[name] = Engine(sd, head="sigmoid1", num_labels=1, precision=args.precision, device=0, tools=True)
     for k in KNOBS:
         os.environ.pop(k, None)
     first = next(iter(engines))

@@ -53,7 +53,7 @@ def main():
     args = ap.parse_args()
 
     from apmc_amd.engine import load_library
-    lib = load_library(args.lib)
+    lib = load_library(args.lib, tools=True)
     vp, i32 = ctypes.c_void_p, ctypes.c_int32
     fn = getattr(lib, args.entry)
     fn.argtypes = [vp] * 6 + [i32] * 7 + [vp]

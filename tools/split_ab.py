@@ -39,14 +39,14 @@ def main():
     sd = synthetic_state_dict(seed=0, head="sigmoid1")
     engines = {}
     os.environ["AE_SPLIT_STREAMS"] = "0"
-    engines["single"] = Engine(sd, head="sigmoid1", num_labels=1, precision=args.precision, device=0)
+    engines["single"] = Engine(sd, head="sigmoid1", num_labels=1, precision=args.precision, device=0, tools=True)
     os.environ["AE_SPLIT_STREAMS"] = "1"
     for parts in args.parts.split(","):
         for lag in args.lags.split(","):
             os.environ["AE_SPLIT_LAG"] = lag
             os.environ["AE_SPLIT_PARTS"] = parts
             engines[f"p{parts}lag{lag}"] = Engine(sd, head="sigmoid1", num_labels=1,
-                                                  precision=args.precision, device=0)
+                                                  precision=args.precision, device=0, tools=True)
     for k in ("AE_SPLIT_STREAMS", "AE_SPLIT_LAG", "AE_SPLIT_PARTS"):
         os.environ.pop(k)
     B, L = 64, 512
