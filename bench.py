@@ -95,6 +95,35 @@ def log(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+def rank_thread_budget(ranks, env=None):
+    """Host threads of one rank when `ranks` ranks share this host: the CPUs of this process's
+    affinity divided by the ranks, 1..16 (the featurisers' cap, host.gcb_threads), unless the
+    user set APMC_HOST_THREADS.  Every rank runs the host side of its attacks (mutant builder,
+    tokenizer, GCB featuriser threads) and its torch CPU ops on this many threads, so N ranks
+    never oversubscribe the host (torch.distributed.run alone would leave each rank at
+    OMP_NUM_THREADS=1 and the featurisers at the whole affinity each)."""
+    env = os.environ if env is None else env
+    if env.get("APMC_HOST_THREADS"):
+        return max(1, int(env["APMC_HOST_THREADS"]))
+    try:
+        cpus = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        cpus = os.cpu_count() or 1
+    return max(1, min(16, cpus // max(1, ranks)))
+
+
+def relaunch_env(gpus, env=None):
+    """Environment of the N ranks relaunch_as_ranks starts: the dmabuf IPC mode RCCL needs on
+    this pool and each rank's host thread budget (rank_thread_budget) as OMP_NUM_THREADS and
+    APMC_HOST_THREADS."""
+    env = dict(os.environ if env is None else env)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    t = rank_thread_budget(gpus, env)
+    env["OMP_NUM_THREADS"] = str(t)
+    env["APMC_HOST_THREADS"] = str(t)
+    return env
+
+
 def relaunch_as_ranks(args):
     """--gpus N outside torchrun: run N ranks via torch.distributed.run as a child process
     (started before this process touches the GPU) and exit with its status."""
@@ -102,9 +131,7 @@ def relaunch_as_ranks(args):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
            f"--master-port={port}", str(pathlib.Path(__file__).resolve())] + sys.argv[1:]
-    env = dict(os.environ)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    return subprocess.call(cmd, env=env)
+    return subprocess.call(cmd, env=relaunch_env(args.gpus))
 
 
 def executed_flops_per_query(L, C=1):
@@ -809,6 +836,8 @@ def main():
         gpu = 0
         torch.cuda.set_device(0)
     dev = torch.device(f"cuda:{gpu}")
+    if world > 1:  # the rank's share of the host (relaunch_env; torchrun alone gives 1 thread)
+        torch.set_num_threads(rank_thread_budget(world))
     global COLL_DEV
     COLL_DEV = torch.device("cpu") if rehearse else dev  # where collective tensors live
 

@@ -224,3 +224,81 @@ def test_inflight_cap_spreads_short_queues():
     assert _inflight(64, 400, 8) == 25
     assert _inflight(64, 400, 1) == 64
     assert _inflight(64, 3, 8) == 1
+
+
+def test_relaunch_splits_host_threads_per_rank(tmp_path):
+    """bench.py --gpus N relaunches itself as N ranks with each rank's host budget = the host's
+    CPUs / N (1..16): torch threads, OMP_NUM_THREADS and the C++ featurisers' worker threads
+    (host.gcb_threads) all take it, so N ranks sharing one host do not oversubscribe it.  Runs
+    the relaunch's own environment (bench.relaunch_env) under torch.distributed.run, gloo,
+    world 2."""
+    import json
+    import subprocess
+
+    sys.path.insert(0, str(ROOT))
+    import bench
+    env = bench.relaunch_env(2)
+    want = bench.rank_thread_budget(2, {k: v for k, v in env.items() if k != "APMC_HOST_THREADS"})
+    assert env["OMP_NUM_THREADS"] == env["APMC_HOST_THREADS"] == str(want)
+    cpus = len(os.sched_getaffinity(0))
+    assert want == max(1, min(16, cpus // 2))
+    out = tmp_path / "threads.json"
+    port = 29500 + os.getpid() % 1000
+    subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                    "--nproc-per-node=2", "--master-addr", "127.0.0.1", f"--master-port={port}",
+                    str(ROOT / "tests" / "_rank_threads.py"), str(out)],
+                   env=env, check=True, timeout=300, capture_output=True)
+    parts = json.loads(out.read_text())
+    assert sorted(p["rank"] for p in parts) == [0, 1]
+    for p in parts:
+        assert p["torch"] == want and p["host"] == want and p["omp"] == str(want), p
+    # an explicit APMC_HOST_THREADS wins
+    assert bench.rank_thread_budget(8, {"APMC_HOST_THREADS": "5"}) == 5
+
+
+def test_collectives_pick_the_backend_device(monkeypatch):
+    """gather_stats all-gathers on the rank's current GPU under nccl (RCCL) and on the host under
+    gloo (or an explicit device when given); merge_records uses all_gather_object (which places
+    its buffers on the current device under nccl).  Checked against a stand-in torch.distributed
+    that records the device of every tensor it is handed."""
+    import torch
+    import torch.distributed as tdist
+
+    sys.path.insert(0, str(ROOT))
+    import _apmc  # noqa: F401
+    from apmc_amd import dist as adist
+
+    seen = {}
+
+    def all_gather(out, t):
+        seen["device"] = t.device
+        for o in out:
+            o.copy_(t)
+
+    def all_gather_object(parts, obj):
+        seen["object"] = True
+        for i in range(len(parts)):
+            parts[i] = [dict(r, index=r["index"] + 100 * i) for r in obj]
+
+    for name, val in (("is_available", lambda: True), ("is_initialized", lambda: True),
+                      ("get_world_size", lambda: 2), ("all_gather", all_gather),
+                      ("all_gather_object", all_gather_object)):
+        monkeypatch.setattr(tdist, name, val)
+    monkeypatch.setattr(tdist, "get_backend", lambda: "gloo")
+    st = adist.gather_stats([1.0, 2.0], device=torch.device("meta"))
+    assert seen["device"].type == "cpu" and st.shape == (2, 2)  # gloo: host, whatever is asked
+    monkeypatch.setattr(tdist, "get_backend", lambda: "nccl")
+    # nccl without an explicit device: the rank's current GPU (a stand-in index here, no GPU)
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 3)
+    orig_tensor = torch.tensor
+
+    def tensor(v, dtype=None, device=None):
+        seen["asked"] = torch.device(device) if device is not None else None
+        return orig_tensor(v, dtype=dtype)  # built on the host: no GPU in this container
+    monkeypatch.setattr(torch, "tensor", tensor)
+    adist.gather_stats([1.0, 2.0])
+    assert seen["asked"] == torch.device("cuda", 3)
+    adist.gather_stats([1.0, 2.0], device=torch.device("cuda", 1))
+    assert seen["asked"] == torch.device("cuda", 1)
+    recs = adist.merge_records([{"index": 2}, {"index": 0}])
+    assert seen["object"] and [r["index"] for r in recs] == [0, 2, 100, 102]
