@@ -51,41 +51,52 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
 }
 
-// exact-erf GELU through a rational erfc (Abramowitz & Stegun 7.1.26, |erf error| <= 1.5e-7):
-// erfc(z) = t·P5(t)·exp(-z²) = E, t = 1/(1 + 0.3275911 z), z = |x|/√2.  With u = x/2,
-// GELU(x) = u + |u| - |u|·E (x >= 0: x - u·E; x < 0: u·E), so no compare / select: one FMA ends
-// it.  Over [-12, 12] it is within 3.3e-7 absolute of the float64 GELU (torch's f32 GELU: 1.2e-6
-// absolute), 5 Horner FMAs + rcp + exp2 — the split-precision FFN1 epilogue is VALU-bound on
-// this (tools/gemm_bench.py diag 4 vs 0).
-__device__ __forceinline__ float gelu_erfc_fast(float x) {
-  const float u = 0.5f * x, au = fabsf(u);
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.46328380415598320f, au, 1.0f));
-  float p = 1.061405429f;
-  p = fmaf(p, t, -1.453152027f);
-  p = fmaf(p, t, 1.421413741f);
-  p = fmaf(p, t, -0.284496736f);
-  p = fmaf(p, t, 0.254829592f);
-  const float e = __builtin_amdgcn_exp2f(u * (-2.88539008177792680f * u));  // exp(-x²/2)
-  return fmaf(-au, (p * t) * e, u + au);
+typedef float gelu_f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+// exact-erf GELU (HF "gelu") of NP2 pairs x, in place:  GELU(x) = max(x, 0) - s·E',
+// s = min(|x|, 6), E' = erfc(s/√2) / 2 = exp2(P6(s)), P6 the degree-6 polynomial of
+// tools/fit_gelu.py (a weighted minimax fit of log2 erfc(s/√2) - 1 on the GELU error itself,
+// s·E'·ln2·ΔP).  For |x| <= 6 this is the identity x·Φ(x) = max(x, 0) - |x|·Φ(-|x|); past it the
+// s·E' term is at most 6·E'(6) = 6.6e-9, so large |x| give x (x > 0) or -6.6e-9 (x < 0).  Over
+// every f32 x within 2.9e-7 absolute of the float64 GELU and 8.2e-8 beyond the f32 rounding of
+// the result (the Abramowitz & Stegun 7.1.26 form it replaced — rcp + exp + five FMAs — 2.1e-7
+// beyond rounding; torch's f32 GELU 1.2e-6).  Per pair: two v_min (|x| as a source modifier), six
+// packed FMAs, two v_exp_f32, two v_max and one packed FMA — no reciprocal; written step-major
+// over the pairs so that independent chains interleave (no VOP3P dependency stalls).
+template <int NP2>
+__device__ __forceinline__ void gelu_exp2_pairs(gelu_f2 (&x)[NP2]) {
+  gelu_f2 s[NP2], p[NP2];
+#pragma unroll
+  for (int k = 0; k < NP2; ++k)
+    s[k] = __builtin_elementwise_min(__builtin_elementwise_abs(x[k]), gelu_f2(6.0f));
+#pragma unroll
+  for (int k = 0; k < NP2; ++k)
+    p[k] = __builtin_elementwise_fma(gelu_f2(3.309332169e-05f), s[k], gelu_f2(-7.692241343e-04f));
+#pragma unroll
+  for (int k = 0; k < NP2; ++k) p[k] = __builtin_elementwise_fma(p[k], s[k], gelu_f2(8.080731146e-03f));
+#pragma unroll
+  for (int k = 0; k < NP2; ++k) p[k] = __builtin_elementwise_fma(p[k], s[k], gelu_f2(-5.341212824e-02f));
+#pragma unroll
+  for (int k = 0; k < NP2; ++k) p[k] = __builtin_elementwise_fma(p[k], s[k], gelu_f2(-4.587709606e-01f));
+#pragma unroll
+  for (int k = 0; k < NP2; ++k) p[k] = __builtin_elementwise_fma(p[k], s[k], gelu_f2(-1.151201725e+00f));
+#pragma unroll
+  for (int k = 0; k < NP2; ++k) p[k] = __builtin_elementwise_fma(p[k], s[k], gelu_f2(-9.999930859e-01f));
+#pragma unroll
+  for (int k = 0; k < NP2; ++k) {
+    const gelu_f2 e = {__builtin_amdgcn_exp2f(p[k].x), __builtin_amdgcn_exp2f(p[k].y)};
+    x[k] = __builtin_elementwise_fma(-s[k], e, __builtin_elementwise_max(x[k], gelu_f2(0.0f)));
+  }
 }
 
-// gelu_erfc_fast on a pair, written on 2-wide vectors so every non-transcendental step is one
-// packed-f32 instruction (v_pk_fma / v_pk_mul / v_pk_add: the same IEEE operation per element,
-// so the results equal two gelu_erfc_fast calls bit for bit); the rcp and exp2 stay scalar.
-typedef float gelu_f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ gelu_f2 gelu_erfc_fast2(gelu_f2 x) {
-  const gelu_f2 u = x * 0.5f;
-  const gelu_f2 au = {fabsf(u.x), fabsf(u.y)};
-  const gelu_f2 d = __builtin_elementwise_fma(gelu_f2(0.46328380415598320f), au, gelu_f2(1.0f));
-  const gelu_f2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-  gelu_f2 p = gelu_f2(1.061405429f);
-  p = __builtin_elementwise_fma(p, t, gelu_f2(-1.453152027f));
-  p = __builtin_elementwise_fma(p, t, gelu_f2(1.421413741f));
-  p = __builtin_elementwise_fma(p, t, gelu_f2(-0.284496736f));
-  p = __builtin_elementwise_fma(p, t, gelu_f2(0.254829592f));
-  const gelu_f2 a = u * (-2.88539008177792680f * u);
-  const gelu_f2 e = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
-  return __builtin_elementwise_fma(-au, (p * t) * e, u + au);
+// split of an f32 pair into bf16 hi / lo planes (hi = rne(y), lo = rne(y - hi)), each plane's pair
+// as one 32-bit word (element 0 in the low half): two v_cvt_pk_bf16_f32, the hi pair widened back
+// to f32 by a shift and a mask, one packed subtract
+__device__ __forceinline__ void split_pair(gelu_f2 y, uint32_t& hw, uint32_t& lw) {
+  hw = __builtin_bit_cast(uint32_t, __builtin_convertvector(y, bf16x2_t));
+  const gelu_f2 hf = {__builtin_bit_cast(float, hw << 16), __builtin_bit_cast(float, hw & 0xffff0000u)};
+  lw = __builtin_bit_cast(uint32_t, __builtin_convertvector(y - hf, bf16x2_t));
 }
 
 // bf16 round-to-nearest-even of an f32 (NaN-preserving cast lowered to v_cvt_pk_bf16_f32).

@@ -394,31 +394,20 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
           // 16 slots: 2048 bank-conflict cycles per tile, profiles/r4g_pmc_lds.json)
           const floatx16& c = acc[2 * half + tt][tn];
           uint32_t hw[4][2], lw[4][2];
+          gelu_f2 y[8];  // pair i/2 of register quad j: y[2 j + i / 2]
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int cc = tn * 32 + 8 * j + 4 * lh;  // column within the wave's 64
             const int col = cb0 + cc < N ? cb0 + cc : N - 4;
             const floatx4 bv = *reinterpret_cast<const floatx4*>(bias + col);
-            float yv[4];
 #pragma unroll
             for (int i = 0; i < 4; i += 2) {
-              const gelu_f2 z = gelu_f2{c[4 * j + i], c[4 * j + i + 1]} + gelu_f2{bv[i], bv[i + 1]};
-              const gelu_f2 y = EPI == PK_EPI_GELU_PACKED ? gelu_erfc_fast2(z) : z;
-              yv[i] = y.x;
-              yv[i + 1] = y.y;
+              y[2 * j + i / 2] = gelu_f2{c[4 * j + i], c[4 * j + i + 1]} + gelu_f2{bv[i], bv[i + 1]};
             }
-            ushortx4 h, l;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const float y = yv[i];
-              const __bf16 hv = (__bf16)y;
-              h[i] = __builtin_bit_cast(unsigned short, hv);
-              l[i] = f2bf(y - (float)hv);
-            }
-            const uint2 hu = __builtin_bit_cast(uint2, h), lu = __builtin_bit_cast(uint2, l);
-            hw[j][0] = hu.x; hw[j][1] = hu.y;
-            lw[j][0] = lu.x; lw[j][1] = lu.y;
           }
+          if constexpr (EPI == PK_EPI_GELU_PACKED) gelu_exp2_pairs(y);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) split_pair(y[k], hw[k >> 1][k & 1], lw[k >> 1][k & 1]);
 #pragma unroll
           for (int jp = 0; jp < 4; jp += 2) {
 #pragma unroll
