@@ -38,6 +38,24 @@ from .utils import _tokenize, get_identifier_posistions_from_code, is_valid_subs
 K_TOP = 60  # get_substitutes.py:63
 
 
+def substitute_identifiers(code: str, lang: str):
+    """get_identifiers as each task's get_substitutes.py calls it on the stored program text.
+    C (Defect-detection/preprocess/get_substitutes.py:54) and Java (Clone-detection-BigCloneBench/
+    dataset/get_substitutes.py): get_identifiers(remove_comments_and_docstrings(code, lang)).
+    Python (Authorship-Attribution/dataset/get_substitutes.py:54-57): the stored program is ONE
+    line whose newlines are the two characters '\\n', and the tokenize-based comment / docstring
+    remover runs on that form before get_identifiers turns them into newlines — so a '#' comment
+    removes the rest of the program, and a program tokenize rejects keeps its comments (the
+    except branch).  Pinned by the fixture keys (tests/test_host.py::key_parity)."""
+    if lang == "python":
+        from .attacker import remove_python_docstrings
+        try:
+            return get_identifiers(remove_python_docstrings(code), lang)
+        except Exception:
+            return get_identifiers(code, lang)
+    return get_identifiers(remove_comments(code), lang)
+
+
 class SubstituteGenerator:
     """`engine` is an Engine built with_mlm=True (head "none" is enough).  cosine=False is the
     GraphCodeBERT preprocessing (no naturalness re-encode: every top-60 candidate is kept)."""
@@ -93,8 +111,7 @@ class SubstituteGenerator:
     # ------------------------------------------------------------------------------------------
     def generate(self, func: str, trace=None) -> dict[str, list[str]]:
         """`item["substitutes"]` for one function (get_substitutes.py:54-137)."""
-        lang = self.lang
-        identifiers, code_tokens = get_identifiers(remove_comments(func), lang)
+        identifiers, code_tokens = substitute_identifiers(func, self.lang)
         variable_names = [name[0] for name in identifiers if " " not in name[0].strip()]
         return self.generate_from_tokens(code_tokens, variable_names, trace)
 

@@ -308,8 +308,8 @@ def key_parity(task):
     dataset/get_substitutes.py:52-140) fixtures: (exact, consistent, subsequence, total).
     subsequence = the keys are an ordered subsequence of our names (the only difference is names
     the reference kept no substitute for)."""
-    from apmc_amd.attacker import get_identifiers
-    from apmc_amd.host import Tokenizer, remove_comments
+    from apmc_amd.host import Tokenizer
+    from apmc_amd.substitutes import substitute_identifiers
     from apmc_amd.utils import _tokenize, get_identifier_posistions_from_code, is_valid_variable_name
     tok = Tokenizer()
     lang = "java" if task == "clone" else "python"
@@ -317,10 +317,9 @@ def key_parity(task):
     for js in load(CLONE if task == "clone" else AA):
         tot += 1
         keys = list(js["substitutes"].keys())
-        if task == "clone":
-            idents, toks = get_identifiers(remove_comments(js["code1"]), lang)
-        else:
-            idents, toks = get_identifiers(js["code"].replace("\\n", "\n"), lang)
+        # the stored text as the task's get_substitutes.py reads it (the authorship programs with
+        # their newlines as literal '\\n': its comment remover runs on that one-line form)
+        idents, toks = substitute_identifiers(js["code1"] if task == "clone" else js["code"], lang)
         words, sub_words, kk = _tokenize(" ".join(toks), tok)
         names = [i[0] for i in idents if " " not in i[0].strip()]
         pos = get_identifier_posistions_from_code(words, names)
@@ -342,11 +341,12 @@ def test_dfg_java_python_vs_reference_fixture_keys():
     """DFG_java / DFG_python (dfg_java.cpp, dfg_python.cpp) against the reference's own keys, at
     the measured counts (DESIGN.md §5 classifies every remaining function by cause): Java 433 /
     477 / 488 of the 500 BigCloneBench code1 in data/ exact / truncation-consistent / ordered
-    subsequence, Python 71 / 128 / 130 of the 132 authorship programs."""
+    subsequence, Python 90 / 130 / 130 of the 132 authorship programs (the two left: a broken
+    string literal whose tree-sitter recovery defines two names, and a program that is Haskell)."""
     e, c, s, t = key_parity("clone")
     assert t == 500 and e >= 433 and c >= 477 and s >= 488, (e, c, s, t)
     e, c, s, t = key_parity("authorship")
-    assert t == 132 and e >= 71 and c >= 128 and s >= 130, (e, c, s, t)
+    assert t == 132 and e >= 90 and c >= 130 and s >= 130, (e, c, s, t)
 
 
 def _names(code, lang):
