@@ -69,6 +69,11 @@ __device__ __forceinline__ void dma4s(uint32_t voff, const void* sbase, uint32_t
       : "memory", "m0");
 }
 
+// max without the canonicalising v_max x, x that fmaxf (llvm.maxnum, IEEE mode) puts in front of
+// every MFMA result it reads: IEEE maximum (v_maximum3_f32 on gfx950).  Scores are finite or
+// -inf (absent keys), never NaN, so the two agree on every value the loop sees.
+__device__ __forceinline__ float max_nc(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+
 template <int NP>
 struct PPL {
   static constexpr int RB = 128 * NP;             // bytes of one key's 64 d (NP planes)
@@ -228,7 +233,7 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && !(HAS_MASK && NP == 2)) ? 3 : 2
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float p = __builtin_amdgcn_exp2f(s[r] - m_new);  // exp2(-inf) = 0
-      psum += p;
+      psum = r == 0 ? p : psum + p;  // p >= +0: the same sum without the leading 0 + p
       const __bf16 h = (__bf16)p;
       ph[r >> 3][r & 7] = h;
       pl[r >> 3][r & 7] = (__bf16)(p - (float)h);
@@ -440,9 +445,9 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && !(HAS_MASK && NP == 2)) ? 3 : 2
           if constexpr (TREE) {
             float a[6];
 #pragma unroll
-            for (int r = 0; r < 5; ++r) a[r] = fmaxf(s_cur[3 * r], fmaxf(s_cur[3 * r + 1], s_cur[3 * r + 2]));
+            for (int r = 0; r < 5; ++r) a[r] = max_nc(s_cur[3 * r], max_nc(s_cur[3 * r + 1], s_cur[3 * r + 2]));
             a[5] = s_cur[15];
-            mt = fmaxf(fmaxf(a[0], fmaxf(a[1], a[2])), fmaxf(a[3], fmaxf(a[4], a[5])));
+            mt = max_nc(max_nc(a[0], max_nc(a[1], a[2])), max_nc(a[3], max_nc(a[4], a[5])));
           } else {
 #pragma unroll
             for (int r = 0; r < 16; r += 2) mt = fmaxf(mt, fmaxf(s_cur[r], s_cur[r + 1]));
@@ -458,19 +463,19 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && !(HAS_MASK && NP == 2)) ? 3 : 2
             // additive finfo.min mask), as tile_max
             const bool in = kt * KT + kk < len;
             s_cur[r] = !in ? -INFINITY : (((mb >> kk) & 1u) ? s_cur[r] : -FLT_MAX);
-            mt = fmaxf(mt, s_cur[r]);
+            mt = max_nc(mt, s_cur[r]);
           }
         }
         if constexpr (FAST) {
           // lanes l and l ^ 32 hold the two halves of a query's keys: swap the halves on the VALU
           const auto sw = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(uint32_t, mt),
                                                           __builtin_bit_cast(uint32_t, mt), false, false);
-          mt = fmaxf(__builtin_bit_cast(float, (uint32_t)sw[0]), __builtin_bit_cast(float, (uint32_t)sw[1]));
+          mt = max_nc(__builtin_bit_cast(float, (uint32_t)sw[0]), __builtin_bit_cast(float, (uint32_t)sw[1]));
         } else {
           mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
         }
         grow = __any(mt > m_run + 8.f);
-        m_new = grow ? fmaxf(m_run, mt) : m_run;
+        m_new = grow ? max_nc(m_run, mt) : m_run;
         alpha = __builtin_amdgcn_exp2f(m_run - m_new);  // 1 when m_new == m_run; 0 from -inf
       }
       // PIPE 72: the rare O rescale BEFORE the region, so no branch separates tile kt's exp /

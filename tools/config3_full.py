@@ -5,6 +5,10 @@
                                            their "substitutes")
   python tools/config3_full.py compare OUT.jsonl [OUT2.jsonl ...] [--timing LOG ...]
                                         -> JSON summary: items, key-set diff against the fixtures
+  python tools/config3_full.py rundiff A1.jsonl[,A2.jsonl] B1.jsonl[,B2.jsonl]
+                                        -> JSON: two of OUR runs compared item by item (keys and
+                                           every key's substitute set, as sets: list order inside
+                                           an entry is Python set order in the reference)
 
 The reference's fixture files hold get_substitutes.py's output for these functions; their
 "substitutes" KEYS are the identifiers that survived get_identifiers + the filters (and kept at
@@ -104,9 +108,49 @@ def compare(outs, timing_logs):
     print(json.dumps(res, indent=1))
 
 
+def rundiff(a_files, b_files):
+    def load(files):
+        out = {}
+        for f in files.split(","):
+            for line in open(f):
+                d = json.loads(line)
+                out[d["idx"]] = d["substitutes"]
+        return out
+    a, b = load(a_files), load(b_files)
+    common = sorted(set(a) & set(b))
+    same_items = key_diff = 0
+    entries = entries_same = 0
+    diffs = []
+    for i in common:
+        sa, sb = a[i], b[i]
+        if set(sa) != set(sb):
+            key_diff += 1
+        ks = set(sa) & set(sb)
+        differing = []
+        for k in ks:
+            entries += 1
+            if set(sa[k]) == set(sb[k]):
+                entries_same += 1
+            else:
+                differing.append((k, len(set(sa[k]) ^ set(sb[k])), len(sa[k]), len(sb[k])))
+        if set(sa) == set(sb) and not differing:
+            same_items += 1
+        elif len(diffs) < 40:
+            diffs.append({"idx": i, "keys_only_a": sorted(set(sa) - set(sb)),
+                          "keys_only_b": sorted(set(sb) - set(sa)),
+                          "entries_differing": [{"key": k, "sym_diff": d, "n_a": na, "n_b": nb}
+                                                for k, d, na, nb in differing[:6]]})
+    print(json.dumps({"items_a": len(a), "items_b": len(b), "items_common": len(common),
+                      "items_identical": same_items, "items_with_key_set_diff": key_diff,
+                      "entries_common": entries, "entries_identical": entries_same,
+                      "first_diffs": diffs}, indent=1))
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "make":
         make()
+    elif sys.argv[1] == "rundiff":
+        rundiff(sys.argv[2], sys.argv[3])
     else:
         args = sys.argv[2:]
         logs = args[args.index("--timing") + 1:] if "--timing" in args else []
