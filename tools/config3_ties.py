@@ -7,7 +7,10 @@ measured on the fp32 run:
   * the 60th / 61st masked-LM logit of each sub-word row of the name's occurrences (top-60,
     get_substitutes.py:63; the 61st from ae_mlm_topk with k = 61),
   * the 30th / 31st cosine score of each occurrence (the naturalness cut, :104-107) and, for a
-    multi-sub-word name, the 4th / 5th (get_bpe_substitues reads the first 4 columns, utils.py:209).
+    multi-sub-word name, every adjacent pair among the first 5 (get_bpe_substitues reads the first
+    4 columns in cosine order and caps their cartesian product at 24 in that order,
+    utils.py:209-248), and every adjacent pair of its rows' top-60 logits (candidate j is the
+    rank-j id of EVERY row of the span, so any swap re-pairs the columns).
 The two runs' own f32x3 error is measured on the same items: eps_logit = max |f32x3 - fp32| over
 the sorted top-60 scores, eps_sim = max |f32x3 - fp32| over the cosine scores of occurrences whose
 60 candidates agree.  An entry is a NEAR TIE when some cut it reads has a gap below 2 eps (both runs
@@ -93,11 +96,16 @@ def main():
                     continue
                 k0, k1 = kk[pos]
                 rows = range(k0, min(k1, sc61.shape[0]))
-                gaps_logit += [float(sc61[r, K_TOP - 1] - sc61[r, K_TOP]) for r in rows]
+                multi = k1 - k0 > 1
+                for r in rows:
+                    if multi:  # candidate j pairs the rank-j ids of every row: any adjacent swap
+                        gaps_logit.append(float(np.min(sc61[r, :K_TOP] - sc61[r, 1:K_TOP + 1])))
+                    else:
+                        gaps_logit.append(float(sc61[r, K_TOP - 1] - sc61[r, K_TOP]))
                 s = np.sort(np.asarray(sims, np.float64))[::-1]
                 gaps_sim.append(float(s[29] - s[30]))
-                if k1 - k0 > 1:
-                    gaps_sim.append(float(s[3] - s[4]))
+                if multi:  # the first 4 columns, in cosine order (the capped cartesian product)
+                    gaps_sim.append(float(np.min(s[:4] - s[1:5])))
             tie = ((gaps_logit and min(gaps_logit) < 2 * eps_logit) or
                    (gaps_sim and min(gaps_sim) < 2 * eps_sim))
             near += bool(tie)
