@@ -40,10 +40,14 @@ hipError_t ae_launch_gemm_packed(const unsigned short*, const unsigned short*, c
 hipError_t ae_launch_gemm_packed_qkv192(const unsigned short*, const unsigned short*, const float*,
                                         const float*, float*, unsigned short*, int, int, int, int,
                                         int, hipStream_t);
-hipError_t ae_launch_gemm_packed_ln(const unsigned short*, const unsigned short*, const float*,
-                                    const float*, float*, unsigned short*, int, int, int, int,
-                                    const float*, const float*, float, uint64_t*, int*, int*,
-                                    hipStream_t);
+hipError_t ae_launch_gemm_packed_fold(const unsigned short*, const unsigned short*, const float*,
+                                      const float*, const uint64_t*, float, unsigned short*, int,
+                                      int, int, int, int, hipStream_t);
+hipError_t ae_launch_gemm_packed_res_stats(const unsigned short*, const unsigned short*,
+                                           const float*, const float*, const uint64_t*,
+                                           const float*, const float*, float, float*,
+                                           unsigned short*, uint64_t*, int, int, int, int,
+                                           hipStream_t);
 hipError_t ae_launch_compact(const int*, const int*, const int*, int, int, int, int, int*, int*,
                              int*, int*, hipStream_t);
 hipError_t ae_launch_embed_ln(const int*, const int*, const float*, const float*, const float*,
@@ -92,8 +96,12 @@ struct LayerW {
   // split-bf16 planes (AE_PREC_BF16: hi only; AE_PREC_F32X3: hi + lo)
   unsigned short *wqkv_h, *wo_h, *w1_h, *w2_h;
   unsigned short *wqkv_l, *wo_l, *w1_l, *w2_l;
-  // packed planes for gemm_planes.hip (F32X3: [N][K/32][hi 32 | lo 32]; BF16: = the hi plane)
+  // packed planes for gemm_planes.hip (F32X3: [N][K/32][hi 32 | lo 32]; BF16: the hi plane).
+  // wqkv_p of layers >= 1 and every w1_p carry the preceding LayerNorm's gain folded in
+  // (gemm_planes.hip FoldArgs): W' = W·diag(g), with s = row sums of W' (as its planes hold it)
+  // and the folded bias bias + W·b
   unsigned short *wqkv_p, *wo_p, *w1_p, *w2_p;
+  float *sqkv, *bqkv_f, *s1, *b1_f;
 };
 
 struct ProfRec {
@@ -118,27 +126,17 @@ struct ae_engine {
   // packed bf16 activation planes of the split-precision path (gemm_planes.hip layout, np planes):
   // LN output, attention context, FFN1 output.  Allocated only when `planes` is on.
   unsigned short *xp = nullptr, *cp = nullptr, *hp = nullptr;
-  // row statistics and per-row-block counters of the fused residual + LayerNorm GEMM epilogue
-  // (gemm_planes.hip PK_EPI_RES_LN); the counters are zero between launches
+  // per-tile row statistics [T][4] of the pre-LayerNorm rows (gemm_planes.hip PK_EPI_RES_STATS):
+  // lnst of the FFN2 output (read by the next layer's QKV and O-projection), lnst2 of the
+  // O-projection output (read by FFN1 and FFN2)
   uint64_t* lnst = nullptr;
-  int* lnctr = nullptr;
-  size_t ctr_stride = 0;  // ints per part region of lnctr
+  uint64_t* lnst2 = nullptr;
   bool planes = false;
   int np = 1;
   // last-layer CLS attention with W_k absorbed into the query (cls_attention.hip): per-sequence
   // u = W_k^T q and p-weighted row sums [n][12][768], per-64-key-chunk partial records
   // (AE_CLS_ABSORB=0 at engine creation: the full-T QKV GEMM + one-query attention instead)
   bool cls_absorb = true;
-  // where the residual + LayerNorm after the O-projection / FFN2 runs (AE_LN_FIX at engine
-  // creation):
-  //   0 (default) the two-stream form: a separate LayerNorm kernel after each part's GEMM (the
-  //     GEMM adds the residual); the single-stream form: inside the GEMM by the co-resident
-  //     exchange (gemm_planes.hip LnArgs mode 0);
-  //   2 the co-resident exchange on both forms, each part of the two-stream form with its own
-  //     counters (measured 16.06 vs 15.89 ms per B=64 x 512 step, 9.40 vs 9.28 ragged:
-  //     profiles/r4h_engine_ab.json — the fused GEMMs wait for partners beside the other part's
-  //     kernels, the separate LayerNorm overlaps them).
-  int ln_kind = 0;
   // the QKV GEMM may run on 256 x 192 tiles (its packed-plane epilogue) where that finishes in
   // fewer tile rounds (AE_QKV192=1 at engine creation)
   bool qkv192 = false;
@@ -261,6 +259,36 @@ int upload_packed(ae_engine* e, const float* host, size_t rows, size_t K, unsign
   return AE_OK;
 }
 
+// A LayerNorm (gain g, shift b over the K inputs) folded into the packed-plane weight of the GEMM
+// that consumes its output (gemm_planes.hip FoldArgs): uploads the planes of W' = W·diag(g)
+// (np 2: hi | lo, np 1: hi), s[n] = sum_k W'[n][k] as those planes hold it, and the folded bias
+// bias[n] + sum_k W[n][k]·b[k] (double sums).
+int upload_folded(ae_engine* e, const float* W, const float* bias, const float* g, const float* b,
+                  size_t rows, size_t K, int np, unsigned short** planes, float** s_dev,
+                  float** bias_dev) {
+  std::vector<float> wf(rows * K), sv(rows), bv(rows);
+  for (size_t r = 0; r < rows; ++r) {
+    double ss = 0.0, bb = bias[r];
+    for (size_t k = 0; k < K; ++k) {
+      const float x = W[r * K + k] * g[k];
+      wf[r * K + k] = x;
+      const float h = host_bf2f(host_f2bf(x));
+      ss += (double)h + (np == 2 ? (double)host_bf2f(host_f2bf(x - h)) : 0.0);
+      bb += (double)W[r * K + k] * (double)b[k];
+    }
+    sv[r] = (float)ss;
+    bv[r] = (float)bb;
+  }
+  int rc = np == 2 ? upload_packed(e, wf.data(), rows, K, planes)
+                   : upload_split(e, wf.data(), wf.size(), planes, nullptr);
+  if (rc) return rc;
+  if ((rc = dev_alloc(e, (void**)s_dev, rows * 4)) || (rc = dev_alloc(e, (void**)bias_dev, rows * 4)))
+    return rc;
+  HIPC(hipMemcpy(*s_dev, sv.data(), rows * 4, hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(*bias_dev, bv.data(), rows * 4, hipMemcpyHostToDevice));
+  return AE_OK;
+}
+
 int ensure_workspace(ae_engine* e, size_t T, size_t n) {
   const size_t H = e->cfg.hidden, F = e->cfg.ffn;
   if (T > e->cap_T) {
@@ -268,11 +296,10 @@ int ensure_workspace(ae_engine* e, size_t T, size_t n) {
     HIPC(hipDeviceSynchronize());
     for (void* p : {(void*)e->x, (void*)e->qkv, (void*)e->ctx, (void*)e->tmp, (void*)e->h1,
                     (void*)e->tok_ids, (void*)e->tok_pos, (void*)e->src_col, (void*)e->xp,
-                    (void*)e->cp, (void*)e->hp, (void*)e->lnst, (void*)e->lnctr})
+                    (void*)e->cp, (void*)e->hp, (void*)e->lnst, (void*)e->lnst2})
       dev_free(e, p);
     e->xp = e->cp = e->hp = nullptr;
-    e->lnst = nullptr;
-    e->lnctr = nullptr;
+    e->lnst = e->lnst2 = nullptr;
     int rc = 0;
     if ((rc = dev_alloc(e, (void**)&e->x, nt * H * 4))) return rc;
     if ((rc = dev_alloc(e, (void**)&e->qkv, nt * 3 * H * 4))) return rc;
@@ -288,11 +315,7 @@ int ensure_workspace(ae_engine* e, size_t T, size_t n) {
       if ((rc = dev_alloc(e, (void**)&e->hp, nt * F * 2 * e->np))) return rc;
       const size_t blocks = (nt + 255) / 256;
       if ((rc = dev_alloc(e, (void**)&e->lnst, blocks * 256 * 4 * 8))) return rc;
-      // arrival / departure counters per 256-row block, one region per part of the two-stream
-      // encoder (parts run concurrently; each launch's counters start at its region)
-      e->ctr_stride = 2 * blocks + 8;
-      if ((rc = dev_alloc(e, (void**)&e->lnctr, ae_engine::kMaxParts * e->ctr_stride * 4))) return rc;
-      HIPC(hipMemset(e->lnctr, 0, ae_engine::kMaxParts * e->ctr_stride * 4));
+      if ((rc = dev_alloc(e, (void**)&e->lnst2, blocks * 256 * 4 * 8))) return rc;
     }
     e->cap_T = nt;
   }
@@ -408,24 +431,6 @@ int gemm_pk(ae_engine* e, const unsigned short* A, const unsigned short* Wp, con
   return AE_OK;
 }
 
-// The O-projection / FFN2 of the split-precision path over the rows [t0, t0 + M) of part `part`
-// with the layer's residual add and LayerNorm fused into the epilogue by the co-resident exchange
-// (mode 0): x = LN(A·W^T + bias + x), written as f32 and packed planes.  The 4 tiles of a row
-// block are consecutive in one XCD's in-order dispatch, so beside another stream's kernels they
-// still become co-resident (at most one partial group per launch and XCD waits for a CU, and the
-// other kernels' workgroups finish on their own); the bounded wait flags err instead of hanging.
-int gemm_pk_ln(ae_engine* e, const unsigned short* A, const unsigned short* Wp, const float* bias,
-               const float* g, const float* b, int64_t t0, int M, int K, int part,
-               hipStream_t st) {
-  const int H = e->cfg.hidden;
-  Prof p(e, st, e->prof_kind == AE_KIND_GEMM_ANY, 2.0 * M * H * K);
-  float* x = e->x + t0 * H;
-  HIPC(ae_launch_gemm_packed_ln(A, Wp, bias, x, x, e->xp + t0 * H * e->np, M, H, K, e->np, g, b,
-                                e->cfg.ln_eps, e->lnst + t0 * 4, e->lnctr + part * e->ctr_stride,
-                                e->err, st));
-  return AE_OK;
-}
-
 // attention over packed planes: the production loop, or an experiment variant (unmasked launches)
 hipError_t attention_pp(ae_engine* e, const unsigned short* qkvp, float* out, unsigned short* op,
                         const int* cu, const int* q_rows, int max_q, int n, int heads,
@@ -438,54 +443,76 @@ hipError_t attention_pp(ae_engine* e, const unsigned short* qkvp, float* out, un
   return ae_launch_attention_pp(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, st);
 }
 
-// One full encoder layer of the split-precision path over the token rows [t0, t0 + M) of the
-// sequences [s0, s0 + ns) on stream st, with the residual + LayerNorm as their own kernels (the
-// two-stream encoder; results equal the fused path's to LayerNorm rounding).
-int layer_rows(ae_engine* e, const LayerW& w, int64_t t0, int M, int s0, int ns, int max_len,
-               const uint32_t* mask_bits, int L, hipStream_t st, hipEvent_t mark = nullptr,
-               int mark_after = 1, int part = 0) {
+// One full encoder layer li of the split-precision path over the token rows [t0, t0 + M) of the
+// sequences [s0, s0 + ns) on stream st, with both LayerNorms folded into the GEMMs that follow
+// them (gemm_planes.hip FoldArgs): between layers the rows stay pre-LayerNorm (v in e->tmp, its
+// planes in e->xp, its tile statistics in e->lnst / e->lnst2), and
+//   QKV   = fold(v, LN2 of layer li-1)                    (layer 0: the embedding LN's x as it is)
+//   v     = ctx·Wo^T + bo + LN2_{li-1}(v)                 (+ tile statistics -> lnst2)
+//   h     = GELU(fold(v, LN1 of layer li))
+//   v     = h·W2^T + b2 + LN1_li(v)                        (+ tile statistics -> lnst)
+// no LayerNorm pass over the rows, and no exchange between workgroups.  last: the encoder's last
+// full layer, whose output LN2_li(v) is written to e->x (f32) for the CLS path / MLM head.
+// Every row's arithmetic is independent of the part boundaries and of M.
+int layer_rows(ae_engine* e, int li, int64_t t0, int M, int s0, int ns, int max_len,
+               const uint32_t* mask_bits, int L, hipStream_t st, bool last,
+               hipEvent_t mark = nullptr, int mark_after = 1) {
   const int H = e->cfg.hidden, F = e->cfg.ffn, np = e->np;
-  unsigned short* qkvp = reinterpret_cast<unsigned short*>(e->qkv);
+  const LayerW& w = e->layers[li];
+  const LayerW* prev = li > 0 ? &e->layers[li - 1] : nullptr;
+  const float eps = e->cfg.ln_eps;
+  unsigned short* qkvp = reinterpret_cast<unsigned short*>(e->qkv) + t0 * 3 * H * np;
   unsigned short* xp = e->xp + t0 * H * np;
-  float* x = e->x + t0 * H;
-  float* tmp = e->tmp + t0 * H;
-  int rc, k = 0;
+  unsigned short* cp = e->cp + t0 * H * np;
+  unsigned short* hp = e->hp + t0 * F * np;
+  float* v = e->tmp + t0 * H;
+  uint64_t* sa = e->lnst + t0 * 4;   // FFN2 output statistics
+  uint64_t* sb = e->lnst2 + t0 * 4;  // O-projection output statistics
+  int k = 0;
   // records `mark` on st after the mark_after-th kernel of the layer (the second stream's lag)
   auto done = [&]() -> int {
     if (mark && ++k == mark_after) HIPC(hipEventRecord(mark, st));
     return AE_OK;
   };
-  if ((rc = gemm_pk(e, xp, w.wqkv_p, w.bqkv, nullptr, nullptr, qkvp + t0 * 3 * H * np, M, 3 * H, H,
-                    EPI_BIAS_PACKED, st, false)) || (rc = done()))
-    return rc;
+  const bool prof = e->prof_kind == AE_KIND_GEMM_ANY;
+  {
+    Prof p(e, st, prof, 2.0 * M * 3 * H * H);
+    if (prev)
+      HIPC(ae_launch_gemm_packed_fold(xp, w.wqkv_p, w.bqkv_f, w.sqkv, sa, eps, qkvp, M, 3 * H, H,
+                                      0, np, st));
+    else
+      HIPC(ae_launch_gemm_packed(xp, w.wqkv_p, w.bqkv, nullptr, nullptr, qkvp, M, 3 * H, H,
+                                 EPI_BIAS_PACKED, np, st));
+  }
+  if (int rc = done()) return rc;
   {
     Prof p(e, st, e->prof_kind == AE_KIND_ATTENTION, 0.0);
-    HIPC(attention_pp(e, qkvp, e->ctx, e->cp, e->cu + s0, nullptr, max_len, ns,
-                      e->cfg.heads, mask_bits ? mask_bits + (size_t)s0 * L * (L / 32) : nullptr,
-                      L, np, st));
+    HIPC(attention_pp(e, reinterpret_cast<unsigned short*>(e->qkv), e->ctx, e->cp, e->cu + s0,
+                      nullptr, max_len, ns, e->cfg.heads,
+                      mask_bits ? mask_bits + (size_t)s0 * L * (L / 32) : nullptr, L, np, st));
   }
-  if ((rc = done())) return rc;
-  if (e->ln_kind == 2) {
-    if ((rc = gemm_pk_ln(e, e->cp + t0 * H * np, w.wo_p, w.bo, w.ln1g, w.ln1b, t0, M, H, part,
-                         st)) || (rc = done()))
-      return rc;
-  } else {
-    if ((rc = gemm_pk(e, e->cp + t0 * H * np, w.wo_p, w.bo, x, tmp, nullptr, M, H, H,
-                      EPI_BIAS_RESIDUAL, st, false)) || (rc = done()))
-      return rc;
-    HIPC(ae_launch_layernorm(tmp, w.ln1g, w.ln1b, e->cfg.ln_eps, M, x, xp, np, st));
-    if ((rc = done())) return rc;
+  if (int rc = done()) return rc;
+  {
+    Prof p(e, st, prof, 2.0 * M * H * H);
+    HIPC(ae_launch_gemm_packed_res_stats(cp, w.wo_p, w.bo, prev ? v : e->x + t0 * H,
+                                         prev ? sa : nullptr, prev ? prev->ln2g : nullptr,
+                                         prev ? prev->ln2b : nullptr, eps, v, xp, sb, M, H, H, np,
+                                         st));
   }
-  if ((rc = gemm_pk(e, xp, w.w1_p, w.b1, nullptr, nullptr, e->hp + t0 * F * np, M, F, H,
-                    EPI_BIAS_GELU, st, true)) || (rc = done()))
-    return rc;
-  if (e->ln_kind == 2)
-    return gemm_pk_ln(e, e->hp + t0 * F * np, w.w2_p, w.b2, w.ln2g, w.ln2b, t0, M, F, part, st);
-  if ((rc = gemm_pk(e, e->hp + t0 * F * np, w.w2_p, w.b2, x, tmp, nullptr, M, H, F,
-                    EPI_BIAS_RESIDUAL, st, false)) || (rc = done()))
-    return rc;
-  HIPC(ae_launch_layernorm(tmp, w.ln2g, w.ln2b, e->cfg.ln_eps, M, x, xp, np, st));
-  return done();
+  if (int rc = done()) return rc;
+  {
+    Prof p(e, st, prof || e->prof_kind == AE_KIND_GEMM_FFN1, 2.0 * M * F * H);
+    HIPC(ae_launch_gemm_packed_fold(xp, w.w1_p, w.b1_f, w.s1, sb, eps, hp, M, F, H, 1, np, st));
+  }
+  if (int rc = done()) return rc;
+  {
+    Prof p(e, st, prof, 2.0 * M * H * F);
+    HIPC(ae_launch_gemm_packed_res_stats(hp, w.w2_p, w.b2, v, sb, w.ln1g, w.ln1b, eps, v, xp, sa,
+                                         M, H, F, np, st));
+  }
+  if (int rc = done()) return rc;
+  if (last) HIPC(ae_launch_layernorm(v, w.ln2g, w.ln2b, eps, M, e->x + t0 * H, nullptr, 0, st));
+  return AE_OK;
 }
 
 // Runs the encoder over compacted tokens; on return the last-layer CLS rows are in e->xc
@@ -504,33 +531,38 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
                           node_avg ? mask_bits : nullptr, L, e->cu, n, st));
   unsigned short* qkvp = reinterpret_cast<unsigned short*>(e->qkv);  // planes mode: [T][np·3H]
   int first = 0;  // first layer the single-stream loop below runs
-  if (pl && e->split && lens) {
-    // full layers in P parts of the batch (sequence ranges, each on its own stream, every part
-    // one lag behind the previous); one part when n == 1, so every batch size runs the same
-    // per-row arithmetic
+  if (pl) {
+    // the full layers (layer_rows): with two streams in P parts of the batch (sequence ranges,
+    // each on its own stream, every part one lag behind the previous; one part when n == 1),
+    // else one part of all rows on st.  Every row's arithmetic is the same either way.
     const int NLs = cls_only ? NL - 1 : NL;
-    const int P = n < e->split_parts ? n : e->split_parts;
+    const int P = e->split && lens ? (n < e->split_parts ? n : e->split_parts) : (n > 0 ? 1 : 0);
     int s_beg[ae_engine::kMaxParts + 1], ml[ae_engine::kMaxParts];
-    for (int p = 0; p <= P; ++p) s_beg[p] = (int)((int64_t)n * p / P);
+    int64_t r_beg[ae_engine::kMaxParts + 1];
+    for (int p = 0; p <= P; ++p) s_beg[p] = (int)((int64_t)n * p / (P ? P : 1));
     for (int p = 0; p < P; ++p) {
       ml[p] = 0;
-      for (int i = s_beg[p]; i < s_beg[p + 1]; ++i) ml[p] = lens[i] > ml[p] ? lens[i] : ml[p];
+      if (lens)
+        for (int i = s_beg[p]; i < s_beg[p + 1]; ++i) ml[p] = lens[i] > ml[p] ? lens[i] : ml[p];
+      else
+        ml[p] = max_len;
     }
+    // row ranges: host prefix sums of the uploaded lens (all rows for one part)
+    for (int p = 0; p <= P; ++p) r_beg[p] = P == 1 ? (p ? T : 0) : e->pinned_cu[s_beg[p]];
     auto stream_of = [&](int p) { return p == 0 ? st : e->sts[p]; };
     if (P > 1) {
       HIPC(hipEventRecord(e->ev_fork, st));
       for (int p = 1; p < P; ++p) HIPC(hipStreamWaitEvent(e->sts[p], e->ev_fork, 0));
     }
     for (int li = 0; li < NLs; ++li) {
-      const LayerW& w = e->layers[li];
       for (int p = 0; p < P; ++p) {
         if (li == 0 && p > 0) HIPC(hipStreamWaitEvent(e->sts[p], e->ev_lag[p - 1], 0));
-        const int64_t t0 = e->pinned_cu[s_beg[p]];  // host prefix sums of the uploaded lens
-        const int M = (int)(e->pinned_cu[s_beg[p + 1]] - t0);
+        const int64_t t0 = r_beg[p];
+        const int M = (int)(r_beg[p + 1] - t0);
         int rc;
-        if ((rc = layer_rows(e, w, t0, M, s_beg[p], s_beg[p + 1] - s_beg[p], ml[p], mask_bits, L,
-                             stream_of(p), li == 0 && p + 1 < P ? e->ev_lag[p] : nullptr,
-                             e->split_lag, p)))
+        if ((rc = layer_rows(e, li, t0, M, s_beg[p], s_beg[p + 1] - s_beg[p], ml[p], mask_bits, L,
+                             stream_of(p), li == NLs - 1,
+                             li == 0 && p + 1 < P ? e->ev_lag[p] : nullptr, e->split_lag)))
           return rc;
       }
     }
@@ -559,8 +591,13 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
                                    w.wqkv + (size_t)2 * H * H, w.bqkv + 2 * H, e->cu, n, max_len,
                                    mask_bits, L, scale, e->cls_u, e->cls_part, e->cls_y, e->cc,
                                    e->err, st));
+    } else if (pl && li > 0) {
+      // Q | K | V as packed planes (Q pre-scaled) straight into the attention's LDS-DMA, from the
+      // previous layer's pre-LayerNorm rows (the LayerNorm folded in)
+      Prof p(e, st, e->prof_kind == AE_KIND_GEMM_ANY, 2.0 * T * 3 * H * H);
+      HIPC(ae_launch_gemm_packed_fold(e->xp, w.wqkv_p, w.bqkv_f, w.sqkv, e->lnst, eps, qkvp,
+                                      (int)T, 3 * H, H, 0, e->np, st));
     } else if (pl) {
-      // Q | K | V as packed planes (Q pre-scaled) straight into the attention's LDS-DMA
       if ((rc = gemm_pk(e, e->xp, w.wqkv_p, w.bqkv, nullptr, nullptr, qkvp, (int)T, 3 * H, H,
                         EPI_BIAS_PACKED, st, false)))
         return rc;
@@ -579,16 +616,7 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
                           last_cls ? e->one : nullptr, last_cls ? 1 : max_len, n, heads,
                           mask_bits, L, e->np, st));
     }
-    if (!last_cls && pl) {
-      // O-proj + residual + LN1 and FFN2 + residual + LN2 each one kernel (x updated in place)
-      if ((rc = gemm_pk_ln(e, e->cp, w.wo_p, w.bo, w.ln1g, w.ln1b, 0, (int)T, H, 0, st)))
-        return rc;
-      if ((rc = gemm_pk(e, e->xp, w.w1_p, w.b1, nullptr, nullptr, e->hp, (int)T, F, H,
-                        EPI_BIAS_GELU, st, true)))
-        return rc;
-      if ((rc = gemm_pk_ln(e, e->hp, w.w2_p, w.b2, w.ln2g, w.ln2b, 0, (int)T, F, 0, st)))
-        return rc;
-    } else if (!last_cls) {
+    if (!last_cls) {  // the exact-fp32 mode (the split modes ran their full layers above)
       if ((rc = gemm(e, e->ctx, w.wo, w.wo_h, w.wo_l, w.bo, e->x, e->tmp, (int)T, H, H, EPI_BIAS_RESIDUAL,
                      st, false)))
         return rc;
@@ -739,20 +767,35 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
         ae_destroy(e);
         return fail(rc, m);
       }
+      // the planes GEMMs: W_o and W_2 as they are; FFN1 with this layer's LN1 folded in, the QKV
+      // of layers >= 1 with the previous layer's LN2 (layer 0's input is the embedding LN's x)
+      const std::string pp = "encoder.layer." + std::to_string(l - 1) + ".";
+      const ae_weight_view* g1 = view(p + "attention.output.LayerNorm.weight");
+      const ae_weight_view* b1 = view(p + "attention.output.LayerNorm.bias");
+      const ae_weight_view* bi = view(p + "intermediate.dense.bias");
+      const int np = lo ? 2 : 1;
       if (lo) {
-        if ((rc = upload_packed(e, hw.data(), 3 * H, H, &w.wqkv_p)) ||
+        if ((l == 0 && (rc = upload_packed(e, hw.data(), 3 * H, H, &w.wqkv_p))) ||
             (rc = upload_packed(e, vo->data, H, H, &w.wo_p)) ||
-            (rc = upload_packed(e, v1->data, F, H, &w.w1_p)) ||
             (rc = upload_packed(e, v2->data, H, F, &w.w2_p))) {
           std::string m = g_err;
           ae_destroy(e);
           return fail(rc, m);
         }
       } else {
-        w.wqkv_p = w.wqkv_h;
+        if (l == 0) w.wqkv_p = w.wqkv_h;
         w.wo_p = w.wo_h;
-        w.w1_p = w.w1_h;
         w.w2_p = w.w2_h;
+      }
+      if ((rc = upload_folded(e, v1->data, bi->data, g1->data, b1->data, F, H, np, &w.w1_p, &w.s1,
+                              &w.b1_f)) ||
+          (l > 0 && (rc = upload_folded(e, hw.data(), hb.data(),
+                                        view(pp + "output.LayerNorm.weight")->data,
+                                        view(pp + "output.LayerNorm.bias")->data, 3 * H, H, np,
+                                        &w.wqkv_p, &w.sqkv, &w.bqkv_f)))) {
+        std::string m = g_err;
+        ae_destroy(e);
+        return fail(rc, m);
       }
     }
   }
@@ -786,8 +829,6 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
   {
     const char* ca = std::getenv("AE_CLS_ABSORB");  // A/B runs: 0 = full-T QKV + attention
     e->cls_absorb = !(ca && ca[0] == '0');
-    const char* lf = std::getenv("AE_LN_FIX");  // A/B runs: 0 or 2 (see ln_kind)
-    if (lf && (lf[0] == '0' || lf[0] == '2')) e->ln_kind = lf[0] - '0';
     const char* q192 = std::getenv("AE_QKV192");  // A/B runs: 1 = 256 x 192 QKV tiles allowed
     e->qkv192 = q192 && q192[0] == '1';
   }

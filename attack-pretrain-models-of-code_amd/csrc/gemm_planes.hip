@@ -2,7 +2,8 @@
 // (AE_PREC_BF16 / AE_PREC_F32X3).
 //
 // Operands arrive already split into bf16: the weights at engine creation (W = W_hi + W_lo), the
-// activations by the kernel that produced them (LayerNorm, attention, the FFN1 epilogue), so the
+// activations by the kernel that produced them (the embedding LayerNorm, attention, the GEMM
+// epilogues), so the
 // main loop moves and multiplies nothing but bf16.  Packed layout ("NP planes per 128-B block"):
 //   NP = 2 (f32x3): row = K/32 blocks of 128 B, block b = [hi of k 32b..32b+31 | lo of the same]
 //   NP = 1 (bf16):  row = K bf16 (the hi plane)
@@ -11,15 +12,18 @@
 // from ONE load of the four planes.
 //
 // Two kernels, chosen per shape by ae_launch_gemm_packed: gemm_pp_kernel (256 x 256 tiles, every
-// epilogue) and gemm_pp192_kernel (256 x 192 tiles for the N = 768 GEMMs, f32 epilogues and the
-// fused residual + LayerNorm).  Both:
+// epilogue) and gemm_pp192_kernel (256 x 192 tiles for the N = 768 GEMMs: f32 epilogues and the
+// residual + row-statistics epilogue of the folded LayerNorm).  Both:
 //   * operands reach LDS by LDS-DMA (global_load_lds_dwordx4, one wave instruction = 8 rows x
 //     128 B, lane-linear image); the 16-B chunk of row r is XOR-swizzled by (r >> 1) & 7 on the
 //     SOURCE address, so fragment ds_read_b128s of 16 rows hit 16 different bank slots
 //   * DMA issued from inline asm with hand-counted vmcnt (the compiler's wait-count pass would
 //     otherwise drain it before every fragment read); raw s_barrier; XCD-aware tile order
 //   * epilogues: +bias -> f32, +bias+residual -> f32, +bias -> tanh -> f32, +bias -> GELU -> packed
-//     bf16 planes (the FFN2 operand), +bias -> packed planes (QKV), +bias+residual -> LayerNorm
+//     bf16 planes (the FFN2 operand), +bias -> packed planes (QKV), and the folded-LayerNorm pair:
+//     the QKV / FFN1 GEMMs over the PRE-LayerNorm rows with the row's (mean, rstd) applied in the
+//     epilogue (FoldArgs), the O-projection / FFN2 writing f32 + planes + per-tile row statistics
+//     (StatArgs) — no LayerNorm pass over the rows and no exchange between workgroups
 // The round-1 kernel (gemm_pk_kernel, one wave group, 2-3 stage ring), the role-split persistent
 // kernel (gemm_pprs_kernel) and the two-workgroups-per-CU kernel (gemm_w2.hip) were measured
 // slower and removed (git history before round 4; DESIGN.md §3 keeps their numbers).
@@ -35,43 +39,59 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // PK_EPI_BIAS_PACKED: +bias -> packed planes (the QKV output feeding attention_pp.hip); only the
 // ping-pong 256 x 256 kernel has it
-// PK_EPI_RES_LN: +bias +residual -> LayerNorm over the whole 768-wide row -> f32 + packed planes
-// (the O-projection / FFN2 + LayerNorm of every encoder layer; 256 x 192 kernel only, see below)
+// PK_EPI_BIAS_FOLD / PK_EPI_GELU_FOLD: PK_EPI_BIAS_PACKED / PK_EPI_GELU_PACKED whose A operand is
+// the PRE-LayerNorm row v of the previous residual add, with the LayerNorm folded into the GEMM
+// (the QKV and FFN1 GEMMs of the encoder; see FoldArgs)
+// PK_EPI_RES_STATS: +bias +residual -> f32 + packed planes + per-tile row statistics;
+// PK_EPI_RES_STATS_LN: the same with the residual a pre-LayerNorm row, normalised on the fly
+// (see StatArgs; 256 x 192 kernel only).  (Round 4's PK_EPI_RES_LN = 5 — residual + LayerNorm
+// inside the O-projection / FFN2 epilogue, the 4 column tiles of a row block exchanging row
+// statistics as co-resident workgroups — was replaced by the folded form in round 6: DESIGN.md §3.)
 enum { PK_EPI_BIAS = 0, PK_EPI_GELU_PACKED = 1, PK_EPI_RES = 2, PK_EPI_TANH = 3, PK_EPI_BIAS_PACKED = 4,
-       PK_EPI_RES_LN = 5 };
+       PK_EPI_GELU_FOLD = 6, PK_EPI_BIAS_FOLD = 7, PK_EPI_RES_STATS = 8, PK_EPI_RES_STATS_LN = 9 };
 
 // (mean, M2) of a row segment: M2 = sum of squared deviations from the segment mean
 struct RowStat {
   float mean, m2;
 };
 
-// Arguments of the fused residual + LayerNorm epilogue (PK_EPI_RES_LN).
-struct LnArgs {
-  const float* gamma;
-  const float* beta;
+// LayerNorm folded into the following GEMM.  With x = LN(v) = (v - mean) * rstd * g + b,
+//   x·W^T + bias = rstd * (v·W'^T - mean * s) + bias'
+// where W' = W with column k scaled by g[k], s[n] = sum_k W'[n][k] and bias' = bias + W·b (all
+// prepared at engine creation), so the GEMM multiplies the pre-LayerNorm rows v directly and the
+// epilogue applies the row's (mean, rstd) — merged from the 4 per-tile statistics the producing
+// PK_EPI_RES_STATS epilogue wrote.  No LayerNorm pass over the rows.
+struct FoldArgs {
+  const float* s;          // [N]
+  const uint64_t* stats;   // [M rows][4] RowStat of the 4 192-column tiles of each row
   float eps;
-  __bf16* xp;        // packed planes of the LayerNorm output ([M][NP * N])
-  uint64_t* stats;   // [tiles_m * 256][4] (mean, M2) of each row over each 192-column tile
-  int* arrive;       // [tiles_m] arrivals per 256-row block (self-resetting, zero between launches)
-  int* depart;       // [tiles_m]
-  int* err;          // set to 2 if a row block's partners never arrived (bounded wait)
-  int mode;          // 0 = production (the co-resident exchange: partners wait for each
-                     // other's statistics); timing experiments (results WRONG for 1): 1 = no
-                     // exchange (each tile normalises with its own 192 columns' statistics),
-                     // 2 = mode 0 in the grouped XCD tile order of the other epilogues, 3 = row
-                     // blocks interleaved over the XCDs, 4 = mode 0 with the previous 8-B plane
-                     // stores.  (A mode 5 — the row block's last-arriving tile normalising the
-                     // whole block, no co-residency — measured 1.5-3 ms per step slower and was
-                     // removed in round 4)
 };
 
-// The LayerNorm timing modes 1-4 exist only in the tools library (built with -DAE_TOOLS from
-// these sources, lib/libalert_engine_tools.so); the product library compiles mode 0 alone.
-#ifdef AE_TOOLS
-#define LN_MODE(a) ((a).mode)
-#else
-#define LN_MODE(a) 0
-#endif
+// (mean, rstd) of a 768-wide row from its 4 tile statistics (n = 192 each), merged as (0,1),
+// (2,3), then the halves — the order every consumer uses, so every kernel gets the same bits
+__device__ __forceinline__ void row_norm(const uint64_t* st, float eps, float& mean, float& rstd) {
+  RowStat p[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) p[q] = __builtin_bit_cast(RowStat, st[q]);
+  const float d01 = p[0].mean - p[1].mean, d23 = p[2].mean - p[3].mean;
+  const float m01 = (p[0].mean + p[1].mean) * 0.5f, m23 = (p[2].mean + p[3].mean) * 0.5f;
+  const float q01 = (p[0].m2 + p[1].m2) + 96.f * d01 * d01;
+  const float q23 = (p[2].m2 + p[3].m2) + 96.f * d23 * d23;
+  const float d = m01 - m23;
+  mean = (m01 + m23) * 0.5f;
+  const float var = ((q01 + q23) + 192.f * d * d) * (1.f / 768.f);
+  rstd = rsqrtf(var + eps);
+}
+
+// Arguments of the PK_EPI_RES_STATS(_LN) epilogue (gemm_pp192_kernel).
+struct StatArgs {
+  const float* gamma;      // _LN: the residual's LayerNorm gain / shift
+  const float* beta;
+  float eps;
+  __bf16* xp;              // packed planes of the output v ([M][NP * N])
+  uint64_t* stats;         // [M][4] RowStat of each output row over each 192-column tile
+  const uint64_t* rstats;  // _LN: the residual's own tile statistics
+};
 
 namespace {
 constexpr int PK_ROWB = 128;
@@ -163,7 +183,7 @@ template <int NP, int EPI, int DIAG>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
     const __bf16* __restrict__ A, const __bf16* __restrict__ W, const float* __restrict__ bias,
     const float* __restrict__ R, float* __restrict__ C, __bf16* __restrict__ Cp, int M, int N,
-    int K, int group_m) {
+    int K, int group_m, FoldArgs fold) {
   extern __shared__ __attribute__((aligned(16))) unsigned char pk_smem[];
   constexpr int BM = 256, BN = 256, ROWB = PK_ROWB;
   constexpr int A_BYTES = BM * ROWB, STAGE = (BM + BN) * ROWB;  // 64 KiB per K-tile
@@ -374,16 +394,39 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
   // instruction writes (lanes 0-31) would meet rows r and r + 16 on the same banks under a plain
   // (row & 15) swizzle: pk_swz also flips chunk bit 3 for rows 16-31 (the round-3 counters put
   // exactly 2048 conflict cycles on every 256 x 256 tile, profiles/r3ap_pmc_sq.json).
-  constexpr bool PACKED = EPI == PK_EPI_GELU_PACKED || EPI == PK_EPI_BIAS_PACKED;
+  constexpr bool FOLD = EPI == PK_EPI_GELU_FOLD || EPI == PK_EPI_BIAS_FOLD;
+  constexpr bool GELU = EPI == PK_EPI_GELU_PACKED || EPI == PK_EPI_GELU_FOLD;
+  constexpr bool PACKED = GELU || FOLD || EPI == PK_EPI_BIAS_PACKED;
   constexpr int RB = PACKED ? 64 * 2 * NP : 256;  // bytes of a row segment
   constexpr int CPR = RB / 16;                                       // 16-B chunks per row
   unsigned char* reg = pk_smem + wave * 16384;
   const int cb0 = n0 + wn * 64;
+  // folded LayerNorm: (mean, rstd) of this lane's 4 rows (rows past M read row M - 1; not
+  // stored), all 16 statistics loads issued together — one memory latency per tile, not four
+  float fneg[4] = {0.f, 0.f, 0.f, 0.f}, frs[4] = {1.f, 1.f, 1.f, 1.f};
+  if constexpr (FOLD) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float mu;
+      row_norm(fold.stats + (size_t)min(m0 + wm * 128 + r * 32 + li, M - 1) * 4, fold.eps, mu, frs[r]);
+      fneg[r] = -mu;
+    }
+  }
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt) {
       const int lr = tt * 32 + li;  // row within the half
+      const float* fbias = bias;
+      const float* fs = fold.s;
+      if constexpr (FOLD) {
+        // opaque per row pass: the bias / s columns are re-read (L1 hits) instead of held live
+        // across the four passes
+        int z = 0;
+        asm volatile("" : "+s"(z));
+        fbias += z;
+        fs += z;
+      }
 #pragma unroll
       for (int tn = 0; tn < 2; ++tn) {
         if constexpr (PACKED) {
@@ -399,13 +442,22 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
           for (int j = 0; j < 4; ++j) {
             const int cc = tn * 32 + 8 * j + 4 * lh;  // column within the wave's 64
             const int col = cb0 + cc < N ? cb0 + cc : N - 4;
-            const floatx4 bv = *reinterpret_cast<const floatx4*>(bias + col);
+            const floatx4 bv = *reinterpret_cast<const floatx4*>(fbias + col);
+            if constexpr (FOLD) {  // rstd * (acc - mean * s) + bias'
+              const floatx4 sv = *reinterpret_cast<const floatx4*>(fs + col);
 #pragma unroll
-            for (int i = 0; i < 4; i += 2) {
-              y[2 * j + i / 2] = gelu_f2{c[4 * j + i], c[4 * j + i + 1]} + gelu_f2{bv[i], bv[i + 1]};
+              for (int i = 0; i < 4; i += 2)
+                y[2 * j + i / 2] = __builtin_elementwise_fma(
+                    __builtin_elementwise_fma(gelu_f2{sv[i], sv[i + 1]}, gelu_f2(fneg[2 * half + tt]),
+                                              gelu_f2{c[4 * j + i], c[4 * j + i + 1]}),
+                    gelu_f2(frs[2 * half + tt]), gelu_f2{bv[i], bv[i + 1]});
+            } else {
+#pragma unroll
+              for (int i = 0; i < 4; i += 2)
+                y[2 * j + i / 2] = gelu_f2{c[4 * j + i], c[4 * j + i + 1]} + gelu_f2{bv[i], bv[i + 1]};
             }
           }
-          if constexpr (EPI == PK_EPI_GELU_PACKED) gelu_exp2_pairs(y);
+          if constexpr (GELU) gelu_exp2_pairs(y);
 #pragma unroll
           for (int k = 0; k < 8; ++k) split_pair(y[k], hw[k >> 1][k & 1], lw[k >> 1][k & 1]);
 #pragma unroll
@@ -514,7 +566,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
 template <int NP, int EPI, bool NT = false>
 __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
     const __bf16* __restrict__ A, const __bf16* __restrict__ W, const float* __restrict__ bias,
-    const float* R, float* C, int M, int N, int K, int group_m, LnArgs ln) {
+    const float* R, float* C, int M, int N, int K, int group_m, StatArgs ln) {
   extern __shared__ __attribute__((aligned(16))) unsigned char pk_smem[];
   constexpr int BM = 256, BN = 192, ROWB = PK_ROWB;
   constexpr int A_BYTES = BM * ROWB, STAGE = (BM + BN) * ROWB;  // 56 KiB per K-tile
@@ -522,26 +574,11 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
 
   const int tiles_n = (N + BN - 1) / BN;
   const int tiles_m = (M + BM - 1) / BM;
-  int tm0, tn0;
-  if (EPI == PK_EPI_RES_LN && LN_MODE(ln) != 2) {
-    // The 4 N-tiles of a 256-row block exchange row statistics, so they must be co-resident:
-    // blocks b, b+8, b+16, b+24 (one XCD, consecutive in its in-order dispatch) take the row
-    // block's 4 tiles; XCD x owns the contiguous row blocks [x * per, x * per + per) (mode 3:
-    // the XCDs interleave row blocks instead).  Grid = 32 * per; blocks past the last row block
-    // leave before any exchange (all four partners of one do).
-    const int k = blockIdx.x >> 3, per = (tiles_m + 7) / 8;
-    tn0 = k & 3;
-    tm0 = LN_MODE(ln) == 3 ? (k >> 2) * 8 + (blockIdx.x & 7) : (blockIdx.x & 7) * per + (k >> 2);
-    if (tm0 >= tiles_m) return;
-  } else {
-    if (EPI == PK_EPI_RES_LN && (int)blockIdx.x >= tiles_m * tiles_n) return;
-    const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-    const int per_group = group_m * tiles_n;
-    const int g = t / per_group, first_m = g * group_m;
-    const int gsize = min(tiles_m - first_m, group_m);
-    tm0 = first_m + (t - g * per_group) % gsize;
-    tn0 = (t - g * per_group) / gsize;
-  }
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int per_group = group_m * tiles_n;
+  const int g = t / per_group, first_m = g * group_m;
+  const int gsize = min(tiles_m - first_m, group_m);
+  const int tm0 = first_m + (t - g * per_group) % gsize, tn0 = (t - g * per_group) / gsize;
   const int m0 = tm0 * BM, n0 = tn0 * BN;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -686,21 +723,29 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
   }
   if (wm == 0) sync_load();  // same barrier count in both groups; every LDS read and DMA done
 
-  if constexpr (EPI == PK_EPI_RES_LN) {
-    // ---- fused residual + LayerNorm (rowops.hip layernorm_kernel's formula over the 768-wide
-    // row, whose 4 x 192 columns live in the 4 partner workgroups of this row block).
-    // acc[tm][tn] register 4 j + i of lane l = row wm*128 + sm*64 + tm*32 + (l & 31), column
-    // sn*96 + tn*32 + 8 j + 4 (l >> 5) + i of the tile (the transposed MFMA product).
+  if constexpr (EPI == PK_EPI_RES_STATS || EPI == PK_EPI_RES_STATS_LN) {
+    // ---- v = (acc + bias) + residual as f32 and packed planes, plus this tile's (mean, M2) of
+    // every row: the producing half of the folded LayerNorm (FoldArgs) — the O-projection / FFN2
+    // of every encoder layer.  The layer input x = LN(v_prev) is never stored: in the _LN form
+    // the residual rows are the previous pre-LayerNorm rows v_prev, normalised here with their
+    // own statistics (rowops.hip layernorm_kernel's formula); otherwise the residual is used as
+    // it is (layer 0: the embedding LayerNorm's output).  acc[tm][tn] register 4 j + i of lane l
+    // = row wm*128 + sm*64 + tm*32 + (l & 31), column sn*96 + tn*32 + 8 j + 4 (l >> 5) + i of
+    // the tile (the transposed MFMA product).  R may alias C: every element is read before this
+    // workgroup writes it, and no other workgroup touches this tile.
     const int cb0 = n0 + sn * 96;
     const int rb0 = m0 + wm * 128 + sm * 64 + li;  // + 32 tm
-    // (1) v = (acc + bias) + residual.  The residual rows come in coalesced (whole 384-B row
-    // segments, 16 B per lane) into the wave's LDS region — f32 rows of 400 B, conflict-free
-    // both ways — and go back out in the accumulator layout, one 32-row pass (tm) at a time.
-    // R may alias C: every element is read here before this workgroup writes it, and no other
-    // workgroup touches this tile.
     constexpr int RS = 400;
     unsigned char* reg = pk_smem + wave * 32 * RS;
-    const int prow0 = m0 + wm * 128 + sm * 64;  // first row of the wave's 64-row block
+    const int prow0 = m0 + wm * 128 + sm * 64;
+    constexpr bool rnorm = EPI == PK_EPI_RES_STATS_LN;
+    // the residual rows' (mean, rstd) for both passes, their 8 statistics loads issued together
+    float rmu[2] = {0.f, 0.f}, rrs[2] = {1.f, 1.f};
+    if constexpr (rnorm) {
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+        row_norm(ln.rstats + (size_t)min(rb0 + 32 * tm, M - 1) * 4, ln.eps, rmu[tm], rrs[tm]);
+    }
 #pragma unroll
     for (int tm = 0; tm < 2; ++tm) {
 #pragma unroll
@@ -711,21 +756,38 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
                                   : floatx4{0.f, 0.f, 0.f, 0.f};
         *reinterpret_cast<floatx4*>(reg + lr * RS + c * 16) = f;
       }
+      // opaque per pass: the column vectors are re-read (L1 hits), not held live across passes
+      int z = 0;
+      asm volatile("" : "+s"(z));
+      const float* pb = bias + z;
+      const float* pg = ln.gamma + z;
+      const float* pt = ln.beta + z;
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 #pragma unroll
       for (int tn = 0; tn < 3; ++tn)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int col = cb0 + tn * 32 + 8 * j + 4 * lh;
-          const floatx4 bv = *reinterpret_cast<const floatx4*>(bias + col);
-          const floatx4 rv = *reinterpret_cast<const floatx4*>(reg + li * RS + (tn * 8 + 2 * j + lh) * 16);
+          const floatx4 bv = *reinterpret_cast<const floatx4*>(pb + col);
+          floatx4 rv = *reinterpret_cast<const floatx4*>(reg + li * RS + (tn * 8 + 2 * j + lh) * 16);
+          if constexpr (rnorm) {
+            const floatx4 gg = *reinterpret_cast<const floatx4*>(pg + col);
+            const floatx4 bb = *reinterpret_cast<const floatx4*>(pt + col);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) acc[tm][tn][4 * j + i] = (acc[tm][tn][4 * j + i] + bv[i]) + rv[i];
+            for (int i = 0; i < 4; ++i) rv[i] = (rv[i] - rmu[tm]) * rrs[tm] * gg[i] + bb[i];
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            acc[tm][tn][4 * j + i] = (acc[tm][tn][4 * j + i] + bv[i]) + rv[i];
+            // computed here, not sunk to the statistics below (which would keep every loaded
+            // column vector live until then and spill)
+            asm volatile("" : "+v"(acc[tm][tn][4 * j + i]));
+          }
         }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read back before the next pass rewrites
     }
-    // (2) per row over the wave's 96 columns: mean and M2 (sum of squared deviations); the two
-    // lane halves hold 48 columns each
+    // per row over the wave's 96 columns (the lane halves hold 48 each), then the two waves of a
+    // row (sn = 0, 1) merged through LDS in sn order
     float mean96[2], m2_96[2];
 #pragma unroll
     for (int tm = 0; tm < 2; ++tm) {
@@ -748,131 +810,35 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
       mean96[tm] = mu;
       m2_96[tm] = q;
     }
-    // (3) the two waves of a row (sn = 0, 1) combine through LDS (Chan's pairwise merge, n = 96
-    // each, always in sn order so both get the same bits)
-    // [8 waves][2 tm][32 rows], past the 8 wave regions
     RowStat* lst = reinterpret_cast<RowStat*>(pk_smem + 8 * 32 * RS);
     if (lh == 0) {
 #pragma unroll
       for (int tm = 0; tm < 2; ++tm) lst[(wave * 2 + tm) * 32 + li] = RowStat{mean96[tm], m2_96[tm]};
     }
     __syncthreads();
-    RowStat tile[2];
-#pragma unroll
-    for (int tm = 0; tm < 2; ++tm) {
-      const RowStat o = lst[((wave ^ 1) * 2 + tm) * 32 + li];
-      const RowStat mine{mean96[tm], m2_96[tm]};
-      const RowStat a = sn == 0 ? mine : o;
-      const RowStat b = sn == 0 ? o : mine;
-      const float d = a.mean - b.mean;
-      tile[tm] = RowStat{(a.mean + b.mean) * 0.5f, (a.m2 + b.m2) + 48.f * d * d};
-    }
-    // (4) publish this tile's (mean, M2) of its 256 rows; one lane signals for the workgroup
-    // after every wave's stores have completed (agent-scope 8-B stores / loads, L2-coherent:
-    // the partners share this XCD's L2, and the loads skip the CU's L1)
-    // (rows past M publish nothing: the two-stream engine's parts share one statistics array,
-    // and a part's first rows sit where the previous part's padding rows would land)
     if (sn == 0 && lh == 0) {
 #pragma unroll
-      for (int tm = 0; tm < 2; ++tm)
-        if (rb0 + 32 * tm < M)
-          __hip_atomic_store(ln.stats + ((size_t)(rb0 + 32 * tm) * 4 + tn0),
-                             __builtin_bit_cast(uint64_t, tile[tm]), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0 && LN_MODE(ln) != 1) {
-      // release / acquire at agent scope around the exchange (the workgroup's statistics stores
-      // are ordered before the arrival, the partners' after the wait)
-      __hip_atomic_fetch_add(ln.arrive + tm0, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      // bounded wait (~1 s): a partner that never arrives flags the engine instead of hanging
-      int ok = 0;
-      for (int spin = 0; spin < (1 << 20); ++spin) {
-        if (__hip_atomic_load(ln.arrive + tm0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= tiles_n) {
-          ok = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      if (!ok) __hip_atomic_store(ln.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    // (5) the row's statistics over all 768 columns: merge the 4 tiles ((0,1), (2,3), then the
-    // halves), the same order in every workgroup and wave
-    float mean[2], rstd[2];
-#pragma unroll
-    for (int tm = 0; tm < 2; ++tm) {
-      RowStat p[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        p[q] = LN_MODE(ln) == 1 ? tile[tm]
-                            : __builtin_bit_cast(RowStat, __hip_atomic_load(
-                                  ln.stats + (size_t)(rb0 + 32 * tm) * 4 + q, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT));
-      const float d01 = p[0].mean - p[1].mean, d23 = p[2].mean - p[3].mean;
-      const float m01 = (p[0].mean + p[1].mean) * 0.5f, m23 = (p[2].mean + p[3].mean) * 0.5f;
-      const float q01 = (p[0].m2 + p[1].m2) + 96.f * d01 * d01;
-      const float q23 = (p[2].m2 + p[3].m2) + 96.f * d23 * d23;
-      const float d = m01 - m23;
-      mean[tm] = (m01 + m23) * 0.5f;
-      const float var = ((q01 + q23) + 192.f * d * d) * (1.f / 768.f);
-      rstd[tm] = rsqrtf(var + ln.eps);
-    }
-    __syncthreads();  // every wave has read the statistics
-    if (tid == 0 && LN_MODE(ln) != 1) {
-      // the last of the 4 partners to leave re-arms the counters for the next launch
-      if (__hip_atomic_fetch_add(ln.depart + tm0, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-          tiles_n - 1) {
-        __hip_atomic_store(ln.arrive + tm0, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(ln.depart + tm0, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int tm = 0; tm < 2; ++tm) {
+        const RowStat o = lst[((wave ^ 1) * 2 + tm) * 32 + li];
+        const float d = mean96[tm] - o.mean;
+        const RowStat t{(mean96[tm] + o.mean) * 0.5f, (m2_96[tm] + o.m2) + 48.f * d * d};
+        if (rb0 + 32 * tm < M) ln.stats[(size_t)(rb0 + 32 * tm) * 4 + tn0] = __builtin_bit_cast(uint64_t, t);
       }
     }
-    // (6) normalise in registers; through the wave's LDS region again, write x (f32) and its
-    // packed planes as whole row segments (384 B of x, three 128-B [hi | lo] blocks of planes)
+    // v through the wave's LDS region again: x-style whole row segments (two 16-B f32 stores and
+    // one 16-B store per plane for 8 consecutive columns of a row per lane)
 #pragma unroll
     for (int tm = 0; tm < 2; ++tm) {
 #pragma unroll
       for (int tn = 0; tn < 3; ++tn)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int col = cb0 + tn * 32 + 8 * j + 4 * lh;
-          const floatx4 gg = *reinterpret_cast<const floatx4*>(ln.gamma + col);
-          const floatx4 bb = *reinterpret_cast<const floatx4*>(ln.beta + col);
           floatx4 o;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) o[i] = (acc[tm][tn][4 * j + i] - mean[tm]) * rstd[tm] * gg[i] + bb[i];
+          for (int i = 0; i < 4; ++i) o[i] = acc[tm][tn][4 * j + i];
           *reinterpret_cast<floatx4*>(reg + li * RS + (tn * 8 + 2 * j + lh) * 16) = o;
         }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (LN_MODE(ln) == 4) {  // timing A/B only: the previous 4-column form (8-B plane stores)
-#pragma unroll
-        for (int k = 0; k < 12; ++k) {
-          const int idx = k * 64 + lane, lr = idx / 24, c = idx % 24;
-          const int row = prow0 + tm * 32 + lr;
-          const floatx4 o = *reinterpret_cast<const floatx4*>(reg + lr * RS + c * 16);
-          if (row < M) {
-            const int col = cb0 + 4 * c;
-            *reinterpret_cast<floatx4*>(C + (size_t)row * N + col) = o;
-            ushortx4 h, l;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              h[i] = f2bf(o[i]);
-              l[i] = f2bf(o[i] - __builtin_bit_cast(float, (uint32_t)h[i] << 16));
-            }
-            unsigned short* dst = reinterpret_cast<unsigned short*>(ln.xp) + (size_t)row * NP * N +
-                                  (size_t)(col >> 5) * 32 * NP + (col & 31);
-            *reinterpret_cast<ushortx4*>(dst) = h;
-            if (NP == 2) *reinterpret_cast<ushortx4*>(dst + 32) = l;
-          }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        continue;
-      }
-      // 8 consecutive columns per lane: x as two 16-B stores, each plane as one 16-B store (24
-      // store instructions per pass, all 16 B per lane; was 36, two thirds of them 8 B)
-      // round k = 3 g + kk: round kk's chunks 16 g rows further down (see the f32 epilogue)
 #pragma unroll
       for (int k = 0; k < 6; ++k) {
         const int kk = k % 3, g = k / 3;
@@ -882,18 +848,14 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
         const floatx4 o1 = *reinterpret_cast<const floatx4*>(reg + lr * RS + c8 * 32 + 16);
         if (row < M) {
           const int col = cb0 + 8 * c8;
-          float* const xrow = C + (size_t)prow0 * N + (uint32_t)(lr + tm * 32) * (uint32_t)N;
-          *reinterpret_cast<floatx4*>(xrow + col) = o0;
-          *reinterpret_cast<floatx4*>(xrow + col + 4) = o1;
-          uint32_t h[4], l[4];
+          float* const vrow = C + (size_t)prow0 * N + (uint32_t)(lr + tm * 32) * (uint32_t)N;
+          *reinterpret_cast<floatx4*>(vrow + col) = o0;
+          *reinterpret_cast<floatx4*>(vrow + col + 4) = o1;
+          uint32_t h[4], l[4];  // column pairs as packed bf16 conversions (split_pair)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float a = i < 2 ? o0[2 * i] : o1[2 * i - 4], b = i < 2 ? o0[2 * i + 1] : o1[2 * i - 3];
-            const uint32_t ha = f2bf(a), hb = f2bf(b);
-            h[i] = ha | (hb << 16);
-            l[i] = (uint32_t)f2bf(a - __builtin_bit_cast(float, ha << 16)) |
-                   ((uint32_t)f2bf(b - __builtin_bit_cast(float, hb << 16)) << 16);
-          }
+          for (int i = 0; i < 4; ++i)
+            split_pair(i < 2 ? gelu_f2{o0[2 * i], o0[2 * i + 1]} : gelu_f2{o1[2 * i - 4], o1[2 * i - 3]},
+                       h[i], l[i]);
           unsigned short* dst = reinterpret_cast<unsigned short*>(ln.xp) + (size_t)prow0 * NP * N +
                                 (uint32_t)(lr + tm * 32) * (uint32_t)(NP * N) +
                                 (uint32_t)((col >> 5) * 32 * NP + (col & 31));
@@ -1023,7 +985,8 @@ constexpr int PP_PERSIST = 9;
 
 template <int NP, int EPI, int DIAG>
 hipError_t pp_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R, float* C,
-                     __bf16* Cp, int M, int N, int K, int group_m, hipStream_t st) {
+                     __bf16* Cp, int M, int N, int K, int group_m, hipStream_t st,
+                     FoldArgs fold = FoldArgs{}) {
   constexpr int lds = 2 * (256 + 256) * PK_ROWB;  // 128 KiB
   if (hipError_t e = ensure_dynamic_lds((const void*)gemm_pp_kernel<NP, EPI, DIAG>, lds); e != hipSuccess)
     return e;
@@ -1031,7 +994,7 @@ hipError_t pp_launch(const __bf16* A, const __bf16* W, const float* bias, const 
   // persistent grid (one workgroup per CU looping over the tiles) or one workgroup per tile
   const int grid = DIAG == PP_PERSIST ? std::min(tiles, cu_count()) : tiles;
   hipLaunchKernelGGL((gemm_pp_kernel<NP, EPI, DIAG>), dim3(grid), dim3(512), lds, st, A, W, bias,
-                     R, C, Cp, M, N, K, group_m);
+                     R, C, Cp, M, N, K, group_m, fold);
   return hipGetLastError();
 }
 
@@ -1061,13 +1024,12 @@ hipError_t pp_epi(int epi, const __bf16* A, const __bf16* W, const float* bias, 
 template <int NP, int EPI, bool NT = false>
 hipError_t pp192_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R,
                         float* C, int M, int N, int K, int group_m, hipStream_t st,
-                        LnArgs ln = LnArgs{}) {
+                        StatArgs ln = StatArgs{}) {
   constexpr int lds = 2 * (256 + 192) * PK_ROWB;  // 112 KiB
   if (hipError_t e = ensure_dynamic_lds((const void*)gemm_pp192_kernel<NP, EPI, NT>, lds); e != hipSuccess)
     return e;
   const int tiles_m = (M + 255) / 256;
-  const int tiles = EPI == PK_EPI_RES_LN && LN_MODE(ln) != 2 ? 32 * ((tiles_m + 7) / 8)
-                                                        : tiles_m * ((N + 191) / 192);
+  const int tiles = tiles_m * ((N + 191) / 192);
   hipLaunchKernelGGL((gemm_pp192_kernel<NP, EPI, NT>), dim3(tiles), dim3(512), lds, st, A, W, bias, R,
                      C, M, N, K, group_m, ln);
   return hipGetLastError();
@@ -1183,52 +1145,53 @@ extern "C" hipError_t ae_launch_gemm_packed_qkv192(const unsigned short* A, cons
 }
 
 
-// C = LayerNorm(A·W^T + bias + R) over rows of N = 768 (the O-projection / FFN2 + LayerNorm of an
-// encoder layer), written as f32 C [M][768] and packed planes Cp [M][np*768]; R may equal C.
-// stats: [(M + 255) / 256 * 256][4] 8-B words; ctr: 2 * ((M + 255) / 256) ints, zero on the first
-// call (the kernel leaves them zero); err: the engine's device error word.
-namespace {
-hipError_t packed_ln(const unsigned short* A, const unsigned short* W, const float* bias,
-                     const float* R, float* C, unsigned short* Cp, int M, int N, int K, int np,
-                     const float* gamma, const float* beta, float eps, uint64_t* stats, int* ctr,
-                     int* err, int mode, hipStream_t st) {
+// The folded-LayerNorm pair (FoldArgs).  Cp = packed planes of
+//   gelu = 0: rstd * (A·W'^T - mean * s) + bias'          (the QKV GEMM of layers >= 1)
+//   gelu = 1: GELU(rstd * (A·W'^T - mean * s) + bias')    (FFN1)
+// A: the packed planes of the pre-LayerNorm rows v; stats: their [M][4] tile statistics.
+extern "C" hipError_t ae_launch_gemm_packed_fold(const unsigned short* A, const unsigned short* W,
+                                                 const float* bias, const float* s,
+                                                 const uint64_t* stats, float eps,
+                                                 unsigned short* Cp, int M, int N, int K, int gelu,
+                                                 int np, hipStream_t st) {
   if (M <= 0) return hipSuccess;
-  if (N != 768 || K % 64 != 0 || (np != 1 && np != 2) || !bias || !R || !C || !Cp || !gamma ||
-      !beta || !stats || !ctr || !err)
-    return hipErrorInvalidValue;
-  const int tiles_m = (M + 255) / 256;
-  LnArgs ln{gamma, beta, eps, reinterpret_cast<__bf16*>(Cp), stats, ctr, ctr + tiles_m, err, mode};
+  if (!pk_shape_ok(M, N, K, np) || !bias || !s || !stats || !Cp) return hipErrorInvalidValue;
+  const FoldArgs fold{s, stats, eps};
   auto a = reinterpret_cast<const __bf16*>(A);
   auto w = reinterpret_cast<const __bf16*>(W);
-  if (np == 2) return pp192_launch<2, PK_EPI_RES_LN>(a, w, bias, R, C, M, N, K, PK_GROUP_M, st, ln);
-  return pp192_launch<1, PK_EPI_RES_LN>(a, w, bias, R, C, M, N, K, PK_GROUP_M, st, ln);
+  __bf16* cp = reinterpret_cast<__bf16*>(Cp);
+  if (np == 2)
+    return gelu ? pp_launch<2, PK_EPI_GELU_FOLD, 0>(a, w, bias, nullptr, nullptr, cp, M, N, K, PK_GROUP_M, st, fold)
+                : pp_launch<2, PK_EPI_BIAS_FOLD, 0>(a, w, bias, nullptr, nullptr, cp, M, N, K, PK_GROUP_M, st, fold);
+  return gelu ? pp_launch<1, PK_EPI_GELU_FOLD, 0>(a, w, bias, nullptr, nullptr, cp, M, N, K, PK_GROUP_M, st, fold)
+              : pp_launch<1, PK_EPI_BIAS_FOLD, 0>(a, w, bias, nullptr, nullptr, cp, M, N, K, PK_GROUP_M, st, fold);
 }
-}  // namespace
 
-extern "C" hipError_t ae_launch_gemm_packed_ln(const unsigned short* A, const unsigned short* W,
-                                               const float* bias, const float* R, float* C,
-                                               unsigned short* Cp, int M, int N, int K, int np,
-                                               const float* gamma, const float* beta, float eps,
-                                               uint64_t* stats, int* ctr, int* err,
-                                               hipStream_t st) {
-  return packed_ln(A, W, bias, R, C, Cp, M, N, K, np, gamma, beta, eps, stats, ctr, err, 0, st);
+// v = A·W^T + bias + r over rows of N = 768 (the O-projection / FFN2), written as f32 C and packed
+// planes Cp, with the (mean, M2) of every row over each of its 4 192-column tiles into stats
+// ([M][4] 8-B words).  r = R as it is when rstats is null, else r = LN(R) with R's own tile
+// statistics rstats and gamma / beta (R a pre-LayerNorm row).  R may equal C.
+extern "C" hipError_t ae_launch_gemm_packed_res_stats(
+    const unsigned short* A, const unsigned short* W, const float* bias, const float* R,
+    const uint64_t* rstats, const float* gamma, const float* beta, float eps, float* C,
+    unsigned short* Cp, uint64_t* stats, int M, int N, int K, int np, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  if (N != 768 || K % 64 != 0 || (np != 1 && np != 2) || !bias || !R || !C || !Cp || !stats ||
+      (rstats && (!gamma || !beta)))
+    return hipErrorInvalidValue;
+  const StatArgs ln{gamma, beta, eps, reinterpret_cast<__bf16*>(Cp), stats, rstats};
+  auto a = reinterpret_cast<const __bf16*>(A);
+  auto w = reinterpret_cast<const __bf16*>(W);
+  if (rstats)
+    return np == 2 ? pp192_launch<2, PK_EPI_RES_STATS_LN>(a, w, bias, R, C, M, N, K, PK_GROUP_M, st, ln)
+                   : pp192_launch<1, PK_EPI_RES_STATS_LN>(a, w, bias, R, C, M, N, K, PK_GROUP_M, st, ln);
+  return np == 2 ? pp192_launch<2, PK_EPI_RES_STATS>(a, w, bias, R, C, M, N, K, PK_GROUP_M, st, ln)
+                 : pp192_launch<1, PK_EPI_RES_STATS>(a, w, bias, R, C, M, N, K, PK_GROUP_M, st, ln);
 }
 
 #ifdef AE_TOOLS
 // ---- tools library only (lib/libalert_engine_tools.so, -DAE_TOOLS): timing experiments whose
 // variants give WRONG results on purpose; the product library exports none of this.
-
-// Timing experiments of the fused residual + LayerNorm GEMM (tools/gemm_bench.py): `mode` as
-// LnArgs::mode.  Not part of include/alert_engine.h.
-extern "C" hipError_t ae_bench_gemm_packed_ln(const unsigned short* A, const unsigned short* W,
-                                              const float* bias, const float* R, float* C,
-                                              unsigned short* Cp, int M, int N, int K, int np,
-                                              const float* gamma, const float* beta, float eps,
-                                              uint64_t* stats, int* ctr, int* err, int mode,
-                                              hipStream_t st) {
-  if (mode < 0 || mode > 4) return hipErrorInvalidValue;
-  return packed_ln(A, W, bias, R, C, Cp, M, N, K, np, gamma, beta, eps, stats, ctr, err, mode, st);
-}
 
 // Kernel experiments (tools/gemm_bench.py, tests): explicit tile width (0 = the production choice)
 // and a diagnostic variant (0 = the production kernel; see DIAG above — values 1-7 give WRONG

@@ -315,60 +315,137 @@ def test_attention_pp_restructured_loops_bit_identical(gpu, case):
     assert torch.equal(outs[72], outs[6])  # exp / split and the next S MFMAs hand-interleaved
 
 
-@pytest.mark.parametrize("M,K,np_", [(300, 768, 2), (512, 3072, 2), (1000, 768, 1), (37, 768, 2),
-                                     (4097, 768, 2)])
-def test_gemm_packed_ln_matches_f64(gpu, M, K, np_):
-    """ae_launch_gemm_packed_ln (256 x 192 kernel, PK_EPI_RES_LN): x = LayerNorm(A·W^T + bias + x)
-    over 768-wide rows whose 4 column tiles live in 4 workgroups that exchange row statistics.
-    Against float64 of the split products; the residual aliases the output (in place, as the
-    engine runs it); three launches in a row reuse the self-resetting row-block counters (a
-    counter left non-zero would make a later launch read stale statistics or time out)."""
+def _fold_lib():
     lib = _lib()
-    vp, i32 = ctypes.c_void_p, ctypes.c_int32
-    lib.ae_launch_gemm_packed_ln.argtypes = [vp] * 6 + [i32] * 4 + [vp, vp, ctypes.c_float] + \
-        [vp] * 4
-    lib.ae_launch_gemm_packed_ln.restype = ctypes.c_int
+    vp, i32, f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_float
+    lib.ae_launch_gemm_packed_fold.argtypes = [vp] * 5 + [f32, vp] + [i32] * 5 + [vp]
+    lib.ae_launch_gemm_packed_fold.restype = ctypes.c_int
+    lib.ae_launch_gemm_packed_res_stats.argtypes = [vp] * 7 + [f32] + [vp] * 3 + [i32] * 4 + [vp]
+    lib.ae_launch_gemm_packed_res_stats.restype = ctypes.c_int
+    return lib
+
+
+def _split_prod(A, W, np_):
+    """float64 of the split products a_hi·w_hi (+ a_hi·w_lo + a_lo·w_hi)."""
+    Ah, Al = _split(A)
+    Wh, Wl = _split(W)
+    y = Ah.double() @ Wh.double().T
+    if np_ == 2:
+        y = y + Ah.double() @ Wl.double().T + Al.double() @ Wh.double().T
+    return y
+
+
+def _tile_stats(v):
+    """[M, 768] -> the [M][4] RowStat words of the kernels: (mean, M2) of each 192-column tile."""
+    t = v.double().reshape(v.shape[0], 4, 192)
+    mean = t.mean(2)
+    m2 = ((t - mean[:, :, None]) ** 2).sum(2)
+    rs = torch.stack([mean.float(), m2.float()], 2).contiguous()  # [M, 4, 2] f32
+    return rs.view(torch.int64).reshape(-1)
+
+
+def _ln64(v, gamma, beta, eps=1e-5):
+    v = v.double()
+    mu = v.mean(1, keepdim=True)
+    var = ((v - mu) ** 2).mean(1, keepdim=True)
+    return (v - mu) / torch.sqrt(var + eps) * gamma.double() + beta.double(), var
+
+
+@pytest.mark.parametrize("M,K,np_", [(300, 768, 2), (4097, 768, 2), (37, 3072, 2), (1000, 768, 1)])
+def test_gemm_packed_res_stats_matches_f64(gpu, M, K, np_):
+    """ae_launch_gemm_packed_res_stats (256 x 192 kernel): v = A·W^T + bias + r as f32 and packed
+    planes plus the (mean, M2) of every row over its 4 192-column tiles, first with a plain
+    residual (PK_EPI_RES_STATS: layer 0), then with the residual the previous pre-LayerNorm rows
+    normalised on the fly from the statistics the first launch wrote (PK_EPI_RES_STATS_LN).
+    Both in place (R = C), as the engine runs them; against float64 of the split products."""
+    lib = _fold_lib()
     N = 768
-    g = torch.Generator().manual_seed(M + K)
-    W = torch.randn(N, K, generator=g) * 0.05
-    bias = torch.randn(N, generator=g) * 0.5
+    g = torch.Generator().manual_seed(7 * M + K)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     gamma = 1.0 + 0.1 * torch.randn(N, generator=g)
     beta = 0.1 * torch.randn(N, generator=g)
-    Wh, Wl = _split(W)
-    dW = _pack(Wh, Wl, np_).cuda()
-    # device copies held by name: a temporary's memory is recycled before the launch reads it
-    db, dg, dbeta = bias.cuda(), gamma.cuda(), beta.cuda()
-    blocks = (M + 255) // 256
-    stats = torch.zeros(blocks * 256 * 4, dtype=torch.int64, device="cuda")
-    ctr = torch.zeros(2 * blocks, dtype=torch.int32, device="cuda")
-    err = torch.zeros(4, dtype=torch.int32, device="cuda")
-    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    for it in range(3):
+    dg, dbeta = gamma.cuda(), beta.cuda()
+    s1 = torch.zeros(M * 4, dtype=torch.int64, device="cuda")
+    s2 = torch.zeros(M * 4, dtype=torch.int64, device="cuda")
+    R0 = torch.randn(M, N, generator=g) * 2.0 + 0.5
+    v = R0.cuda()
+    prev = None
+    for it, (rst, out_st) in enumerate(((None, s1), (s1, s2))):
         A = torch.randn(M, K, generator=g) * 0.7
-        X = torch.randn(M, N, generator=g) * 2.0 + 0.5
-        Ah, Al = _split(A)
-        y = Ah.double() @ Wh.double().T
-        if np_ == 2:
-            y = y + Ah.double() @ Wl.double().T + Al.double() @ Wh.double().T
-        y = y + bias.double() + X.double()
-        mu = y.mean(1, keepdim=True)
-        var = ((y - mu) ** 2).mean(1, keepdim=True)
-        ref = (y - mu) / torch.sqrt(var + 1e-5) * gamma.double() + beta.double()
-        scale = (A.abs().double() @ W.abs().double().T).amax(1, keepdim=True)
-        dA = _pack(Ah, Al, np_).cuda()
-        x = X.cuda()
-        xp = torch.zeros((M, np_ * N), dtype=torch.bfloat16, device="cuda")
-        rc = lib.ae_launch_gemm_packed_ln(_p(dA), _p(dW), _p(db), _p(x), _p(x), _p(xp),
-                                          M, N, K, np_, _p(dg), _p(dbeta), 1e-5,
-                                          _p(stats), _p(ctr), _p(err), st)
+        W = torch.randn(N, K, generator=g) * 0.05
+        bias = torch.randn(N, generator=g) * 0.5
+        dA, dW, db = _pack(*_split(A), np_).cuda(), _pack(*_split(W), np_).cuda(), bias.cuda()
+        vp = torch.zeros((M, np_ * N), dtype=torch.bfloat16, device="cuda")
+        if rst is None:
+            r = R0.double()
+        else:
+            r, _ = _ln64(prev, gamma, beta)
+        rc = lib.ae_launch_gemm_packed_res_stats(
+            _p(dA), _p(dW), _p(db), _p(v), _p(rst), _p(dg if rst is not None else None),
+            _p(dbeta if rst is not None else None), 1e-5, _p(v), _p(vp), _p(out_st), M, N, K,
+            np_, st)
         assert rc == 0
         torch.cuda.synchronize()
-        assert int(err[0]) == 0 and int(ctr.abs().sum()) == 0, it
-        got = x.double().cpu()
-        # LN amplifies the GEMM's f32-accumulation error by rstd * gamma
-        tol = (1e-5 * scale + 1e-6) * 1.2 / torch.sqrt(var + 1e-5) + 2e-6
+        ref = _split_prod(A, W, np_) + bias.double() + r
+        scale = (A.abs().double() @ W.abs().double().T).amax(1, keepdim=True)
+        got = v.double().cpu()
+        # the on-the-fly LayerNorm reads f32 tile statistics: ~1e-6 relative on the residual
+        tol = 1e-5 * scale + 1e-6 + (2e-6 * (r.abs() + 1.0) if rst is not None else 0.0)
         assert torch.isfinite(got).all()
         assert ((got - ref).abs() <= tol).all(), (it, float(((got - ref).abs() - tol).max()))
-        planes = _unpack(xp.cpu(), np_, N)
+        planes = _unpack(vp.cpu(), np_, N)
         rel = 2e-5 if np_ == 2 else 5e-3
         assert ((planes - got).abs() <= rel * got.abs() + 1e-7).all(), it
+        # the tile statistics of the f32 output, against float64 of the same values
+        ws = out_st.cpu().view(torch.float32).reshape(M, 4, 2).double()
+        t = got.reshape(M, 4, 192)
+        mean = t.mean(2)
+        m2 = ((t - mean[:, :, None]) ** 2).sum(2)
+        assert ((ws[:, :, 0] - mean).abs() <= 1e-6 * (t.abs().amax(2) + 1)).all(), it
+        assert ((ws[:, :, 1] - m2).abs() <= 1e-5 * m2 + 1e-6).all(), it
+        prev = got
+
+
+@pytest.mark.parametrize("M,N,np_,gelu", [(300, 2304, 2, 0), (4100, 3072, 2, 1), (37, 3072, 2, 1),
+                                          (1000, 2304, 1, 0), (600, 3072, 1, 1)])
+def test_gemm_packed_fold_matches_f64(gpu, M, N, np_, gelu):
+    """ae_launch_gemm_packed_fold (256 x 256 kernel, PK_EPI_BIAS_FOLD / PK_EPI_GELU_FOLD): the
+    QKV / FFN1 GEMM over PRE-LayerNorm rows v with the LayerNorm folded in,
+        y = rstd · (v·W'^T - mean · s) + bias',  W' = W·diag(gamma), s = rowsums(W'),
+        bias' = bias + W·beta                                    (GELU'd for FFN1)
+    must equal LayerNorm(v)·W^T + bias in float64 — rows with a mean offset and varied scale, so
+    the mean · s cancellation is exercised.  Packed-plane output."""
+    lib = _fold_lib()
+    K = 768
+    g = torch.Generator().manual_seed(3 * M + N + gelu)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    v = torch.randn(M, K, generator=g) * (0.5 + 2.0 * torch.rand(M, 1, generator=g)) + \
+        3.0 * torch.randn(M, 1, generator=g)
+    gamma = 1.0 + 0.1 * torch.randn(K, generator=g)
+    beta = 0.1 * torch.randn(K, generator=g)
+    W = torch.randn(N, K, generator=g) * 0.05
+    bias = torch.randn(N, generator=g) * 0.5
+    Wf = W * gamma  # W·diag(gamma) in f32, as ae_create folds it
+    Wh, Wl = _split(Wf)
+    s = (Wh.double() + (Wl.double() if np_ == 2 else 0.0)).sum(1).float()
+    bf = (bias.double() + W.double() @ beta.double()).float()
+    dv = _pack(*_split(v), np_).cuda()
+    dW = _pack(Wh, Wl, np_).cuda()
+    ds, dbf = s.cuda(), bf.cuda()
+    dst = _tile_stats(v).cuda()
+    out = torch.zeros((M, np_ * N), dtype=torch.bfloat16, device="cuda")
+    rc = lib.ae_launch_gemm_packed_fold(_p(dv), _p(dW), _p(dbf), _p(ds), _p(dst), 1e-5, _p(out),
+                                        M, N, K, gelu, np_, st)
+    assert rc == 0
+    torch.cuda.synchronize()
+    x, var = _ln64(v, gamma, beta)
+    ref = x @ W.double().T + bias.double()
+    if gelu:
+        ref = 0.5 * ref * (1.0 + torch.erf(ref / np.sqrt(2.0)))
+    got = _unpack(out.cpu(), np_, N)
+    # the split products' error on v (not on LN(v)), times rstd: |v| includes the mean offset
+    scale = (v.abs().double() @ Wf.abs().double().T) / torch.sqrt(var + 1e-5)
+    rel = 1e-5 if np_ == 2 else 8e-3
+    tol = rel * scale + (2e-5 if np_ == 2 else 1e-2) * ref.abs() + 2e-6
+    assert torch.isfinite(got).all()
+    assert ((got - ref).abs() <= tol).all(), float(((got - ref).abs() - tol).max())

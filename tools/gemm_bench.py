@@ -9,8 +9,8 @@ per variant: median / min µs per launch and the algorithmic TFLOP/s (2·M·N·K
 A variant is "diag" (ae_bench_gemm_packed's DIAG: 0 = production kernel, other values time parts
 of the pipeline and give wrong results) optionally with "@bn" (kernel: 512 = the 256 x 256
 ping-pong kernel, 192 = the 256 x 192 one, 0 = the production choice) and ":np".
-The *_ln shapes time ae_bench_gemm_packed_ln (O-proj / FFN2 + residual + LayerNorm fused); their
-diag is its mode (0 production, 1 no cross-workgroup exchange, 2 grouped tile order).
+(The folded-LayerNorm epilogues of the engine are timed against their plain forms by
+tools/fold_bench.py.)
 """
 import argparse
 import ctypes
@@ -35,9 +35,6 @@ SHAPES = {  # name: (N, K, epilogue) with M = tokens (64 x 512 by default)
     "qkvp": (2304, 768, 4),
     "oproj_res": (768, 768, 2),
     "ffn2_res": (768, 3072, 2),
-    # fused residual + LayerNorm (ae_bench_gemm_packed_ln; the variant's diag is its mode)
-    "oproj_ln": (768, 768, 5),
-    "ffn2_ln": (768, 3072, 5),
 }
 
 
@@ -58,9 +55,6 @@ def main():
     fn = getattr(lib, args.entry)
     fn.argtypes = [vp] * 6 + [i32] * 7 + [vp]
     fn.restype = ctypes.c_int
-    fln = lib.ae_bench_gemm_packed_ln
-    fln.argtypes = [vp] * 6 + [i32] * 4 + [vp, vp, ctypes.c_float] + [vp] * 3 + [i32, vp]
-    fln.restype = ctypes.c_int
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream(dev)
     sp = ctypes.c_void_p(st.cuda_stream)
@@ -94,26 +88,13 @@ def main():
         C = torch.empty((M, N), device=dev)
         Cp = torch.empty((M, 2 * N), dtype=torch.bfloat16, device=dev)
         R = None
-        if epi in (2, 5):
+        if epi == 2:
             R = torch.randn((M, N), generator=g, device=dev)
-        if epi == 5:
-            gam, bet = torch.ones(N, device=dev), torch.zeros(N, device=dev)
-            blocks = (M + 255) // 256
-            stats = torch.zeros(blocks * 256 * 4, dtype=torch.int64, device=dev)
-            ctr = torch.zeros(2 * blocks, dtype=torch.int32, device=dev)
-            err = torch.zeros(4, dtype=torch.int32, device=dev)
         for (diag, bn, np_) in variants:
             A, W = bufs[np_]
-            if epi == 5:
-                # R is the output too (in place, as the engine runs it): x stays normalised
-                call = (lambda A=A, W=W, N=N, K=K, np_=np_, diag=diag, R=R, gam=gam, bet=bet,
-                        stats=stats, ctr=ctr, err=err, bias=bias, Cp=Cp:
-                        fln(p(A), p(W), p(bias), p(R), p(R), p(Cp), M, N, K, np_, p(gam), p(bet),
-                            1e-5, p(stats), p(ctr), p(err), diag, sp))
-            else:
-                call = (lambda A=A, W=W, bias=bias, C=C, Cp=Cp, N=N, K=K, epi=epi, np_=np_, bn=bn,
-                        diag=diag, R=R: fn(p(A), p(W), p(bias), p(R), p(C), p(Cp), M, N, K, epi,
-                                           np_, bn, diag, sp))
+            call = (lambda A=A, W=W, bias=bias, C=C, Cp=Cp, N=N, K=K, epi=epi, np_=np_, bn=bn,
+                    diag=diag, R=R: fn(p(A), p(W), p(bias), p(R), p(C), p(Cp), M, N, K, epi,
+                                       np_, bn, diag, sp))
             rc = call()
             if rc != 0:
                 print(json.dumps({"shape": name, "variant": [diag, bn, np_], "error": rc}))
