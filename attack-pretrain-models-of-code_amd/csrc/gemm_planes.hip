@@ -46,7 +46,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // PK_EPI_RES_STATS_LN: the same with the residual a pre-LayerNorm row, normalised on the fly
 // (see StatArgs; 256 x 192 kernel only).  (Round 4's PK_EPI_RES_LN = 5 — residual + LayerNorm
 // inside the O-projection / FFN2 epilogue, the 4 column tiles of a row block exchanging row
-// statistics as co-resident workgroups — was replaced by the folded form in round 6: DESIGN.md §3.)
+// statistics as co-resident workgroups — was replaced by the folded form in round 5: DESIGN.md §3.)
 enum { PK_EPI_BIAS = 0, PK_EPI_GELU_PACKED = 1, PK_EPI_RES = 2, PK_EPI_TANH = 3, PK_EPI_BIAS_PACKED = 4,
        PK_EPI_GELU_FOLD = 6, PK_EPI_BIAS_FOLD = 7, PK_EPI_RES_STATS = 8, PK_EPI_RES_STATS_LN = 9 };
 
