@@ -404,6 +404,9 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
   // folded LayerNorm: (mean, rstd) of this lane's 4 rows (rows past M read row M - 1; not
   // stored), all 16 statistics loads issued together — one memory latency per tile, not four
   float fneg[4] = {0.f, 0.f, 0.f, 0.f}, frs[4] = {1.f, 1.f, 1.f, 1.f};
+  // and the tile's 256 columns of bias' and s staged once in LDS past the staging regions (the
+  // launch adds 2 KiB): read per column quad at LDS latency, not re-loaded from L1 / L2 per pass
+  float* const colt = reinterpret_cast<float*>(pk_smem + 8 * 16384);
   if constexpr (FOLD) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -411,22 +414,19 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
       row_norm(fold.stats + (size_t)min(m0 + wm * 128 + r * 32 + li, M - 1) * 4, fold.eps, mu, frs[r]);
       fneg[r] = -mu;
     }
+    if (tid < 128) {
+      const int v = tid >> 6, q = tid & 63;
+      const int c = min(n0 + 4 * q, N - 4);
+      *reinterpret_cast<floatx4*>(colt + v * 256 + 4 * q) =
+          *reinterpret_cast<const floatx4*>((v ? fold.s : bias) + c);
+    }
+    __syncthreads();
   }
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt) {
       const int lr = tt * 32 + li;  // row within the half
-      const float* fbias = bias;
-      const float* fs = fold.s;
-      if constexpr (FOLD) {
-        // opaque per row pass: the bias / s columns are re-read (L1 hits) instead of held live
-        // across the four passes
-        int z = 0;
-        asm volatile("" : "+s"(z));
-        fbias += z;
-        fs += z;
-      }
 #pragma unroll
       for (int tn = 0; tn < 2; ++tn) {
         if constexpr (PACKED) {
@@ -442,9 +442,10 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
           for (int j = 0; j < 4; ++j) {
             const int cc = tn * 32 + 8 * j + 4 * lh;  // column within the wave's 64
             const int col = cb0 + cc < N ? cb0 + cc : N - 4;
-            const floatx4 bv = *reinterpret_cast<const floatx4*>(fbias + col);
+            const floatx4 bv = FOLD ? *reinterpret_cast<const floatx4*>(colt + (col - n0))
+                                    : *reinterpret_cast<const floatx4*>(bias + col);
             if constexpr (FOLD) {  // rstd * (acc - mean * s) + bias'
-              const floatx4 sv = *reinterpret_cast<const floatx4*>(fs + col);
+              const floatx4 sv = *reinterpret_cast<const floatx4*>(colt + 256 + (col - n0));
 #pragma unroll
               for (int i = 0; i < 4; i += 2)
                 y[2 * j + i / 2] = __builtin_elementwise_fma(
@@ -746,6 +747,18 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
       for (int tm = 0; tm < 2; ++tm)
         row_norm(ln.rstats + (size_t)min(rb0 + 32 * tm, M - 1) * 4, ln.eps, rmu[tm], rrs[tm]);
     }
+    // the tile's 192 columns of bias (and gamma, beta) staged once in LDS (past the wave regions
+    // and the statistics exchange): read per column quad at LDS latency instead of an L1 / L2
+    // round trip per quad (measured: the global form cost the O-projection 15 us per launch)
+    constexpr int NV = rnorm ? 3 : 1;
+    float* const colt = reinterpret_cast<float*>(pk_smem + 8 * 32 * RS + 4096);
+    if (tid < NV * 48) {
+      const int v = tid / 48, q = tid % 48;
+      const float* src = v == 0 ? bias : v == 1 ? ln.gamma : ln.beta;
+      *reinterpret_cast<floatx4*>(colt + v * 192 + 4 * q) =
+          *reinterpret_cast<const floatx4*>(src + n0 + 4 * q);
+    }
+    __syncthreads();
 #pragma unroll
     for (int tm = 0; tm < 2; ++tm) {
 #pragma unroll
@@ -756,23 +769,17 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
                                   : floatx4{0.f, 0.f, 0.f, 0.f};
         *reinterpret_cast<floatx4*>(reg + lr * RS + c * 16) = f;
       }
-      // opaque per pass: the column vectors are re-read (L1 hits), not held live across passes
-      int z = 0;
-      asm volatile("" : "+s"(z));
-      const float* pb = bias + z;
-      const float* pg = ln.gamma + z;
-      const float* pt = ln.beta + z;
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 #pragma unroll
       for (int tn = 0; tn < 3; ++tn)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int col = cb0 + tn * 32 + 8 * j + 4 * lh;
-          const floatx4 bv = *reinterpret_cast<const floatx4*>(pb + col);
+          const int tc = sn * 96 + tn * 32 + 8 * j + 4 * lh;  // column within the tile
+          const floatx4 bv = *reinterpret_cast<const floatx4*>(colt + tc);
           floatx4 rv = *reinterpret_cast<const floatx4*>(reg + li * RS + (tn * 8 + 2 * j + lh) * 16);
           if constexpr (rnorm) {
-            const floatx4 gg = *reinterpret_cast<const floatx4*>(pg + col);
-            const floatx4 bb = *reinterpret_cast<const floatx4*>(pt + col);
+            const floatx4 gg = *reinterpret_cast<const floatx4*>(colt + 192 + tc);
+            const floatx4 bb = *reinterpret_cast<const floatx4*>(colt + 384 + tc);
 #pragma unroll
             for (int i = 0; i < 4; ++i) rv[i] = (rv[i] - rmu[tm]) * rrs[tm] * gg[i] + bb[i];
           }
@@ -987,7 +994,9 @@ template <int NP, int EPI, int DIAG>
 hipError_t pp_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R, float* C,
                      __bf16* Cp, int M, int N, int K, int group_m, hipStream_t st,
                      FoldArgs fold = FoldArgs{}) {
-  constexpr int lds = 2 * (256 + 256) * PK_ROWB;  // 128 KiB
+  // 128 KiB (+ 2 KiB of bias' / s columns for the folded epilogues)
+  constexpr int lds = 2 * (256 + 256) * PK_ROWB +
+                      (EPI == PK_EPI_GELU_FOLD || EPI == PK_EPI_BIAS_FOLD ? 2048 : 0);
   if (hipError_t e = ensure_dynamic_lds((const void*)gemm_pp_kernel<NP, EPI, DIAG>, lds); e != hipSuccess)
     return e;
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
