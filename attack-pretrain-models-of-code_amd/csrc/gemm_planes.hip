@@ -193,6 +193,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
 
   const int tiles_n = (N + BN - 1) / BN;
   const int tiles_m = (M + BM - 1) / BM;
+  constexpr bool FOLD_EPI = EPI == PK_EPI_GELU_FOLD || EPI == PK_EPI_BIAS_FOLD;
   // persistent when the grid is smaller than the tile count (pp_launch): workgroup w takes the
   // virtual blocks w, w + grid, ... — the same tiles, XCD and order as one block per tile — so a
   // CU goes from one tile's epilogue straight into the next tile's prologue, with no workgroup
@@ -324,6 +325,25 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
     __builtin_amdgcn_sched_barrier(0);
   };
 
+  // folded LayerNorm: the epilogue's side data — bias' and s of the tile's 256 columns (2 KiB)
+  // and the 4 tile statistics of its 256 rows (8 KiB) — moved into LDS past the stages by
+  // LDS-DMA ahead of the prologue (waves 0-4, two 1-KiB pieces each).  They are older than every
+  // K-tile piece, so the counted waits below cover them; the epilogue reads them at LDS latency.
+  constexpr uint32_t SIDE = 2 * STAGE;  // byte offset of [bias' 256 | s 256] then [256 rows][4] u64
+  if constexpr (FOLD_EPI) {
+    if (wave == 0) {
+      const int c = min(n0 + 4 * lane, N - 4);
+      dma16(bias + c, lds0 + SIDE);
+      dma16(fold.s + c, lds0 + SIDE + 1024);
+    } else if (wave <= 4) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int r0 = (wave - 1) * 64 + h * 32;  // first tile row of the piece; 2 lanes per row
+        dma16(fold.stats + (size_t)min(m0 + r0 + (lane >> 1), M - 1) * 4 + 2 * (lane & 1),
+              lds0 + SIDE + 2048 + (uint32_t)(r0 * 32));
+      }
+    }
+  }
   // prologue: K-tile 0 whole and K-tile 1's first two quarters (the loop issues the rest)
   if (nk > 0) {
 #pragma unroll
@@ -403,24 +423,18 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
   const int cb0 = n0 + wn * 64;
   // folded LayerNorm: (mean, rstd) of this lane's 4 rows (rows past M read row M - 1; not
   // stored), all 16 statistics loads issued together — one memory latency per tile, not four
+  // (from the side data the prologue moved into LDS: bias' / s of the tile's columns, the tile
+  // rows' statistics; rows past M carry row M - 1's, never stored)
   float fneg[4] = {0.f, 0.f, 0.f, 0.f}, frs[4] = {1.f, 1.f, 1.f, 1.f};
-  // and the tile's 256 columns of bias' and s staged once in LDS past the staging regions (the
-  // launch adds 2 KiB): read per column quad at LDS latency, not re-loaded from L1 / L2 per pass
-  float* const colt = reinterpret_cast<float*>(pk_smem + 8 * 16384);
+  const float* const colt = reinterpret_cast<const float*>(pk_smem + SIDE);
   if constexpr (FOLD) {
+    const uint64_t* lst = reinterpret_cast<const uint64_t*>(pk_smem + SIDE + 2048);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float mu;
-      row_norm(fold.stats + (size_t)min(m0 + wm * 128 + r * 32 + li, M - 1) * 4, fold.eps, mu, frs[r]);
+      row_norm(lst + (wm * 128 + r * 32 + li) * 4, fold.eps, mu, frs[r]);
       fneg[r] = -mu;
     }
-    if (tid < 128) {
-      const int v = tid >> 6, q = tid & 63;
-      const int c = min(n0 + 4 * q, N - 4);
-      *reinterpret_cast<floatx4*>(colt + v * 256 + 4 * q) =
-          *reinterpret_cast<const floatx4*>((v ? fold.s : bias) + c);
-    }
-    __syncthreads();
   }
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
@@ -678,6 +692,29 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
     __builtin_amdgcn_sched_barrier(0);
   };
 
+  // PK_EPI_RES_STATS(_LN): the epilogue's side data — bias (gamma, beta) of the tile's 192
+  // columns (1 KiB each) and, for _LN, the residual rows' tile statistics (8 KiB) — moved into LDS
+  // past the stages by LDS-DMA ahead of the prologue (older than every K-tile piece, so the
+  // counted waits below cover them)
+  constexpr bool STATS_EPI = EPI == PK_EPI_RES_STATS || EPI == PK_EPI_RES_STATS_LN;
+  constexpr uint32_t SIDE = 2 * STAGE;  // [bias | gamma | beta] (1 KiB each), [256 rows][4] u64
+  if constexpr (STATS_EPI) {
+    if (wave == 0) {
+      const int c = n0 + 4 * min(lane, 47);
+      dma16(bias + c, lds0 + SIDE);
+      if constexpr (EPI == PK_EPI_RES_STATS_LN) {
+        dma16(ln.gamma + c, lds0 + SIDE + 1024);
+        dma16(ln.beta + c, lds0 + SIDE + 2048);
+      }
+    } else if (EPI == PK_EPI_RES_STATS_LN && wave <= 4) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int r0 = (wave - 1) * 64 + h * 32;  // first tile row of the piece; 2 lanes per row
+        dma16(ln.rstats + (size_t)min(m0 + r0 + (lane >> 1), M - 1) * 4 + 2 * (lane & 1),
+              lds0 + SIDE + 3072 + (uint32_t)(r0 * 32));
+      }
+    }
+  }
   // prologue: K-tile 0 whole, K-tile 1's A + W(tn 0) (its W(tn 1), W(tn 2): phases 0, 1 of kt 0)
   if (nk > 0) {
 #pragma unroll
@@ -740,25 +777,16 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
     unsigned char* reg = pk_smem + wave * 32 * RS;
     const int prow0 = m0 + wm * 128 + sm * 64;
     constexpr bool rnorm = EPI == PK_EPI_RES_STATS_LN;
-    // the residual rows' (mean, rstd) for both passes, their 8 statistics loads issued together
+    // the residual rows' (mean, rstd) for both passes and the tile's bias (gamma, beta) columns,
+    // all from the side data the prologue moved into LDS (rows past M carry row M - 1's)
+    const float* const colt = reinterpret_cast<const float*>(pk_smem + SIDE);
     float rmu[2] = {0.f, 0.f}, rrs[2] = {1.f, 1.f};
     if constexpr (rnorm) {
+      const uint64_t* rst = reinterpret_cast<const uint64_t*>(pk_smem + SIDE + 3072);
 #pragma unroll
       for (int tm = 0; tm < 2; ++tm)
-        row_norm(ln.rstats + (size_t)min(rb0 + 32 * tm, M - 1) * 4, ln.eps, rmu[tm], rrs[tm]);
+        row_norm(rst + (rb0 - m0 + 32 * tm) * 4, ln.eps, rmu[tm], rrs[tm]);
     }
-    // the tile's 192 columns of bias (and gamma, beta) staged once in LDS (past the wave regions
-    // and the statistics exchange): read per column quad at LDS latency instead of an L1 / L2
-    // round trip per quad (measured: the global form cost the O-projection 15 us per launch)
-    constexpr int NV = rnorm ? 3 : 1;
-    float* const colt = reinterpret_cast<float*>(pk_smem + 8 * 32 * RS + 4096);
-    if (tid < NV * 48) {
-      const int v = tid / 48, q = tid % 48;
-      const float* src = v == 0 ? bias : v == 1 ? ln.gamma : ln.beta;
-      *reinterpret_cast<floatx4*>(colt + v * 192 + 4 * q) =
-          *reinterpret_cast<const floatx4*>(src + n0 + 4 * q);
-    }
-    __syncthreads();
 #pragma unroll
     for (int tm = 0; tm < 2; ++tm) {
 #pragma unroll
@@ -778,8 +806,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
           const floatx4 bv = *reinterpret_cast<const floatx4*>(colt + tc);
           floatx4 rv = *reinterpret_cast<const floatx4*>(reg + li * RS + (tn * 8 + 2 * j + lh) * 16);
           if constexpr (rnorm) {
-            const floatx4 gg = *reinterpret_cast<const floatx4*>(colt + 192 + tc);
-            const floatx4 bb = *reinterpret_cast<const floatx4*>(colt + 384 + tc);
+            const floatx4 gg = *reinterpret_cast<const floatx4*>(colt + 256 + tc);
+            const floatx4 bb = *reinterpret_cast<const floatx4*>(colt + 512 + tc);
 #pragma unroll
             for (int i = 0; i < 4; ++i) rv[i] = (rv[i] - rmu[tm]) * rrs[tm] * gg[i] + bb[i];
           }
@@ -994,9 +1022,9 @@ template <int NP, int EPI, int DIAG>
 hipError_t pp_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R, float* C,
                      __bf16* Cp, int M, int N, int K, int group_m, hipStream_t st,
                      FoldArgs fold = FoldArgs{}) {
-  // 128 KiB (+ 2 KiB of bias' / s columns for the folded epilogues)
+  // 128 KiB (+ 10 KiB of side data for the folded epilogues: bias' / s columns, row statistics)
   constexpr int lds = 2 * (256 + 256) * PK_ROWB +
-                      (EPI == PK_EPI_GELU_FOLD || EPI == PK_EPI_BIAS_FOLD ? 2048 : 0);
+                      (EPI == PK_EPI_GELU_FOLD || EPI == PK_EPI_BIAS_FOLD ? 10240 : 0);
   if (hipError_t e = ensure_dynamic_lds((const void*)gemm_pp_kernel<NP, EPI, DIAG>, lds); e != hipSuccess)
     return e;
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
@@ -1034,7 +1062,9 @@ template <int NP, int EPI, bool NT = false>
 hipError_t pp192_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R,
                         float* C, int M, int N, int K, int group_m, hipStream_t st,
                         StatArgs ln = StatArgs{}) {
-  constexpr int lds = 2 * (256 + 192) * PK_ROWB;  // 112 KiB
+  // 112 KiB (+ 11 KiB of side data for the residual + statistics epilogues)
+  constexpr int lds = 2 * (256 + 192) * PK_ROWB +
+                      (EPI == PK_EPI_RES_STATS || EPI == PK_EPI_RES_STATS_LN ? 11264 : 0);
   if (hipError_t e = ensure_dynamic_lds((const void*)gemm_pp192_kernel<NP, EPI, NT>, lds); e != hipSuccess)
     return e;
   const int tiles_m = (M + 255) / 256;

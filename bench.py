@@ -958,8 +958,8 @@ def main():
         "roofline": {
             "bound": "mfma",
             "kernel": {"fp32": "gemm_f32_nt_kernel<EPI_BIAS_GELU>",
-                       "f32x3": "gemm_pp_kernel<2, EPI_GELU_PACKED>",
-                       "bf16": "gemm_pp_kernel<1, EPI_GELU_PACKED>"}[args.precision]
+                       "f32x3": "gemm_pp_kernel<2, PK_EPI_GELU_FOLD>",
+                       "bf16": "gemm_pp_kernel<1, PK_EPI_GELU_FOLD>"}[args.precision]
                       + " (FFN1 [T,768]x[768,3072])",
             "achieved": round(achieved, 3) if achieved else None,
             "peak": peak,

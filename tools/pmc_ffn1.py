@@ -10,7 +10,7 @@ import statistics
 import sys
 
 root, precision = sys.argv[1], sys.argv[2]
-pat = sys.argv[3] if len(sys.argv) > 3 else "gemm_pp_kernel<2, 1"
+pat = sys.argv[3] if len(sys.argv) > 3 else "gemm_pp_kernel<2, 6"  # PK_EPI_GELU_FOLD
 grid = int(sys.argv[4]) if len(sys.argv) > 4 else 1536 * 512
 M, N, K = 64 * 512, 3072, 768
 np_ = 2 if precision == "f32x3" else 1

@@ -17,7 +17,8 @@ import sys
 SIMDS = 1024  # 256 CUs x 4
 
 root = pathlib.Path(sys.argv[1])
-pats = sys.argv[2:] or ["gemm_pp_kernel<2, 1", "gemm_pp_kernel<2, 4", "gemm_pp192_kernel<2, 5",
+# FFN1 / QKV (folded LayerNorm), O-projection / FFN2 (+ residual + statistics), attention
+pats = sys.argv[2:] or ["gemm_pp_kernel<2, 6", "gemm_pp_kernel<2, 7", "gemm_pp192_kernel<2, 9",
                         "attn_pp_kernel<2, false, true"]
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 dur = collections.defaultdict(list)

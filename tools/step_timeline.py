@@ -13,7 +13,11 @@ import sys
 def cls(name):
     for key, label in (("gemm_pp192_kernel<2, 2", "gemm192 +res (O-proj/FFN2)"),
                        ("gemm_pp192_kernel<2, 5", "gemm192 +res+LN"),
+                       ("gemm_pp192_kernel<2, 8", "gemm192 +res+stats (layer 0)"),
+                       ("gemm_pp192_kernel<2, 9", "gemm192 +LN(res)+stats (O-proj/FFN2)"),
                        ("gemm_pp_kernel<2, 1", "gemm256 GELU (FFN1)"),
+                       ("gemm_pp_kernel<2, 6", "gemm256 fold GELU (FFN1)"),
+                       ("gemm_pp_kernel<2, 7", "gemm256 fold packed (QKV)"),
                        ("gemm_pp_kernel<2, 4", "gemm256 packed (QKV)"),
                        ("gemm_pp192_kernel<2, 4", "gemm192 packed (QKV)"),
                        ("attn_pp_kernel", "attention"), ("layernorm_kernel", "layernorm"),
