@@ -127,6 +127,7 @@ class Model:
         self.tokenizer = tokenizer
         self.args = args
         self.query = 0
+        self.tokens = 0  # non-pad tokens of every scored row (diagnostics: tokens / s on device)
         self.block_size = getattr(args, "block_size", None)
         # the Authorship-Attribution victim tokenizes raw source (no ' '.join(code.split()))
         self.raw = task == "authorship"
@@ -229,6 +230,7 @@ class Model:
 
         nq = [p.n for p in payloads]
         self.query += sum(nq)
+        self.tokens += int(sum(int(p.lens.sum()) for p in payloads if p.n))
         live = [p for p in payloads if p.n]
         if not live:
             return ScoresReady([([], []) for _ in payloads])

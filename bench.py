@@ -427,6 +427,7 @@ def attack_leg(dev, n_examples, deadline_s, inflight, rank, world, precision):
     _, t = run_sharded_gi_batched(model, codes, subs, labels, args, max_inflight=inflight,
                                   device=dev, deadline=time.time() + deadline_s,
                                   key="bench_attack_queue")
+    tokens = model.tokens
     model.engine.close()
     wall = t["wall_s"]
     return {"workload": "CodeBERT Devign greedy->GA attack (gi_attack --use_ga), "
@@ -441,6 +442,11 @@ def attack_leg(dev, n_examples, deadline_s, inflight, rank, world, precision):
             "victim_queries": t["queries"], "wall_s": round(wall, 2),
             "victim_queries_per_s": round(t["queries"] / wall, 2),
             "attacked_examples_per_min": round(60 * t["examples"] / wall, 3),
+            # scored non-pad tokens (this rank's victim): the device-side work rate, comparable
+            # with the microbench varlen leg's tokens / s
+            "tokens_scored": tokens,
+            "tokens_per_s": round(tokens / wall, 1) if tokens else None,
+            "mean_tokens_per_query": round(tokens / t["queries"], 1) if t["queries"] else None,
             "per_rank": t["per_rank"],
             "rng": "random.Random(123456 + index) per example",
             "batching": f"cross-example: up to {inflight} examples' requests per device batch",
