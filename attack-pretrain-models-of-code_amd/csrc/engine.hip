@@ -152,11 +152,11 @@ struct ae_engine {
   int* pinned_cu = nullptr;
   size_t cap_pinned = 0;
   hipEvent_t pinned_ready = nullptr;
-  // two-stream encoder (split-precision modes; AE_SPLIT_STREAMS=0 at engine creation turns it
-  // off): the batch's sequences in two halves, each half's layers on its own stream, the second
-  // half one kernel behind, so one half's memory-bound phases (GEMM epilogues, LayerNorm) and
-  // tile-quantisation tails can run beside the other half's MFMA-bound main loops; LayerNorm as
-  // its own kernel (no cross-workgroup exchange, whose partners must be co-resident)
+  // two-stream encoder (split-precision modes unless cfg.streams = AE_STREAMS_ONE; the tools
+  // library's AE_SPLIT_STREAMS=0 too): the batch's sequences in two halves, each half's layers on
+  // its own stream, the second half one kernel behind, so one half's memory-bound phases (GEMM
+  // epilogue bursts) and tile-quantisation tails can run beside the other half's MFMA-bound main
+  // loops; every row's arithmetic is the one-stream form's (layer_rows)
   static constexpr int kMaxParts = 4;
   bool split = false;
   int split_parts = 2;  // parts of the batch, each on its own stream (AE_SPLIT_PARTS, 2..4)

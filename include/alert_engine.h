@@ -77,8 +77,8 @@ extern "C" {
 /* Encoder schedule of the split-precision modes (ignored by AE_PREC_FP32). */
 #define AE_STREAMS_TWO 0 /* default: the batch as two halves on two HIP streams, one kernel apart
                             (one half's memory-bound phases beside the other's MFMA loops)   */
-#define AE_STREAMS_ONE 1 /* every kernel on the caller's stream (the fused residual +
-                            LayerNorm GEMM epilogue; what the bench's roofline pass times)    */
+#define AE_STREAMS_ONE 1 /* every kernel on the caller's stream (bit-identical scores; what
+                            the bench's roofline pass times)                                  */
 
 typedef struct ae_config {
   int32_t layers;      /* 12 */
