@@ -37,9 +37,6 @@ hipError_t ae_bench_attention_pp(const unsigned short*, float*, unsigned short*,
 hipError_t ae_launch_gemm_packed(const unsigned short*, const unsigned short*, const float*,
                                  const float*, float*, unsigned short*, int, int, int, int, int,
                                  hipStream_t);
-hipError_t ae_launch_gemm_packed_qkv192(const unsigned short*, const unsigned short*, const float*,
-                                        const float*, float*, unsigned short*, int, int, int, int,
-                                        int, hipStream_t);
 hipError_t ae_launch_gemm_packed_fold(const unsigned short*, const unsigned short*, const float*,
                                       const float*, const uint64_t*, float, unsigned short*, int,
                                       int, int, int, int, hipStream_t);
@@ -137,9 +134,6 @@ struct ae_engine {
   // u = W_k^T q and p-weighted row sums [n][12][768], per-64-key-chunk partial records
   // (AE_CLS_ABSORB=0 at engine creation: the full-T QKV GEMM + one-query attention instead)
   bool cls_absorb = true;
-  // the QKV GEMM may run on 256 x 192 tiles (its packed-plane epilogue) where that finishes in
-  // fewer tile rounds (AE_QKV192=1 at engine creation)
-  bool qkv192 = false;
   float *cls_u = nullptr, *cls_y = nullptr, *cls_part = nullptr;
   size_t cap_cls_part = 0;
   int *tok_ids = nullptr, *tok_pos = nullptr, *src_col = nullptr, *cu = nullptr, *one = nullptr;
@@ -424,10 +418,7 @@ int gemm_pk(ae_engine* e, const unsigned short* A, const unsigned short* Wp, con
             hipStream_t st, bool is_ffn1) {
   const bool prof = (e->prof_kind == AE_KIND_GEMM_ANY) || (e->prof_kind == AE_KIND_GEMM_FFN1 && is_ffn1);
   Prof p(e, st, prof, 2.0 * M * N * K);
-  if (e->qkv192 && Cp && !is_ffn1)  // the QKV GEMM (packed output, not FFN1)
-    HIPC(ae_launch_gemm_packed_qkv192(A, Wp, bias, R, C, Cp, M, N, K, epi, e->np, st));
-  else
-    HIPC(ae_launch_gemm_packed(A, Wp, bias, R, C, Cp, M, N, K, epi, e->np, st));
+  HIPC(ae_launch_gemm_packed(A, Wp, bias, R, C, Cp, M, N, K, epi, e->np, st));
   return AE_OK;
 }
 
@@ -829,8 +820,6 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
   {
     const char* ca = std::getenv("AE_CLS_ABSORB");  // A/B runs: 0 = full-T QKV + attention
     e->cls_absorb = !(ca && ca[0] == '0');
-    const char* q192 = std::getenv("AE_QKV192");  // A/B runs: 1 = 256 x 192 QKV tiles allowed
-    e->qkv192 = q192 && q192[0] == '1';
   }
 #endif
   if (e->planes) {

@@ -1169,19 +1169,6 @@ extern "C" hipError_t ae_launch_gemm_packed(const unsigned short* A, const unsig
              : pp_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
 }
 
-// ae_launch_gemm_packed with the 256 x 192 kernel also eligible for the packed-plane epilogue
-// (N % 192 == 0; the same rounds rule picks the width).  The engine's QKV launches under
-// AE_QKV192=1.  Not part of include/alert_engine.h.
-extern "C" hipError_t ae_launch_gemm_packed_qkv192(const unsigned short* A, const unsigned short* W,
-                                                   const float* bias, const float* R, float* C,
-                                                   unsigned short* Cp, int M, int N, int K, int epi,
-                                                   int np, hipStream_t st) {
-  if (M <= 0) return hipSuccess;
-  if (!pk_shape_ok(M, N, K, np)) return hipErrorInvalidValue;
-  return pp_choose(M, N, epi, true) == 192
-             ? pp192_dispatch(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st)
-             : pp_dispatch<0>(A, W, bias, R, C, Cp, M, N, K, epi, np, PK_GROUP_M, st);
-}
 
 
 // The folded-LayerNorm pair (FoldArgs).  Cp = packed planes of

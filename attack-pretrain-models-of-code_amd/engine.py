@@ -124,7 +124,7 @@ class Engine:
         or "one" (every kernel on the caller's stream).  tools=True builds the engine from the
         tools library (lib/libalert_engine_tools.so, the same sources with -DAE_TOOLS), whose
         engine also reads the A/B knobs AE_ATTN_VARIANT, AE_SPLIT_STREAMS / _PARTS / _LAG,
-        AE_QKV192, AE_CLS_ABSORB at creation (tools/engine_ab.py, alternative-form
+        AE_CLS_ABSORB at creation (tools/engine_ab.py, alternative-form
         parity tests); the product library reads no environment."""
         import torch
 

@@ -352,28 +352,6 @@ def test_encoder_forms_bit_identical(gpu, precision):
         e.close()
 
 
-@pytest.mark.parametrize("split", ["1", "0"])
-def test_qkv192_tiles_bit_identical(gpu, monkeypatch, split):
-    """The QKV GEMM on 256 x 192 tiles (AE_QKV192=1: the 256 x 192 kernel's packed-plane
-    epilogue, chosen where it takes fewer tile rounds) sums every output in the same order as
-    the 256 x 256 kernel: the scores are bit-identical, on full and ragged batches and both
-    encoder forms."""
-    from apmc_amd.engine import Engine
-    sd = synthetic_sd(7, "sigmoid1", 1)
-    engines = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("AE_QKV192", mode)  # a knob of the tools library's engine
-        engines[mode] = Engine(sd, head="sigmoid1", num_labels=1, precision="f32x3",
-                               streams="two" if split == "1" else "one", tools=mode == "1")
-    rng = np.random.default_rng(51)
-    for n, L in ((64, 512), (33, 300), (2, 77)):
-        lens = np.full(n, L) if n == 64 else rng.integers(3, L + 1, n)
-        ids = _rand_ids(rng, n, L, lens)
-        assert np.array_equal(_score(engines["1"], ids), _score(engines["0"], ids))
-    for e in engines.values():
-        e.close()
-
-
 def test_bench_size_batch_properties(gpu):
     """At the bench's full sizes (config-2 rows of L = 512; the batch-1024 microbenchmark), the
     properties that do not need the oracle to run the whole batch: one 1024-row call equals

@@ -73,7 +73,7 @@ def _p(t):
     (64, 768, 3072, 2, 2, "192"),
     (257, 192, 192, 1, 0, "192"),
     (700, 576, 256, 2, 2, "192"),
-    # its packed-plane epilogue (the QKV GEMM, AE_QKV192): N % 192 == 0, ragged M
+    # its packed-plane epilogue (N % 192 == 0, ragged M; a tools-library variant of the QKV GEMM)
     (300, 2304, 768, 2, 4, "192"),
     (1000, 576, 256, 1, 4, "192"),
     (4100, 2304, 128, 2, 4, "192"),

@@ -15,7 +15,7 @@ import time
 
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
-KNOBS = ("AE_ATTN_VARIANT", "AE_SPLIT_STREAMS", "AE_SPLIT_PARTS", "AE_SPLIT_LAG", "AE_QKV192",
+KNOBS = ("AE_ATTN_VARIANT", "AE_SPLIT_STREAMS", "AE_SPLIT_PARTS", "AE_SPLIT_LAG",
          "AE_CLS_ABSORB")
 
 
