@@ -830,8 +830,10 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
 #ifdef AE_TOOLS
     const char* sp = std::getenv("AE_SPLIT_STREAMS");
     if (sp && sp[0] == '0') e->split = false;
-    const char* lag = std::getenv("AE_SPLIT_LAG");  // experiments: 1 (QKV) .. 7 (whole layer 0)
-    if (lag && lag[0] >= '1' && lag[0] <= '7') e->split_lag = lag[0] - '0';
+    // experiments: 1 (after QKV) .. 5 (after the whole layer 0: QKV, attention, O-projection,
+    // FFN1, FFN2 — layer_rows' five kernels)
+    const char* lag = std::getenv("AE_SPLIT_LAG");
+    if (lag && lag[0] >= '1' && lag[0] <= '5') e->split_lag = lag[0] - '0';
     const char* av = std::getenv("AE_ATTN_VARIANT");  // A/B runs: 6, 66, 72 (67 = production)
     if (av) {
       const int v = std::atoi(av);
