@@ -352,6 +352,52 @@ def test_encoder_forms_bit_identical(gpu, precision):
         e.close()
 
 
+def test_folded_layernorm_robust_to_row_mean_offsets(gpu):
+    """The split modes fold each LayerNorm into the next GEMM: it multiplies the PRE-LayerNorm
+    rows and subtracts mean · s in the epilogue, so a residual stream whose rows carry a large
+    common offset (|mean| >> std) is where that cancellation could lose precision.  Synthetic
+    weights whose residual rows are shifted — every LayerNorm bias +4, the O-projection / FFN2
+    biases +3: a row mean of about 7 against a std of 1-2 at every folded GEMM — with LayerNorm
+    gains drawn from 0.5..2 (so s = rowsum(W·diag(g)) is far from 0) and every encoder / head
+    weight row centred (W·1 = 0, so the offsets stay in the residual stream instead of swamping
+    the tokens' signal).  The last layer's hidden states of f32x3 against the exact-fp32 mode
+    (which normalises explicitly): the relative error with the offsets stays within 3x of the same
+    weights' error without them, and the probabilities within the 1e-4 north-star tolerance."""
+    from apmc_amd.engine import Engine
+    rng = np.random.default_rng(9)
+    base = {k: v.copy() for k, v in synthetic_sd(9, "sigmoid1", out_std=0.05).items()}
+    for k in base:
+        if k.endswith("LayerNorm.weight"):
+            base[k] = rng.uniform(0.5, 2.0, base[k].shape).astype(np.float32)
+        elif (k.startswith("encoder.") or k.startswith("classifier.")) and base[k].ndim == 2:
+            base[k] -= base[k].mean(1, keepdims=True)
+    shifted = {k: v.copy() for k, v in base.items()}
+    for k in shifted:
+        if k.endswith("LayerNorm.bias") and not k.startswith("lm_head"):
+            shifted[k] += 4.0
+        elif k.startswith("encoder.") and k.endswith("output.dense.bias"):  # O-proj and FFN2
+            shifted[k] += 3.0
+    n, L = 24, 512
+    ids = _rand_ids(rng, n, L, rng.integers(40, L + 1, n))
+    lens = (ids != 1).sum(1).astype(np.int32)
+    dev_ids = torch.from_numpy(ids).cuda()
+    rel = {}
+    for name, sd in (("base", base), ("shifted", shifted)):
+        e32 = Engine(sd, head="sigmoid1", precision="fp32")
+        e3 = Engine(sd, head="sigmoid1", precision="f32x3")
+        h32, h3 = e32.encode(dev_ids, lens), e3.encode(dev_ids, lens)
+        torch.cuda.synchronize()
+        mask = torch.from_numpy(ids != 1).cuda()[..., None]
+        rel[name] = float(((h3 - h32).abs() * mask).max() / (h32.abs() * mask).max())
+        if name == "shifted":
+            p32, p3 = _score(e32, ids), _score(e3, ids)
+            np.testing.assert_allclose(p3, p32, atol=PROB_TOL, rtol=0)
+        e32.close()
+        e3.close()
+    print(f"hidden-state relative error: base {rel['base']:.2e}, shifted {rel['shifted']:.2e}")
+    assert rel["shifted"] <= 3 * rel["base"] + 1e-7, rel
+
+
 def test_bench_size_batch_properties(gpu):
     """At the bench's full sizes (config-2 rows of L = 512; the batch-1024 microbenchmark), the
     properties that do not need the oracle to run the whole batch: one 1024-row call equals
