@@ -439,10 +439,21 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt) {
-      const int lr = tt * 32 + li;  // row within the half
+    for (int tn = 0; tn < 2; ++tn) {
+      // folded form: this column block's bias' / s quads read from LDS once for both row passes
+      floatx4 fbv[4], fsv[4];
+      if constexpr (FOLD) {
 #pragma unroll
-      for (int tn = 0; tn < 2; ++tn) {
+        for (int j = 0; j < 4; ++j) {
+          const int cc = tn * 32 + 8 * j + 4 * lh;
+          const int col = cb0 + cc < N ? cb0 + cc : N - 4;
+          fbv[j] = *reinterpret_cast<const floatx4*>(colt + (col - n0));
+          fsv[j] = *reinterpret_cast<const floatx4*>(colt + 256 + (col - n0));
+        }
+      }
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const int lr = tt * 32 + li;  // row within the half
         if constexpr (PACKED) {
           // lane half lh holds columns 8 j + 4 lh .. + 3 (4 bf16 = 8 B per plane) of every j; a
           // v_permlane32_swap per register pair (j, j + 1) hands each half the other's 8 B, so
@@ -456,10 +467,9 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
           for (int j = 0; j < 4; ++j) {
             const int cc = tn * 32 + 8 * j + 4 * lh;  // column within the wave's 64
             const int col = cb0 + cc < N ? cb0 + cc : N - 4;
-            const floatx4 bv = FOLD ? *reinterpret_cast<const floatx4*>(colt + (col - n0))
-                                    : *reinterpret_cast<const floatx4*>(bias + col);
+            const floatx4 bv = FOLD ? fbv[j] : *reinterpret_cast<const floatx4*>(bias + col);
             if constexpr (FOLD) {  // rstd * (acc - mean * s) + bias'
-              const floatx4 sv = *reinterpret_cast<const floatx4*>(colt + 256 + (col - n0));
+              const floatx4 sv = fsv[j];
 #pragma unroll
               for (int i = 0; i < 4; i += 2)
                 y[2 * j + i / 2] = __builtin_elementwise_fma(
