@@ -44,6 +44,13 @@ constexpr int KT = 16;              // keys per MFMA tile
 constexpr int XS = H + 4;           // LDS row stride (floats) of the x / u tiles
 constexpr int REC = 32 + NH * H;    // floats per chunk record: m[16], l[16], y[12][768]
 
+// first chunk record of query qj of sequence s (rows [beg, beg + len)): qper·((beg >> 6) + s) bounds
+// qper times the chunk records of the sequences before s, and query qj's ceil(len / 64) chunks
+// follow the sequence's earlier queries' (CLS, qper 1: (beg >> 6) + s, as before)
+__device__ __forceinline__ size_t rec_base(int beg, int s, int qper, int qj, int len) {
+  return (size_t)qper * ((size_t)(beg >> 6) + s) + (size_t)qj * ((len + KC - 1) / KC);
+}
+
 __global__ __launch_bounds__(256) void cls_u_kernel(const float* __restrict__ q,
                                                     const float* __restrict__ wk, int n,
                                                     float* __restrict__ u) {
@@ -74,7 +81,8 @@ __global__ __launch_bounds__(256) void cls_u_kernel(const float* __restrict__ q,
 // profiles/r4o — slower, not kept.)
 __global__ __launch_bounds__(512) void cls_attn_kernel(
     const float* __restrict__ x, const float* __restrict__ u, const int* __restrict__ cu,
-    const uint32_t* __restrict__ mask, int mask_L, float scale, float* __restrict__ part) {
+    const uint32_t* __restrict__ mask, int mask_L, float scale, int qper,
+    float* __restrict__ part) {
   extern __shared__ float lds[];
   float* us = lds;                  // [12][XS]
   float* xs = us + NH * XS;         // [16][XS]
@@ -83,7 +91,8 @@ __global__ __launch_bounds__(512) void cls_attn_kernel(
   float* alpha = pt + 256;          // [16]
   float* mrun = alpha + 16;         // [16]
   float* lrun = mrun + 16;          // [16]
-  const int c = blockIdx.x, s = blockIdx.y;
+  // query qi = blockIdx.y of sequence s = qi / qper (CLS: qper 1, the query is the sequence)
+  const int c = blockIdx.x, qi = blockIdx.y, s = qi / qper, qj = qi - s * qper;
   const int beg = cu[s], len = cu[s + 1] - beg, k0 = c * KC;
   if (k0 >= len) return;
   const int nk = min(KC, len - k0);
@@ -92,7 +101,7 @@ __global__ __launch_bounds__(512) void cls_attn_kernel(
   const uint32_t* mrow = mask ? mask + (size_t)s * mask_L * (mask_L / 32) : nullptr;
 
   // u of this sequence -> LDS (12 x 192 float4)
-  const float4* u4 = reinterpret_cast<const float4*>(u + (size_t)s * NH * H);
+  const float4* u4 = reinterpret_cast<const float4*>(u + (size_t)qi * NH * H);
   for (int i = tid; i < NH * (H / 4); i += 512) {
     const int r = i / (H / 4), c4 = i % (H / 4);
     *reinterpret_cast<float4*>(us + r * XS + 4 * c4) = u4[i];
@@ -188,7 +197,7 @@ __global__ __launch_bounds__(512) void cls_attn_kernel(
         acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[q], xb[4 * q * XS], acc[ct], 0, 0, 0);
     }
   }
-  float* rec = part + ((size_t)(beg >> 6) + s + c) * REC;
+  float* rec = part + (rec_base(beg, s, qper, qj, len) + c) * REC;
   __syncthreads();
   if (tid < 16) {
     rec[tid] = mrun[tid];
@@ -206,12 +215,13 @@ __global__ __launch_bounds__(512) void cls_attn_kernel(
 
 // the chunks of sequence s merged in chunk order: ybar[s][h][c] = Σ_k 2^(m_k - M) y_k[h][c] / L
 __global__ __launch_bounds__(256) void cls_combine_kernel(const float* __restrict__ part,
-                                                          const int* __restrict__ cu,
+                                                          const int* __restrict__ cu, int qper,
                                                           float* __restrict__ ybar,
                                                           int* __restrict__ err) {
-  const int s = blockIdx.x, h = blockIdx.y, col = blockIdx.z * 256 + threadIdx.x;
+  const int qi = blockIdx.x, h = blockIdx.y, col = blockIdx.z * 256 + threadIdx.x;
+  const int s = qi / qper, qj = qi - s * qper;
   const int beg = cu[s], len = cu[s + 1] - beg, nc = (len + KC - 1) / KC;
-  const float* rec0 = part + ((size_t)(beg >> 6) + s) * REC;
+  const float* rec0 = part + rec_base(beg, s, qper, qj, len) * REC;
   float M = -INFINITY;
   for (int c = 0; c < nc; ++c) M = fmaxf(M, rec0[(size_t)c * REC + h]);
   float L = 0.f, y = 0.f;
@@ -223,10 +233,10 @@ __global__ __launch_bounds__(256) void cls_combine_kernel(const float* __restric
       y = fmaf(rec0[(size_t)c * REC + 32 + h * H + col], e, y);
     }
   }
-  if (!(L > 0.f)) {  // no key attended: cannot happen for a CLS row; poison the call
+  if (!(L > 0.f)) {  // no key attended: cannot happen for a CLS / unmasked row; poison the call
     if (threadIdx.x == 0 && blockIdx.z == 0) atomicOr(err, 2);
   }
-  ybar[((size_t)s * NH + h) * H + col] = y * (1.f / L);
+  ybar[((size_t)qi * NH + h) * H + col] = y * (1.f / L);
 }
 
 // ctx[s][64h + d] = b_v[64h + d] + Σ_c W_v[64h + d][c] ybar[s][h][c]: one workgroup per (16
@@ -274,30 +284,38 @@ __global__ __launch_bounds__(256) void cls_vproj_kernel(const float* __restrict_
 
 extern "C" {
 
-// floats of the per-chunk partial records for sequences whose token rows total T (any lens)
-long ae_cls_attention_part_floats(long T, int n) { return ((T >> 6) + n + 2) * (long)REC; }
+// floats of the per-chunk partial records for sequences whose token rows total T (any lens), with
+// qper queries per sequence
+long ae_cls_attention_part_floats(long T, int n, int qper) {
+  return (long)qper * ((T >> 6) + n + 2) * (long)REC;
+}
 
-// q: [n][768] CLS queries (the split modes' W_q carries log2(e)/8, so scale = 1; the exact mode's
+// One query row per (sequence, slot): nq = n·qper queries, query qi of sequence qi / qper (the CLS
+// path: qper 1, the CLS row of every sequence; ae_encode_rows: a window of rows per sequence).
+// q: [nq][768] queries (the split modes' W_q carries log2(e)/8, so scale = 1; the exact mode's
 // does not, scale = log2(e)/8); wk, wv: [768][768] row-major K / V projection weights; bv: [768];
-// x: [T][768] layer-input rows (compacted, cu offsets); u_ws, ybar_ws: [n][12][768];
-// part_ws: ae_cls_attention_part_floats(T, n) floats; ctx: [n][768] out.
+// x: [T][768] layer-input rows (compacted, cu offsets); u_ws, ybar_ws: [nq][12][768];
+// part_ws: ae_cls_attention_part_floats(T, n, qper) floats; ctx: [nq][768] out.  mask (the
+// GraphCodeBERT bit mask, row 0 of each sequence) only with qper 1.
 hipError_t ae_launch_cls_attention(const float* x, const float* q, const float* wk,
                                    const float* wv, const float* bv, const int* cu, int n,
-                                   int max_len, const uint32_t* mask, int mask_L, float scale,
-                                   float* u_ws, float* part_ws, float* ybar_ws, float* ctx,
-                                   int* err, hipStream_t st) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(cls_u_kernel, dim3((n + 3) / 4, NH, H / 256), dim3(256), 0, st, q, wk, n,
+                                   int qper, int max_len, const uint32_t* mask, int mask_L,
+                                   float scale, float* u_ws, float* part_ws, float* ybar_ws,
+                                   float* ctx, int* err, hipStream_t st) {
+  if (n <= 0 || qper <= 0) return hipSuccess;
+  if (mask && qper != 1) return hipErrorInvalidValue;
+  const int nq = n * qper;
+  hipLaunchKernelGGL(cls_u_kernel, dim3((nq + 3) / 4, NH, H / 256), dim3(256), 0, st, q, wk, nq,
                      u_ws);
   const size_t lds = (size_t)(NH * XS + KT * XS + 8 * 256 + 256 + 48) * sizeof(float);
   hipError_t e = ensure_dynamic_lds((const void*)cls_attn_kernel, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(cls_attn_kernel, dim3((max_len + KC - 1) / KC, n), dim3(512), lds, st, x,
-                     u_ws, cu, mask, mask_L, scale, part_ws);
-  hipLaunchKernelGGL(cls_combine_kernel, dim3(n, NH, H / 256), dim3(256), 0, st, part_ws, cu,
-                     ybar_ws, err);
-  hipLaunchKernelGGL(cls_vproj_kernel, dim3((n + 15) / 16, NH, DH / 16), dim3(256), 0, st, ybar_ws,
-                     wv, bv, n, ctx);
+  hipLaunchKernelGGL(cls_attn_kernel, dim3((max_len + KC - 1) / KC, nq), dim3(512), lds, st, x,
+                     u_ws, cu, mask, mask_L, scale, qper, part_ws);
+  hipLaunchKernelGGL(cls_combine_kernel, dim3(nq, NH, H / 256), dim3(256), 0, st, part_ws, cu,
+                     qper, ybar_ws, err);
+  hipLaunchKernelGGL(cls_vproj_kernel, dim3((nq + 15) / 16, NH, DH / 16), dim3(256), 0, st,
+                     ybar_ws, wv, bv, nq, ctx);
   return hipGetLastError();
 }
 

@@ -62,7 +62,7 @@ typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 // every f32 x within 2.9e-7 absolute of the float64 GELU and 8.2e-8 beyond the f32 rounding of
 // the result (the Abramowitz & Stegun 7.1.26 form it replaced — rcp + exp + five FMAs — 2.1e-7
 // beyond rounding; torch's f32 GELU 1.2e-6).  Per pair: two v_min (|x| as a source modifier), six
-// packed FMAs, two v_exp_f32, two v_max and one packed FMA — no reciprocal; written step-major
+// packed FMAs, two v_exp_f32, two v_maximum and one packed FMA — no reciprocal; written step-major
 // over the pairs so that independent chains interleave (no VOP3P dependency stalls).
 template <int NP2>
 __device__ __forceinline__ void gelu_exp2_pairs(gelu_f2 (&x)[NP2]) {
@@ -86,7 +86,9 @@ __device__ __forceinline__ void gelu_exp2_pairs(gelu_f2 (&x)[NP2]) {
 #pragma unroll
   for (int k = 0; k < NP2; ++k) {
     const gelu_f2 e = {__builtin_amdgcn_exp2f(p[k].x), __builtin_amdgcn_exp2f(p[k].y)};
-    x[k] = __builtin_elementwise_fma(-s[k], e, __builtin_elementwise_max(x[k], gelu_f2(0.0f)));
+    // IEEE maximum (v_maximum3_f32), not maxnum: a NaN pre-activation stays NaN (maxnum would
+    // return 0 and the result a finite -6.6e-9 — an upstream overflow must not give finite scores)
+    x[k] = __builtin_elementwise_fma(-s[k], e, __builtin_elementwise_maximum(x[k], gelu_f2(0.0f)));
   }
 }
 

@@ -39,12 +39,12 @@ hipError_t ae_launch_gemm_packed(const unsigned short*, const unsigned short*, c
                                  hipStream_t);
 hipError_t ae_launch_gemm_packed_fold(const unsigned short*, const unsigned short*, const float*,
                                       const float*, const uint64_t*, float, unsigned short*, int,
-                                      int, int, int, int, hipStream_t);
+                                      int, int, int, int, const float*, hipStream_t);
 hipError_t ae_launch_gemm_packed_res_stats(const unsigned short*, const unsigned short*,
                                            const float*, const float*, const uint64_t*,
                                            const float*, const float*, float, float*,
                                            unsigned short*, uint64_t*, int, int, int, int,
-                                           hipStream_t);
+                                           const float*, hipStream_t);
 hipError_t ae_launch_compact(const int*, const int*, const int*, int, int, int, int, int*, int*,
                              int*, int*, hipStream_t);
 hipError_t ae_launch_embed_ln(const int*, const int*, const float*, const float*, const float*,
@@ -66,10 +66,15 @@ hipError_t ae_launch_scatter_rows(const float*, const int*, const int*, int, int
 hipError_t ae_launch_nll_rows(const float*, const int*, int, int, float*, hipStream_t);
 hipError_t ae_launch_graph_mask(const int*, const int*, const int*, const int*, int, int, int,
                                 uint32_t*, hipStream_t);
-long ae_cls_attention_part_floats(long, int);
+long ae_cls_attention_part_floats(long, int, int);
 hipError_t ae_launch_cls_attention(const float*, const float*, const float*, const float*,
-                                   const float*, const int*, int, int, const uint32_t*, int, float,
-                                   float*, float*, float*, float*, int*, hipStream_t);
+                                   const float*, const int*, int, int, int, const uint32_t*, int,
+                                   float, float*, float*, float*, float*, int*, hipStream_t);
+hipError_t ae_launch_query_rows(const int*, const int*, const int*, int, int, int, int*,
+                                hipStream_t);
+hipError_t ae_launch_gather_rows(const float*, const int*, const int*, int, int, float*,
+                                 hipStream_t);
+hipError_t ae_launch_scatter_query(const float*, const int*, int, float*, const int*, hipStream_t);
 }
 
 namespace {
@@ -99,6 +104,9 @@ struct LayerW {
   // and the folded bias bias + W·b
   unsigned short *wqkv_p, *wo_p, *w1_p, *w2_p;
   float *sqkv, *bqkv_f, *s1, *b1_f;
+  // plane shift (gemm_planes.hip FoldArgs): kappa of the O-projection / FFN2 outputs (their bias +
+  // their residual's LayerNorm shift) and the accumulator starts kc = kappa·W'^T of FFN1 / QKV
+  float *kap_o, *kap_f, *kc1, *kcqkv;
 };
 
 struct ProfRec {
@@ -146,6 +154,11 @@ struct ae_engine {
   int* pinned_cu = nullptr;
   size_t cap_pinned = 0;
   hipEvent_t pinned_ready = nullptr;
+  // ae_encode_rows: per-sequence first column of the row window (host pinned -> device) and the
+  // compacted row of every query slot [n][nrows] (-1: no row)
+  int *pinned_r0 = nullptr, *row0_dev = nullptr, *qrow = nullptr;
+  size_t cap_r0 = 0, cap_q = 0;
+  hipEvent_t r0_ready = nullptr;
   // two-stream encoder (split-precision modes unless cfg.streams = AE_STREAMS_ONE; the tools
   // library's AE_SPLIT_STREAMS=0 too): the batch's sequences in two halves, each half's layers on
   // its own stream, the second half one kernel behind, so one half's memory-bound phases (GEMM
@@ -257,21 +270,26 @@ int upload_packed(ae_engine* e, const float* host, size_t rows, size_t K, unsign
 // that consumes its output (gemm_planes.hip FoldArgs): uploads the planes of W' = W·diag(g)
 // (np 2: hi | lo, np 1: hi), s[n] = sum_k W'[n][k] as those planes hold it, and the folded bias
 // bias[n] + sum_k W[n][k]·b[k] (double sums).
+// With kappa (the producer's plane shift, [K]), also kc[n] = sum_k kappa[k]·W'[n][k] as the planes
+// hold W' (double sums): the consumer's accumulator start.
 int upload_folded(ae_engine* e, const float* W, const float* bias, const float* g, const float* b,
                   size_t rows, size_t K, int np, unsigned short** planes, float** s_dev,
-                  float** bias_dev) {
-  std::vector<float> wf(rows * K), sv(rows), bv(rows);
+                  float** bias_dev, const float* kappa = nullptr, float** kc_dev = nullptr) {
+  std::vector<float> wf(rows * K), sv(rows), bv(rows), kv(rows);
   for (size_t r = 0; r < rows; ++r) {
-    double ss = 0.0, bb = bias[r];
+    double ss = 0.0, bb = bias[r], kk = 0.0;
     for (size_t k = 0; k < K; ++k) {
       const float x = W[r * K + k] * g[k];
       wf[r * K + k] = x;
       const float h = host_bf2f(host_f2bf(x));
-      ss += (double)h + (np == 2 ? (double)host_bf2f(host_f2bf(x - h)) : 0.0);
+      const double held = (double)h + (np == 2 ? (double)host_bf2f(host_f2bf(x - h)) : 0.0);
+      ss += held;
+      if (kappa) kk += (double)kappa[k] * held;
       bb += (double)W[r * K + k] * (double)b[k];
     }
     sv[r] = (float)ss;
     bv[r] = (float)bb;
+    kv[r] = (float)kk;
   }
   int rc = np == 2 ? upload_packed(e, wf.data(), rows, K, planes)
                    : upload_split(e, wf.data(), wf.size(), planes, nullptr);
@@ -280,6 +298,22 @@ int upload_folded(ae_engine* e, const float* W, const float* bias, const float* 
     return rc;
   HIPC(hipMemcpy(*s_dev, sv.data(), rows * 4, hipMemcpyHostToDevice));
   HIPC(hipMemcpy(*bias_dev, bv.data(), rows * 4, hipMemcpyHostToDevice));
+  if (kappa && kc_dev) {
+    if ((rc = dev_alloc(e, (void**)kc_dev, rows * 4))) return rc;
+    HIPC(hipMemcpy(*kc_dev, kv.data(), rows * 4, hipMemcpyHostToDevice));
+  }
+  return AE_OK;
+}
+
+// kappa = bias + beta (the per-column constant part of a residual add whose residual is a
+// LayerNorm output with shift beta), uploaded; host copy in out
+int upload_kappa(ae_engine* e, const float* bias, const float* beta, size_t n,
+                 std::vector<float>& out, float** dev) {
+  out.resize(n);
+  for (size_t i = 0; i < n; ++i) out[i] = bias[i] + beta[i];
+  int rc = dev_alloc(e, (void**)dev, n * 4);
+  if (rc) return rc;
+  HIPC(hipMemcpy(*dev, out.data(), n * 4, hipMemcpyHostToDevice));
   return AE_OK;
 }
 
@@ -336,8 +370,8 @@ int ensure_workspace(ae_engine* e, size_t T, size_t n) {
 }
 
 // Partial records of the last layer's CLS attention for T rows of n sequences.
-int ensure_cls_part(ae_engine* e, int64_t T, int n) {
-  const size_t need = (size_t)ae_cls_attention_part_floats((long)T, n);
+int ensure_cls_part(ae_engine* e, int64_t T, int n, int qper) {
+  const size_t need = (size_t)ae_cls_attention_part_floats((long)T, n, qper);
   if (need <= e->cap_cls_part) return AE_OK;
   HIPC(hipDeviceSynchronize());
   dev_free(e, e->cls_part);
@@ -470,7 +504,7 @@ int layer_rows(ae_engine* e, int li, int64_t t0, int M, int s0, int ns, int max_
     Prof p(e, st, prof, 2.0 * M * 3 * H * H);
     if (prev)
       HIPC(ae_launch_gemm_packed_fold(xp, w.wqkv_p, w.bqkv_f, w.sqkv, sa, eps, qkvp, M, 3 * H, H,
-                                      0, np, st));
+                                      0, np, w.kcqkv, st));
     else
       HIPC(ae_launch_gemm_packed(xp, w.wqkv_p, w.bqkv, nullptr, nullptr, qkvp, M, 3 * H, H,
                                  EPI_BIAS_PACKED, np, st));
@@ -488,18 +522,19 @@ int layer_rows(ae_engine* e, int li, int64_t t0, int M, int s0, int ns, int max_
     HIPC(ae_launch_gemm_packed_res_stats(cp, w.wo_p, w.bo, prev ? v : e->x + t0 * H,
                                          prev ? sa : nullptr, prev ? prev->ln2g : nullptr,
                                          prev ? prev->ln2b : nullptr, eps, v, xp, sb, M, H, H, np,
-                                         st));
+                                         w.kap_o, st));
   }
   if (int rc = done()) return rc;
   {
     Prof p(e, st, prof || e->prof_kind == AE_KIND_GEMM_FFN1, 2.0 * M * F * H);
-    HIPC(ae_launch_gemm_packed_fold(xp, w.w1_p, w.b1_f, w.s1, sb, eps, hp, M, F, H, 1, np, st));
+    HIPC(ae_launch_gemm_packed_fold(xp, w.w1_p, w.b1_f, w.s1, sb, eps, hp, M, F, H, 1, np, w.kc1,
+                                    st));
   }
   if (int rc = done()) return rc;
   {
     Prof p(e, st, prof, 2.0 * M * H * F);
     HIPC(ae_launch_gemm_packed_res_stats(hp, w.w2_p, w.b2, v, sb, w.ln1g, w.ln1b, eps, v, xp, sa,
-                                         M, H, F, np, st));
+                                         M, H, F, np, w.kap_f, st));
   }
   if (int rc = done()) return rc;
   if (last) HIPC(ae_launch_layernorm(v, w.ln2g, w.ln2b, eps, M, e->x + t0 * H, nullptr, 0, st));
@@ -508,14 +543,20 @@ int layer_rows(ae_engine* e, int li, int64_t t0, int M, int s0, int ns, int max_
 
 // Runs the encoder over compacted tokens; on return the last-layer CLS rows are in e->xc
 // (cls_only) or all rows in e->x.  lens: the host copy of the sequence lengths (two-stream mode).
+// qper > 0 (cls_only): the last layer runs for the query rows e->qrow [n][qper] (ae_encode_rows)
+// instead of the CLS rows; on return they are in e->xc [n·qper][H].
 int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint32_t* mask_bits,
                 int n, int L, int64_t T, int max_len, bool cls_only, hipStream_t st,
-                int keep_all = 0, bool node_avg = false, const int32_t* lens = nullptr) {
+                int keep_all = 0, bool node_avg = false, const int32_t* lens = nullptr,
+                int qper = 0) {
   const int H = e->cfg.hidden, F = e->cfg.ffn, NL = e->cfg.layers, heads = e->cfg.heads;
   const float eps = e->cfg.ln_eps;
   HIPC(hipMemsetAsync(e->err, 0, sizeof(int), st));
   HIPC(ae_launch_compact(ids, pos, e->cu, n, L, e->cfg.pad_id, keep_all, e->tok_ids, e->tok_pos,
                          e->src_col, e->err, st));
+  // ae_encode_rows: the compacted row of every query slot (columns row0_dev[s] + j)
+  if (qper > 0)
+    HIPC(ae_launch_query_rows(e->cu, e->src_col, e->row0_dev, n, qper, (int)T, e->qrow, st));
   const bool pl = e->planes;
   HIPC(ae_launch_embed_ln(e->tok_ids, e->tok_pos, e->wemb, e->pemb, e->temb, e->eg, e->eb, eps,
                           (int)T, e->cfg.max_pos, e->x, pl ? e->xp : nullptr, e->np,
@@ -566,28 +607,35 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
   for (int li = first; li < NL; ++li) {
     const LayerW& w = e->layers[li];
     const bool last_cls = cls_only && li == NL - 1;
+    const int nq = qper > 0 ? n * qper : n;  // rows of the last layer's query path
     int rc;
+    if (last_cls && !e->cls_absorb && qper > 0)
+      return fail(AE_EINVAL, "row windows need the absorbed last layer (AE_CLS_ABSORB)");
     if (last_cls && e->cls_absorb) {
-      // the CLS query per sequence, then attention with W_k absorbed / W_v deferred over the
-      // layer-input rows (cls_attention.hip); no K / V projection of the T rows
-      HIPC(ae_launch_gather_cls(e->x, e->x, e->cu, n, e->cc, e->xc, st));
-      if ((rc = gemm(e, e->xc, w.wqkv, w.wqkv_h, w.wqkv_l, w.bqkv, nullptr, e->hc, n, H, H,
+      // the CLS query per sequence (or the query rows of ae_encode_rows), then attention with W_k
+      // absorbed / W_v deferred over the layer-input rows (cls_attention.hip); no K / V
+      // projection of the T rows
+      if (qper > 0)
+        HIPC(ae_launch_gather_rows(e->x, e->qrow, e->cu, qper, nq, e->xc, st));
+      else
+        HIPC(ae_launch_gather_cls(e->x, e->x, e->cu, n, e->cc, e->xc, st));
+      if ((rc = gemm(e, e->xc, w.wqkv, w.wqkv_h, w.wqkv_l, w.bqkv, nullptr, e->hc, nq, H, H,
                      EPI_BIAS, st, false)))
         return rc;
-      if ((rc = ensure_cls_part(e, T, n))) return rc;
+      if ((rc = ensure_cls_part(e, T, n, qper > 0 ? qper : 1))) return rc;
       Prof p(e, st, e->prof_kind == AE_KIND_ATTENTION, 0.0);
       // split modes fold log2(e)/8 into W_q (ae_create); the exact mode scales here
       const float scale = e->cfg.precision == AE_PREC_FP32 ? 0.18033688011112042f : 1.0f;
       HIPC(ae_launch_cls_attention(e->x, e->hc, w.wqkv + (size_t)H * H,
-                                   w.wqkv + (size_t)2 * H * H, w.bqkv + 2 * H, e->cu, n, max_len,
-                                   mask_bits, L, scale, e->cls_u, e->cls_part, e->cls_y, e->cc,
-                                   e->err, st));
+                                   w.wqkv + (size_t)2 * H * H, w.bqkv + 2 * H, e->cu, n,
+                                   qper > 0 ? qper : 1, max_len, mask_bits, L, scale, e->cls_u,
+                                   e->cls_part, e->cls_y, e->cc, e->err, st));
     } else if (pl && li > 0) {
       // Q | K | V as packed planes (Q pre-scaled) straight into the attention's LDS-DMA, from the
       // previous layer's pre-LayerNorm rows (the LayerNorm folded in)
       Prof p(e, st, e->prof_kind == AE_KIND_GEMM_ANY, 2.0 * T * 3 * H * H);
       HIPC(ae_launch_gemm_packed_fold(e->xp, w.wqkv_p, w.bqkv_f, w.sqkv, e->lnst, eps, qkvp,
-                                      (int)T, 3 * H, H, 0, e->np, st));
+                                      (int)T, 3 * H, H, 0, e->np, w.kcqkv, st));
     } else if (pl) {
       if ((rc = gemm_pk(e, e->xp, w.wqkv_p, w.bqkv, nullptr, nullptr, qkvp, (int)T, 3 * H, H,
                         EPI_BIAS_PACKED, st, false)))
@@ -621,17 +669,17 @@ int run_encoder(ae_engine* e, const int32_t* ids, const int32_t* pos, const uint
       HIPC(ae_launch_layernorm(e->tmp, w.ln2g, w.ln2b, eps, (int)T, e->x, nullptr, 0, st));
     } else {
       if (!e->cls_absorb) HIPC(ae_launch_gather_cls(e->ctx, e->x, e->cu, n, e->cc, e->xc, st));
-      if ((rc = gemm(e, e->cc, w.wo, w.wo_h, w.wo_l, w.bo, e->xc, e->tc, n, H, H, EPI_BIAS_RESIDUAL, st,
-                     false)))
+      if ((rc = gemm(e, e->cc, w.wo, w.wo_h, w.wo_l, w.bo, e->xc, e->tc, nq, H, H, EPI_BIAS_RESIDUAL,
+                     st, false)))
         return rc;
-      HIPC(ae_launch_layernorm(e->tc, w.ln1g, w.ln1b, eps, n, e->xc, nullptr, 0, st));
-      if ((rc = gemm(e, e->xc, w.w1, w.w1_h, w.w1_l, w.b1, nullptr, e->hc, n, F, H, EPI_BIAS_GELU, st,
-                     false)))
+      HIPC(ae_launch_layernorm(e->tc, w.ln1g, w.ln1b, eps, nq, e->xc, nullptr, 0, st));
+      if ((rc = gemm(e, e->xc, w.w1, w.w1_h, w.w1_l, w.b1, nullptr, e->hc, nq, F, H, EPI_BIAS_GELU,
+                     st, false)))
         return rc;
-      if ((rc = gemm(e, e->hc, w.w2, w.w2_h, w.w2_l, w.b2, e->xc, e->tc, n, H, F, EPI_BIAS_RESIDUAL, st,
-                     false)))
+      if ((rc = gemm(e, e->hc, w.w2, w.w2_h, w.w2_l, w.b2, e->xc, e->tc, nq, H, F, EPI_BIAS_RESIDUAL,
+                     st, false)))
         return rc;
-      HIPC(ae_launch_layernorm(e->tc, w.ln2g, w.ln2b, eps, n, e->xc, nullptr, 0, st));
+      HIPC(ae_launch_layernorm(e->tc, w.ln2g, w.ln2b, eps, nq, e->xc, nullptr, 0, st));
     }
   }
   return AE_OK;
@@ -688,6 +736,7 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
   UP("embeddings.LayerNorm.weight", H, &e->eg);
   UP("embeddings.LayerNorm.bias", H, &e->eb);
   e->layers.resize(cfg->layers);
+  std::vector<float> prev_kap_f;  // the previous layer's FFN2 plane shift (its QKV consumer's)
   for (int l = 0; l < cfg->layers; ++l) {
     LayerW& w = e->layers[l];
     std::memset(&w, 0, sizeof(w));
@@ -765,6 +814,20 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
       const ae_weight_view* b1 = view(p + "attention.output.LayerNorm.bias");
       const ae_weight_view* bi = view(p + "intermediate.dense.bias");
       const int np = lo ? 2 : 1;
+      // plane shifts: the O-projection's v = ... + b_o + LN(prev) (layer 0: the embedding LN's
+      // x) and FFN2's v = ... + b_2 + LN1(v_o) carry the constant columns b + beta; their planes
+      // hold v - kappa, and FFN1 / the next layer's QKV start their accumulators at kappa·W'^T
+      std::vector<float> kap_o, kap_f;
+      if ((rc = upload_kappa(e, view(p + "attention.output.dense.bias")->data,
+                             view(l == 0 ? std::string("embeddings.LayerNorm.bias")
+                                         : pp + "output.LayerNorm.bias")->data,
+                             H, kap_o, &w.kap_o)) ||
+          (rc = upload_kappa(e, view(p + "output.dense.bias")->data, b1->data, H, kap_f,
+                             &w.kap_f))) {
+        std::string m = g_err;
+        ae_destroy(e);
+        return fail(rc, m);
+      }
       if (lo) {
         if ((l == 0 && (rc = upload_packed(e, hw.data(), 3 * H, H, &w.wqkv_p))) ||
             (rc = upload_packed(e, vo->data, H, H, &w.wo_p)) ||
@@ -779,15 +842,17 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
         w.w2_p = w.w2_h;
       }
       if ((rc = upload_folded(e, v1->data, bi->data, g1->data, b1->data, F, H, np, &w.w1_p, &w.s1,
-                              &w.b1_f)) ||
+                              &w.b1_f, kap_o.data(), &w.kc1)) ||
           (l > 0 && (rc = upload_folded(e, hw.data(), hb.data(),
                                         view(pp + "output.LayerNorm.weight")->data,
                                         view(pp + "output.LayerNorm.bias")->data, 3 * H, H, np,
-                                        &w.wqkv_p, &w.sqkv, &w.bqkv_f)))) {
+                                        &w.wqkv_p, &w.sqkv, &w.bqkv_f, prev_kap_f.data(),
+                                        &w.kcqkv)))) {
         std::string m = g_err;
         ae_destroy(e);
         return fail(rc, m);
       }
+      prev_kap_f = kap_f;
     }
   }
   if (cfg->head_kind != AE_HEAD_NONE) {
@@ -814,6 +879,8 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
   HIPC(hipMemcpy(e->one, one_host, 16, hipMemcpyHostToDevice));
   HIPC(hipEventCreateWithFlags(&e->pinned_ready, hipEventDisableTiming));
   HIPC(hipEventRecord(e->pinned_ready, nullptr));
+  HIPC(hipEventCreateWithFlags(&e->r0_ready, hipEventDisableTiming));
+  HIPC(hipEventRecord(e->r0_ready, nullptr));
 #ifdef AE_TOOLS
   // A/B knobs of the tools library (lib/libalert_engine_tools.so, tools/engine_ab.py and the
   // alternative-form parity tests); the product library has the defaults compiled in
@@ -868,6 +935,8 @@ int ae_destroy(ae_engine* e) {
     if (p) (void)hipFree(p);
   if (e->pinned_cu) (void)hipHostFree(e->pinned_cu);
   if (e->pinned_ready) (void)hipEventDestroy(e->pinned_ready);
+  if (e->pinned_r0) (void)hipHostFree(e->pinned_r0);
+  if (e->r0_ready) (void)hipEventDestroy(e->r0_ready);
   if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
   for (int p = 0; p < ae_engine::kMaxParts; ++p) {
     if (e->ev_lag[p]) (void)hipEventDestroy(e->ev_lag[p]);
@@ -958,6 +1027,59 @@ int ae_encode_ex(ae_engine* e, const int32_t* ids, const int32_t* lens, int32_t 
 int ae_encode(ae_engine* e, const int32_t* ids, const int32_t* lens, int32_t n, int32_t L,
               float* hidden_out, void* stream) {
   return ae_encode_ex(e, ids, lens, n, L, 0, 0, L, hidden_out, stream);
+}
+
+int ae_encode_rows(ae_engine* e, const int32_t* ids, const int32_t* lens, int32_t n, int32_t L,
+                   int32_t flags, const int32_t* row0, int32_t nrows, float* hidden_out,
+                   void* stream) {
+  int rc = check_common(e, ids, lens, n, L);
+  if (rc) return rc;
+  if (!hidden_out || !row0) return fail(AE_EINVAL, "null hidden_out/row0");
+  if (nrows < 1 || nrows > L) return fail(AE_EINVAL, "bad nrows");
+  for (int i = 0; i < n; ++i)
+    if (row0[i] < 0 || row0[i] + nrows > L)
+      return fail(AE_EINVAL, "row0[" + std::to_string(i) + "]=" + std::to_string(row0[i]) +
+                                 ": window outside [0, L)");
+  if (flags & ~AE_ENC_ATTEND_PAD) return fail(AE_EINVAL, "unknown flags");
+  if (!e->cls_absorb) return fail(AE_EINVAL, "row windows need the absorbed last layer");
+  if (n == 0) return AE_OK;
+  HIPC(hipSetDevice(e->device));
+  hipStream_t st = (hipStream_t)stream;
+  const size_t nq = (size_t)n * nrows;
+  if ((rc = ensure_workspace(e, (size_t)n * L, nq > (size_t)n ? nq : (size_t)n))) return rc;
+  if ((size_t)n > e->cap_r0) {
+    HIPC(hipDeviceSynchronize());
+    const size_t c = n + n / 4 + 64;
+    dev_free(e, e->row0_dev);
+    e->row0_dev = nullptr;
+    if (e->pinned_r0) (void)hipHostFree(e->pinned_r0);
+    e->pinned_r0 = nullptr;
+    if ((rc = dev_alloc(e, (void**)&e->row0_dev, c * 4))) return rc;
+    HIPC(hipHostMalloc((void**)&e->pinned_r0, c * 4, hipHostMallocDefault));
+    e->cap_r0 = c;
+  }
+  if (nq > e->cap_q) {
+    HIPC(hipDeviceSynchronize());
+    const size_t c = nq + nq / 4 + 64;
+    dev_free(e, e->qrow);
+    e->qrow = nullptr;
+    if ((rc = dev_alloc(e, (void**)&e->qrow, c * 4))) return rc;
+    e->cap_q = c;
+  }
+  int64_t T = 0;
+  if ((rc = upload_cu(e, lens, n, L, st, &T))) return rc;
+  HIPC(hipEventSynchronize(e->r0_ready));  // the previous call's copy has left the pinned buffer
+  std::memcpy(e->pinned_r0, row0, (size_t)n * 4);
+  HIPC(hipMemcpyAsync(e->row0_dev, e->pinned_r0, (size_t)n * 4, hipMemcpyHostToDevice, st));
+  HIPC(hipEventRecord(e->r0_ready, st));
+  int max_len = 0;
+  for (int i = 0; i < n; ++i) max_len = lens[i] > max_len ? lens[i] : max_len;
+  // the query slots (e->qrow) are built from row0_dev by run_encoder right after compaction
+  if ((rc = run_encoder(e, ids, nullptr, nullptr, n, L, T, max_len, true, st,
+                        (flags & AE_ENC_ATTEND_PAD) ? 1 : 0, false, lens, nrows)))
+    return rc;
+  HIPC(ae_launch_scatter_query(e->xc, e->qrow, (int)nq, hidden_out, e->err, st));
+  return AE_OK;
 }
 
 }  // extern "C"

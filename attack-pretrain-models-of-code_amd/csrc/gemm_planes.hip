@@ -61,10 +61,17 @@ struct RowStat {
 // prepared at engine creation), so the GEMM multiplies the pre-LayerNorm rows v directly and the
 // epilogue applies the row's (mean, rstd) — merged from the 4 per-tile statistics the producing
 // PK_EPI_RES_STATS epilogue wrote.  No LayerNorm pass over the rows.
+//
+// Plane shift: the producer splits v - kappa into the planes (kappa = its bias plus the LayerNorm
+// shift b of its residual: the per-column constant part of v, StatArgs::shift), so the split's
+// rounding scales with |v - kappa| — the row's spread — and not with a common row offset or a
+// per-column outlier constant.  The consumer starts its accumulators at kc[n] = sum_k kappa[k] ·
+// W'[n][k] (W' as its planes hold it; FoldArgs::kc), so acc = v·W'^T still.
 struct FoldArgs {
   const float* s;          // [N]
   const uint64_t* stats;   // [M rows][4] RowStat of the 4 192-column tiles of each row
   float eps;
+  const float* kc;         // [N] or null: the accumulator start (plane shift of the A rows)
 };
 
 // (mean, rstd) of a 768-wide row from its 4 tile statistics (n = 192 each), merged as (0,1),
@@ -88,9 +95,10 @@ struct StatArgs {
   const float* gamma;      // _LN: the residual's LayerNorm gain / shift
   const float* beta;
   float eps;
-  __bf16* xp;              // packed planes of the output v ([M][NP * N])
+  __bf16* xp;              // packed planes of v - shift ([M][NP * N])
   uint64_t* stats;         // [M][4] RowStat of each output row over each 192-column tile
   const uint64_t* rstats;  // _LN: the residual's own tile statistics
+  const float* shift;      // [N] or null: kappa, subtracted from v before the plane split
 };
 
 namespace {
@@ -342,6 +350,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
         dma16(fold.stats + (size_t)min(m0 + r0 + (lane >> 1), M - 1) * 4 + 2 * (lane & 1),
               lds0 + SIDE + 2048 + (uint32_t)(r0 * 32));
       }
+    } else if (wave == 5 && fold.kc) {  // the accumulator start kc of the tile's 256 columns
+      dma16(fold.kc + min(n0 + 4 * lane, N - 4), lds0 + SIDE + 10240);
     }
   }
   // prologue: K-tile 0 whole and K-tile 1's first two quarters (the loop issues the rest)
@@ -358,6 +368,23 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
   }
   if (DIAG == 1 || DIAG == 6 || DIAG == 7) pp_wait_vm<0>();
   __builtin_amdgcn_s_barrier();
+  if constexpr (FOLD_EPI) {
+    // plane shift (FoldArgs): the accumulators start at kc of their columns (side data, landed
+    // with this wave's first wait — older than every K-tile piece — and visible past the barrier)
+    if (fold.kc) {
+      const float* const kcl = reinterpret_cast<const float*>(pk_smem + SIDE + 10240);
+#pragma unroll
+      for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const floatx4 k4 = *reinterpret_cast<const floatx4*>(kcl + wn * 64 + tn * 32 + 8 * j + 4 * lh);
+#pragma unroll
+          for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[tm][tn][4 * j + i] = k4[i];
+        }
+    }
+  }
   if (wm == 1) sync_load();  // group 1 runs one phase behind
 
   auto wait6 = [&](bool full) {
@@ -723,6 +750,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
         dma16(ln.rstats + (size_t)min(m0 + r0 + (lane >> 1), M - 1) * 4 + 2 * (lane & 1),
               lds0 + SIDE + 3072 + (uint32_t)(r0 * 32));
       }
+    } else if (wave == 5 && ln.shift) {  // the plane shift kappa of the tile's 192 columns
+      dma16(ln.shift + n0 + 4 * min(lane, 47), lds0 + SIDE + 11264);
     }
   }
   // prologue: K-tile 0 whole, K-tile 1's A + W(tn 0) (its W(tn 1), W(tn 2): phases 0, 1 of kt 0)
@@ -897,9 +926,15 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
           *reinterpret_cast<floatx4*>(vrow + col) = o0;
           *reinterpret_cast<floatx4*>(vrow + col + 4) = o1;
           uint32_t h[4], l[4];  // column pairs as packed bf16 conversions (split_pair)
+          floatx4 p0 = o0, p1 = o1;  // the planes hold v - kappa (the plane shift, FoldArgs)
+          if (ln.shift) {
+            const float* const kap = reinterpret_cast<const float*>(pk_smem + SIDE + 11264);
+            p0 -= *reinterpret_cast<const floatx4*>(kap + (col - n0));
+            p1 -= *reinterpret_cast<const floatx4*>(kap + (col - n0) + 4);
+          }
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            split_pair(i < 2 ? gelu_f2{o0[2 * i], o0[2 * i + 1]} : gelu_f2{o1[2 * i - 4], o1[2 * i - 3]},
+            split_pair(i < 2 ? gelu_f2{p0[2 * i], p0[2 * i + 1]} : gelu_f2{p1[2 * i - 4], p1[2 * i - 3]},
                        h[i], l[i]);
           unsigned short* dst = reinterpret_cast<unsigned short*>(ln.xp) + (size_t)prow0 * NP * N +
                                 (uint32_t)(lr + tm * 32) * (uint32_t)(NP * N) +
@@ -1032,9 +1067,10 @@ template <int NP, int EPI, int DIAG>
 hipError_t pp_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R, float* C,
                      __bf16* Cp, int M, int N, int K, int group_m, hipStream_t st,
                      FoldArgs fold = FoldArgs{}) {
-  // 128 KiB (+ 10 KiB of side data for the folded epilogues: bias' / s columns, row statistics)
+  // 128 KiB (+ 11 KiB of side data for the folded epilogues: bias' / s columns, row statistics,
+  // the accumulator start kc)
   constexpr int lds = 2 * (256 + 256) * PK_ROWB +
-                      (EPI == PK_EPI_GELU_FOLD || EPI == PK_EPI_BIAS_FOLD ? 10240 : 0);
+                      (EPI == PK_EPI_GELU_FOLD || EPI == PK_EPI_BIAS_FOLD ? 11264 : 0);
   if (hipError_t e = ensure_dynamic_lds((const void*)gemm_pp_kernel<NP, EPI, DIAG>, lds); e != hipSuccess)
     return e;
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
@@ -1072,9 +1108,10 @@ template <int NP, int EPI, bool NT = false>
 hipError_t pp192_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R,
                         float* C, int M, int N, int K, int group_m, hipStream_t st,
                         StatArgs ln = StatArgs{}) {
-  // 112 KiB (+ 11 KiB of side data for the residual + statistics epilogues)
+  // 112 KiB (+ 12 KiB of side data for the residual + statistics epilogues: bias, gamma, beta,
+  // the residual rows' statistics, the plane shift)
   constexpr int lds = 2 * (256 + 192) * PK_ROWB +
-                      (EPI == PK_EPI_RES_STATS || EPI == PK_EPI_RES_STATS_LN ? 11264 : 0);
+                      (EPI == PK_EPI_RES_STATS || EPI == PK_EPI_RES_STATS_LN ? 12288 : 0);
   if (hipError_t e = ensure_dynamic_lds((const void*)gemm_pp192_kernel<NP, EPI, NT>, lds); e != hipSuccess)
     return e;
   const int tiles_m = (M + 255) / 256;
@@ -1184,15 +1221,16 @@ extern "C" hipError_t ae_launch_gemm_packed(const unsigned short* A, const unsig
 // The folded-LayerNorm pair (FoldArgs).  Cp = packed planes of
 //   gelu = 0: rstd * (A·W'^T - mean * s) + bias'          (the QKV GEMM of layers >= 1)
 //   gelu = 1: GELU(rstd * (A·W'^T - mean * s) + bias')    (FFN1)
-// A: the packed planes of the pre-LayerNorm rows v; stats: their [M][4] tile statistics.
+// A: the packed planes of the pre-LayerNorm rows v (of v - kappa under the plane shift, when kc =
+// kappa·W'^T is given: the accumulators start at kc); stats: v's [M][4] tile statistics.
 extern "C" hipError_t ae_launch_gemm_packed_fold(const unsigned short* A, const unsigned short* W,
                                                  const float* bias, const float* s,
                                                  const uint64_t* stats, float eps,
                                                  unsigned short* Cp, int M, int N, int K, int gelu,
-                                                 int np, hipStream_t st) {
+                                                 int np, const float* kc, hipStream_t st) {
   if (M <= 0) return hipSuccess;
   if (!pk_shape_ok(M, N, K, np) || !bias || !s || !stats || !Cp) return hipErrorInvalidValue;
-  const FoldArgs fold{s, stats, eps};
+  const FoldArgs fold{s, stats, eps, kc};
   auto a = reinterpret_cast<const __bf16*>(A);
   auto w = reinterpret_cast<const __bf16*>(W);
   __bf16* cp = reinterpret_cast<__bf16*>(Cp);
@@ -1204,18 +1242,19 @@ extern "C" hipError_t ae_launch_gemm_packed_fold(const unsigned short* A, const 
 }
 
 // v = A·W^T + bias + r over rows of N = 768 (the O-projection / FFN2), written as f32 C and packed
-// planes Cp, with the (mean, M2) of every row over each of its 4 192-column tiles into stats
-// ([M][4] 8-B words).  r = R as it is when rstats is null, else r = LN(R) with R's own tile
+// planes Cp of v - shift (shift null: of v; the plane shift, FoldArgs), with the (mean, M2) of every
+// row of v over each of its 4 192-column tiles into stats ([M][4] 8-B words).  r = R as it is when rstats is null, else r = LN(R) with R's own tile
 // statistics rstats and gamma / beta (R a pre-LayerNorm row).  R may equal C.
 extern "C" hipError_t ae_launch_gemm_packed_res_stats(
     const unsigned short* A, const unsigned short* W, const float* bias, const float* R,
     const uint64_t* rstats, const float* gamma, const float* beta, float eps, float* C,
-    unsigned short* Cp, uint64_t* stats, int M, int N, int K, int np, hipStream_t st) {
+    unsigned short* Cp, uint64_t* stats, int M, int N, int K, int np, const float* shift,
+    hipStream_t st) {
   if (M <= 0) return hipSuccess;
   if (N != 768 || K % 64 != 0 || (np != 1 && np != 2) || !bias || !R || !C || !Cp || !stats ||
       (rstats && (!gamma || !beta)))
     return hipErrorInvalidValue;
-  const StatArgs ln{gamma, beta, eps, reinterpret_cast<__bf16*>(Cp), stats, rstats};
+  const StatArgs ln{gamma, beta, eps, reinterpret_cast<__bf16*>(Cp), stats, rstats, shift};
   auto a = reinterpret_cast<const __bf16*>(A);
   auto w = reinterpret_cast<const __bf16*>(W);
   if (rstats)

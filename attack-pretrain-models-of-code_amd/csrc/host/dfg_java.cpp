@@ -313,19 +313,27 @@ class JTree {
       name = r;
       typed = true;
     }
-    if (!typed && q == 0) {
-      // a constructor with no modifier (`Name(T p) throws E {`): tree-sitter recovers it as a
-      // call — its parameters are plain leaves, not definitions — and the first exception type
-      // of `throws` as a declared name (the BigCloneBench fixture keys of `HttpRepository`)
+    if (!typed && (q == 0 || (t(q + 1) == "(" && t(q + 2) == ")"))) {
+      // a constructor with no modifier (`Name(T p) throws E {`), or with modifiers and no
+      // parameters (`public Name() throws A, B {`): tree-sitter recovers it as a call — its
+      // parameters are plain leaves, not definitions — followed by a declaration whose
+      // declarators are the simple exception types of `throws` (the BigCloneBench fixture keys
+      // of `HttpRepository`: its one type; of `FileChooserTestFrame`: both of its two)
       leaves_to(root, name + 1);
       leaves_to(root, close_of(p_) + 1);
       if (at("throws") && is_ident(t(p_ + 1))) {
         add_leaf(root, p_++);
         const int lvd0 = make(J_LVD);
         attach(root, lvd0);
-        const int d = make(J_DECLARATOR);
-        attach(lvd0, d);
-        nodes[d].a = add_leaf(d, p_++);
+        for (;;) {
+          const int d = make(J_DECLARATOR);
+          attach(lvd0, d);
+          nodes[d].a = add_leaf(d, p_++);
+          if (!(at(",") && is_ident(t(p_ + 1)) &&
+                (t(p_ + 2) == "," || t(p_ + 2) == "{" || t(p_ + 2) == ";")))
+            break;
+          add_leaf(lvd0, p_++);
+        }
       }
       while (more() && !at("{") && !at(";")) add_leaf(root, p_++);
       return;
@@ -361,7 +369,13 @@ class JTree {
     // declaration continues past the first exception type, so every later simple name is one more
     // declarator — the fixture keys list B and C (never A) exactly in those headers and never
     // after two or more parameters
+    // A header that starts with a marker annotation (`@Override`, no arguments) shifts the
+    // recovery one type further: the declarators start at the third type, after at most two
+    // parameters (`@Override ... (String message) throws A, B, C, D` keys C and D; `@Override ...
+    // (URL url, String skin) throws A, B, C` keys C; no marker-annotated header with two types
+    // keys either).
     bool more_decls = false;
+    int skip_decls = 0;
     if (at("throws")) {
       size_t q = p_ + 1;
       bool qualified = false;
@@ -369,11 +383,23 @@ class JTree {
         qualified = true;
         q += 2;
       }
-      more_decls = nparams <= 1 || qualified;
+      const bool marker = t(0) == "@" && is_ident(t(1)) && t(2) != "(" && t(2) != ".";
+      if (marker && !qualified) {
+        more_decls = nparams <= 2;
+        skip_decls = 1;
+      } else {
+        more_decls = nparams <= 1 || qualified;
+      }
     }
     while (more() && !at("{") && !at(";")) {
       if (lvd >= 0 && more_decls && at(",") && is_ident(t(p_ + 1)) &&
           (t(p_ + 2) == "," || t(p_ + 2) == "{" || t(p_ + 2) == ";")) {
+        if (skip_decls > 0) {
+          --skip_decls;
+          add_leaf(root, p_++);
+          add_leaf(root, p_++);
+          continue;
+        }
         add_leaf(lvd, p_++);
         const int d = make(J_DECLARATOR);
         attach(lvd, d);

@@ -318,6 +318,60 @@ __global__ __launch_bounds__(256) void scatter_rows_kernel(const float* __restri
   }
 }
 
+// Query rows of ae_encode_rows: sequence s asks for its columns [row0[s], row0[s] + nrows); slot
+// s·nrows + j gets the compacted row t of column row0[s] + j (qrow pre-filled with -1 by the
+// caller: a column past lens or a pad the compaction dropped stays -1 and is never written out).
+__global__ __launch_bounds__(256) void query_rows_kernel(const int* __restrict__ cu,
+                                                         const int* __restrict__ src_col,
+                                                         const int* __restrict__ row0, int n,
+                                                         int nrows, int T, int* __restrict__ qrow) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= T) return;
+  int lo = 0, hi = n;  // s with cu[s] <= t < cu[s+1]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (cu[mid] <= t) lo = mid; else hi = mid;
+  }
+  const int c = src_col[t] - row0[lo];
+  if (c >= 0 && c < nrows) qrow[lo * nrows + c] = t;
+}
+
+// xq[i] = x[qrow[i]] (a slot without a row copies its sequence's first row: computed, never stored)
+__global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restrict__ x,
+                                                          const int* __restrict__ qrow,
+                                                          const int* __restrict__ cu, int qper,
+                                                          int nq, float* __restrict__ xq) {
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= nq) return;
+  const int t = qrow[i] >= 0 ? qrow[i] : cu[i / qper];
+  const size_t src = (size_t)t * AE_HIDDEN;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const int col = c * 256 + lane * 4;
+    *reinterpret_cast<floatx4*>(xq + (size_t)i * AE_HIDDEN + col) =
+        *reinterpret_cast<const floatx4*>(x + src + col);
+  }
+}
+
+// out[i] = xq[i] for the slots that have a row (NaN when the lens disagreed with the ids)
+__global__ __launch_bounds__(256) void scatter_query_kernel(const float* __restrict__ xq,
+                                                            const int* __restrict__ qrow, int nq,
+                                                            float* __restrict__ out,
+                                                            const int* __restrict__ err) {
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= nq || qrow[i] < 0) return;
+  const bool bad = err && *err;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const int col = c * 256 + lane * 4;
+    floatx4 v = *reinterpret_cast<const floatx4*>(xq + (size_t)i * AE_HIDDEN + col);
+    if (bad) v = floatx4{NAN, NAN, NAN, NAN};
+    *reinterpret_cast<floatx4*>(out + (size_t)i * AE_HIDDEN + col) = v;
+  }
+}
+
 // Token negative log-likelihood of the MLM logits (CrossEntropyLoss(reduction='none') of
 // utils.py:238-239): nll[t] = logsumexp(logits[t, :]) - logits[t, target[t]].  One 256-thread
 // workgroup per row; the 50265-wide row is read once (online max / rescaled sum per lane).
@@ -424,6 +478,29 @@ hipError_t ae_launch_graph_mask(const int* ids, const int* meta, const int* span
       return e;
   hipLaunchKernelGGL(graph_mask_kernel, dim3(n), dim3(256), lds, st, ids, meta, spans, edges, L,
                      e_cap, bits);
+  return hipGetLastError();
+}
+hipError_t ae_launch_query_rows(const int* cu, const int* src_col, const int* row0, int n,
+                                int nrows, int T, int* qrow, hipStream_t st) {
+  if (n <= 0 || nrows <= 0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(qrow, 0xff, (size_t)n * nrows * sizeof(int), st);
+  if (e != hipSuccess || T <= 0) return e;
+  hipLaunchKernelGGL(query_rows_kernel, dim3((T + 255) / 256), dim3(256), 0, st, cu, src_col, row0,
+                     n, nrows, T, qrow);
+  return hipGetLastError();
+}
+hipError_t ae_launch_gather_rows(const float* x, const int* qrow, const int* cu, int qper, int nq,
+                                 float* xq, hipStream_t st) {
+  if (nq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((nq + 3) / 4), dim3(256), 0, st, x, qrow, cu, qper,
+                     nq, xq);
+  return hipGetLastError();
+}
+hipError_t ae_launch_scatter_query(const float* xq, const int* qrow, int nq, float* out,
+                                   const int* err, hipStream_t st) {
+  if (nq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(scatter_query_kernel, dim3((nq + 3) / 4), dim3(256), 0, st, xq, qrow, nq, out,
+                     err);
   return hipGetLastError();
 }
 hipError_t ae_launch_scatter_rows(const float* x, const int* cu, const int* src_col, int n,

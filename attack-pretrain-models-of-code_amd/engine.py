@@ -37,7 +37,7 @@ class AeWeightView(ctypes.Structure):
 
 # every symbol include/alert_engine.h declares (checked by tests/test_abi.py)
 EXPORTS = ("ae_create", "ae_destroy", "ae_score", "ae_score_graph", "ae_graph_mask", "ae_encode",
-           "ae_encode_ex", "ae_mlm_topk",
+           "ae_encode_ex", "ae_encode_rows", "ae_mlm_topk",
            "ae_mlm_nll", "ae_splice",
            "ae_topk", "ae_cosine_rank", "ae_set_profiling", "ae_kernel_time", "ae_last_error",
            "ae_version", "ae_source_hash")
@@ -78,6 +78,7 @@ def load_library(path: str | os.PathLike | None = None, tools: bool = False) -> 
     lib.ae_graph_mask.argtypes = [vp, vp, vp, vp, i32, i32, i32, vp, vp]
     lib.ae_encode.argtypes = [vp, vp, vp, i32, i32, vp, vp]
     lib.ae_encode_ex.argtypes = [vp, vp, vp, i32, i32, i32, i32, i32, vp, vp]
+    lib.ae_encode_rows.argtypes = [vp, vp, vp, i32, i32, i32, vp, i32, vp, vp]
     lib.ae_mlm_topk.argtypes = [vp, vp, i32, i32, vp, vp, vp]
     lib.ae_mlm_nll.argtypes = [vp, vp, i32, i32, vp, vp]
     lib.ae_splice.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp]
@@ -236,6 +237,24 @@ class Engine:
         _check(self.lib.ae_encode_ex(self.handle, _ptr(ids), ctypes.c_void_p(lens.ctypes.data),
                                      n, L, 1 if attend_pad else 0, row0, nrows, _ptr(out),
                                      _stream(stream)), "ae_encode_ex", self.lib)
+        return out
+
+    def encode_rows(self, ids, lens: np.ndarray, row0: np.ndarray, nrows: int,
+                    attend_pad: bool = False, stream=None):
+        """Hidden states [n, nrows, hidden] of rows [row0[i], row0[i]+nrows) of sequence i
+        (ae_encode_rows: the last layer runs for those rows only).  Rows past lens[i] stay 0."""
+        import torch
+
+        n, L = ids.shape
+        assert ids.dtype == torch.int32 and ids.is_cuda and ids.is_contiguous()
+        lens = np.ascontiguousarray(lens, dtype=np.int32)
+        row0 = np.ascontiguousarray(row0, dtype=np.int32)
+        assert lens.shape == (n,) and row0.shape == (n,)
+        out = torch.zeros((n, nrows, self.shape.hidden), dtype=torch.float32, device=ids.device)
+        _check(self.lib.ae_encode_rows(self.handle, _ptr(ids), ctypes.c_void_p(lens.ctypes.data),
+                                       n, L, 1 if attend_pad else 0,
+                                       ctypes.c_void_p(row0.ctypes.data), nrows, _ptr(out),
+                                       _stream(stream)), "ae_encode_rows", self.lib)
         return out
 
     def mlm_nll(self, ids, stream=None):

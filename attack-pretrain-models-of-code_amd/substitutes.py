@@ -8,7 +8,8 @@ Per example (one `item` of the jsonl):
   2. ONE masked-LM pass over [CLS] + sub-words[:block-2] + [SEP] with a vocabulary-wide top-60
      (ae_mlm_topk: MFMA logits GEMM + radix-select top-k kernel);
   3. per occurrence of every valid identifier: the 60 candidate rewrites of its sub-word span are
-     re-encoded as ONE device batch (ae_encode_ex, only the span rows are written back) and
+     re-encoded as ONE device batch (ae_encode_rows: the last layer runs for each candidate's own
+     span rows only, and only those are written back) and
      ranked by sum-of-cosine / span length against the original's span (ae_cosine_rank); the top
      30 survive (Python's stable sort on the host, as the reference);
   4. single-sub-word spans decode their 30 ids; multi-sub-word spans take the capped cartesian
@@ -154,17 +155,22 @@ class SubstituteGenerator:
         sims_of = {}
         for c0 in range(0, len(occ) if self.cosine else 0, per_call):
             chunk = occ[c0:c0 + per_call]
-            r_lo = min(k0 for _, _, k0, _ in chunk) + 1
-            r_hi = max(k1e for _, _, _, k1e in chunk) + 1
+            # each candidate sequence is read only at its own occurrence's span (rows k0+1 ..
+            # k1e): one window of the chunk's widest span per sequence, so the last layer runs for
+            # those rows only (ae_encode_rows); a window that would pass L - 1 starts earlier
+            nrows = max(k1e - k0 for _, _, k0, k1e in chunk)
             batch = np.repeat(ids_np[None], K_TOP * len(chunk), axis=0)
+            row0 = np.empty(len(batch), dtype=np.int32)
             for j, (_, _, k0, k1e) in enumerate(chunk):
                 batch[j * K_TOP:(j + 1) * K_TOP, k0 + 1:k1e + 1] = preds[k0:k1e].T
+                row0[j * K_TOP:(j + 1) * K_TOP] = min(k0 + 1, L - nrows)
             bdev = torch.from_numpy(batch).to(dev)
-            hid = self.engine.encode(bdev, np.full((len(batch),), L, np.int32), attend_pad=True,
-                                     row0=r_lo, nrows=r_hi - r_lo)
+            hid = self.engine.encode_rows(bdev, np.full((len(batch),), L, np.int32), row0, nrows,
+                                          attend_pad=True)
             sims = torch.empty((len(chunk), K_TOP), dtype=torch.float32, device=dev)
             for j, (_, _, k0, k1e) in enumerate(chunk):
-                cand = hid[j * K_TOP:(j + 1) * K_TOP, k0 + 1 - r_lo:k1e + 1 - r_lo].contiguous()
+                r = k0 + 1 - int(row0[j * K_TOP])
+                cand = hid[j * K_TOP:(j + 1) * K_TOP, r:r + k1e - k0].contiguous()
                 sims[j] = cosine_rank(orig[k0 + 1:k1e + 1].contiguous(), cand, eps=1e-6)
             sims = sims.cpu().numpy()
             for j, o in enumerate(chunk):

@@ -95,6 +95,30 @@ def log(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+class heartbeat:
+    """`with heartbeat("leg"):` logs every `every` s while a long leg runs (a full-fixture config-4
+    leg runs ~10 min with no other output, and a silent GPU command reads as hung)."""
+
+    def __init__(self, what, every=45.0):
+        import threading
+        self.what, self.every, self.stop = what, every, threading.Event()
+        self.thread = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        t0 = time.time()
+        while not self.stop.wait(self.every):
+            log(f"{self.what}: running, {time.time() - t0:.0f} s")
+
+    def __enter__(self):
+        self.thread.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        self.thread.join()
+        return False
+
+
 def rank_thread_budget(ranks, env=None):
     """Host threads of one rank when `ranks` ranks share this host: the CPUs of this process's
     affinity divided by the ranks, 1..16 (the featurisers' cap, host.gcb_threads), unless the
@@ -1029,8 +1053,9 @@ def main():
         res["microbench"] = microbench_leg(dev, args.precision, args.steps, args.warmup, world)
     if args.attack_examples > 0:
         log("config-2 attack leg")
-        res["attack"] = attack_leg(dev, args.attack_examples, args.attack_deadline,
-                                   args.attack_inflight, rank, world, args.precision)
+        with heartbeat("config-2 attack leg"):
+            res["attack"] = attack_leg(dev, args.attack_examples, args.attack_deadline,
+                                       args.attack_inflight, rank, world, args.precision)
     if rank == 0 and world == 1 and not args.no_config1:
         log("config-1 leg")
         res["config1"] = config1_leg(dev, args.precision, threads,
@@ -1040,15 +1065,18 @@ def main():
         res["substitutes"] = subs_leg(dev, args.subs_seconds, rank, world, args.precision)
     if args.aa_examples > 0:
         log("authorship leg")
-        res["authorship"] = aa_leg(dev, args.aa_examples, args.aa_gcb_examples, rank, world,
-                                   args.precision)
+        with heartbeat("authorship leg"):
+            res["authorship"] = aa_leg(dev, args.aa_examples, args.aa_gcb_examples, rank, world,
+                                       args.precision)
     if args.clone_examples > 0:
         log("config-4 leg (GraphCodeBERT clone)")
-        res["clone_gcb"] = clone_leg(dev, args.clone_examples, rank, world, args.precision)
+        with heartbeat("config-4 leg"):
+            res["clone_gcb"] = clone_leg(dev, args.clone_examples, rank, world, args.precision)
     if args.mhm_examples > 0:
         log("MHM-NS leg")
-        res["mhm"] = mhm_leg(dev, args.mhm_examples, args.mhm_seq_examples, rank, world,
-                             args.precision)
+        with heartbeat("MHM-NS leg"):
+            res["mhm"] = mhm_leg(dev, args.mhm_examples, args.mhm_seq_examples, rank, world,
+                                 args.precision)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if dist is not None:

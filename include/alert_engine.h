@@ -28,7 +28,8 @@
  *   ae_mlm_topk   <- codebert_mlm(input_ids)[0] + torch.topk(., 60, -1)
  *                    (CodeXGLUE/Defect-detection/preprocess/get_substitutes.py:62-63)
  *   ae_encode     <- codebert_mlm.roberta(ids)[0] (get_substitutes.py:73,105); ae_encode_ex adds
- *                    the no-attention_mask call form and a row window (the cosine span)
+ *                    the no-attention_mask call form and a row window (the cosine span);
+ *                    ae_encode_rows a window per sequence (get_substitutes.py:98-108)
  *   ae_mlm_nll    <- mlm_model(all_substitutes)[0] + CrossEntropyLoss(reduction='none')
  *                    (utils.py:237-239 get_bpe_substitues)
  *   ae_cosine_rank<- CosineSimilarity(dim=1) summed over the sub-word span / L_sub
@@ -152,6 +153,20 @@ int ae_encode(ae_engine *eng, const int32_t *ids, const int32_t *lens, int32_t n
 #define AE_ENC_ATTEND_PAD 1
 int ae_encode_ex(ae_engine *eng, const int32_t *ids, const int32_t *lens, int32_t n, int32_t L,
                  int32_t flags, int32_t row0, int32_t nrows, float *hidden_out, void *stream);
+
+/* ae_encode_ex with a row window PER SEQUENCE, for the cosine naturalness filter's re-encodes
+ * (get_substitutes.py:98-108: each candidate sequence is read only at the span of the occurrence
+ * it substitutes, orig_embeddings / new_embeddings[0][keys[0]+1:keys[1]+1]).  The last layer runs
+ * for the window rows only (its attention with W_k absorbed into each query and W_v applied to the
+ * p-weighted row sum, cls_attention.hip; O-projection / FFN for nrows rows per sequence), so a
+ * call costs 11 full layers plus O(n·nrows) rows, not 12 full layers.
+ *   row0      HOST int32 [n]: sequence i's window is columns [row0[i], row0[i] + nrows)
+ *             (0 <= row0[i], row0[i] + nrows <= L)
+ *   hidden_out device float [n, nrows, hidden]; a column past lens[i] (or a pad id the call form
+ *             drops) is left untouched, as in ae_encode_ex.  Same flags. */
+int ae_encode_rows(ae_engine *eng, const int32_t *ids, const int32_t *lens, int32_t n, int32_t L,
+                   int32_t flags, const int32_t *row0, int32_t nrows, float *hidden_out,
+                   void *stream);
 
 /* Per-token masked-LM negative log-likelihood of n full rows (no attention_mask: every id is
  * attended):  nll_out[i, t] = logsumexp(logits[i, t, :]) - logits[i, t, ids[i, t]]

@@ -140,6 +140,8 @@ def test_argument_errors_before_any_device_call():
     assert lib.ae_score_graph(None, p, p, None, None, 4, 640, fp, None) == EINVAL
     assert "pos and mask_bits" in _err(lib)
     assert lib.ae_encode_ex(None, p, p, 4, 512, 0, 0, 1, fp, None) == EINVAL
+    assert lib.ae_encode_rows(None, p, p, 4, 512, 0, p, 1, fp, None) == EINVAL
+    assert "null engine" in _err(lib)
     assert lib.ae_set_profiling(None, 0, 1) == EINVAL
     # standalone kernels: shapes checked before launch
     assert lib.ae_topk(fp, 1, 10, 0, fp, p, None) == EINVAL and "bad shape" in _err(lib)

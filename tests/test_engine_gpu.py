@@ -352,50 +352,101 @@ def test_encoder_forms_bit_identical(gpu, precision):
         e.close()
 
 
-def test_folded_layernorm_robust_to_row_mean_offsets(gpu):
+OUTLIER_DIMS = np.array([77, 300, 588])
+OUTLIER_SHIFT = np.array([25.0, -40.0, 30.0], dtype=np.float32)
+
+
+def _fold_case_sd(case):
+    """Synthetic weights for the folded-LayerNorm robustness test (seeded, deterministic).
+    base: LayerNorm gains from 0.5..2 (so s = rowsum(W·diag(g)) is far from 0), every encoder /
+    head weight row centred (W·1 = 0: a common row offset stays in the residual stream instead of
+    swamping the tokens' signal), the classifier out_proj ~ N(0, 1) so the logits spread by about
+    one unit across rows (its bias is centred per case by the test).  shifted: every LayerNorm bias
+    +4 and the O-projection / FFN2 biases +3, a row mean of about 7 against a std of 1-2 at every
+    folded GEMM.  outlier: RoBERTa-style outlier features — three hidden dimensions carry
+    +25 / -40 / +30 in every LayerNorm bias, so the residual stream holds |v| of 20-60 there (the
+    rows' variance is dominated by them) while the other 765 dimensions stay O(1)."""
+    rng = np.random.default_rng(9)
+    sd = {k: v.copy() for k, v in synthetic_sd(9, "sigmoid1", out_std=1.0).items()}
+    for k in sd:
+        if k.endswith("LayerNorm.weight"):
+            sd[k] = rng.uniform(0.5, 2.0, sd[k].shape).astype(np.float32)
+        elif (k.startswith("encoder.") or k.startswith("classifier.")) and sd[k].ndim == 2:
+            sd[k] -= sd[k].mean(1, keepdims=True)
+    for k in sd:
+        if case == "shifted":
+            if k.endswith("LayerNorm.bias") and not k.startswith("lm_head"):
+                sd[k] += 4.0
+            elif k.startswith("encoder.") and k.endswith("output.dense.bias"):  # O-proj and FFN2
+                sd[k] += 3.0
+        elif case == "outlier":
+            if k.endswith("LayerNorm.bias") and not k.startswith("lm_head"):
+                sd[k][OUTLIER_DIMS] += OUTLIER_SHIFT
+    return sd
+
+
+def _host_logits(sd, h):
+    """The sequence-classification head (dense -> tanh -> out_proj, model.py:25 via
+    RobertaClassificationHead) in float64 on the host, from the CLS rows h[:, 0]."""
+    x = h[:, 0, :].astype(np.float64)
+    x = np.tanh(x @ sd["classifier.dense.weight"].astype(np.float64).T +
+                sd["classifier.dense.bias"].astype(np.float64))
+    return (x @ sd["classifier.out_proj.weight"].astype(np.float64).T)[:, 0]
+
+
+@pytest.mark.parametrize("precision", ["f32x3", "bf16"])
+def test_folded_layernorm_robust_to_row_mean_offsets(gpu, precision):
     """The split modes fold each LayerNorm into the next GEMM: it multiplies the PRE-LayerNorm
-    rows and subtracts mean · s in the epilogue, so a residual stream whose rows carry a large
-    common offset (|mean| >> std) is where that cancellation could lose precision.  Synthetic
-    weights whose residual rows are shifted — every LayerNorm bias +4, the O-projection / FFN2
-    biases +3: a row mean of about 7 against a std of 1-2 at every folded GEMM — with LayerNorm
-    gains drawn from 0.5..2 (so s = rowsum(W·diag(g)) is far from 0) and every encoder / head
-    weight row centred (W·1 = 0, so the offsets stay in the residual stream instead of swamping
-    the tokens' signal).  The last layer's hidden states of f32x3 against the exact-fp32 mode
-    (which normalises explicitly): the relative error with the offsets stays within 3x of the same
-    weights' error without them, and the probabilities within the 1e-4 north-star tolerance."""
+    rows (split into bf16 planes) and subtracts mean · s in the epilogue, so the planes' rounding
+    error scales with |v| instead of |v - mean|.  Three weight sets (_fold_case_sd): base, rows
+    shifted to a mean of about 7σ at every folded GEMM, and RoBERTa-style outlier features (three
+    dimensions at |v| 20-60).  Against the exact-fp32 mode (which normalises explicitly), per case:
+    (i) the head's pre-sigmoid logits, computed in float64 from each mode's CLS rows with the
+    out_proj bias centred so they spread over about ±1.5 (a non-saturation guard: logit std across
+    rows >= 0.5) — |Δlogit| <= 4e-4 in f32x3, which bounds |Δp| by 1e-4 at any logit, 8e-2 in bf16
+    (its stated 2e-2 probability tolerance); (ii) the engine's own probabilities at those logits,
+    1e-4 / 2e-2; (iii) the hidden-state error per row against that row's own spread
+    (max_j |Δh_ij| / std_j h_ij over the real tokens), which in f32x3 stays within 4x of the base
+    weights' (bf16 within 8x) — the printed numbers are committed in profiles/."""
     from apmc_amd.engine import Engine
     rng = np.random.default_rng(9)
-    base = {k: v.copy() for k, v in synthetic_sd(9, "sigmoid1", out_std=0.05).items()}
-    for k in base:
-        if k.endswith("LayerNorm.weight"):
-            base[k] = rng.uniform(0.5, 2.0, base[k].shape).astype(np.float32)
-        elif (k.startswith("encoder.") or k.startswith("classifier.")) and base[k].ndim == 2:
-            base[k] -= base[k].mean(1, keepdims=True)
-    shifted = {k: v.copy() for k, v in base.items()}
-    for k in shifted:
-        if k.endswith("LayerNorm.bias") and not k.startswith("lm_head"):
-            shifted[k] += 4.0
-        elif k.startswith("encoder.") and k.endswith("output.dense.bias"):  # O-proj and FFN2
-            shifted[k] += 3.0
     n, L = 24, 512
     ids = _rand_ids(rng, n, L, rng.integers(40, L + 1, n))
     lens = (ids != 1).sum(1).astype(np.int32)
     dev_ids = torch.from_numpy(ids).cuda()
-    rel = {}
-    for name, sd in (("base", base), ("shifted", shifted)):
+    real = ids != 1
+    logit_tol, prob_tol = (4e-4, PROB_TOL) if precision == "f32x3" else (8e-2, 2e-2)
+    rowrel, res = {}, {}
+    for case in ("base", "shifted", "outlier"):
+        sd = _fold_case_sd(case)
         e32 = Engine(sd, head="sigmoid1", precision="fp32")
-        e3 = Engine(sd, head="sigmoid1", precision="f32x3")
-        h32, h3 = e32.encode(dev_ids, lens), e3.encode(dev_ids, lens)
-        torch.cuda.synchronize()
-        mask = torch.from_numpy(ids != 1).cuda()[..., None]
-        rel[name] = float(((h3 - h32).abs() * mask).max() / (h32.abs() * mask).max())
-        if name == "shifted":
-            p32, p3 = _score(e32, ids), _score(e3, ids)
-            np.testing.assert_allclose(p3, p32, atol=PROB_TOL, rtol=0)
+        h32 = e32.encode(dev_ids, lens).cpu().numpy()
         e32.close()
-        e3.close()
-    print(f"hidden-state relative error: base {rel['base']:.2e}, shifted {rel['shifted']:.2e}")
-    assert rel["shifted"] <= 3 * rel["base"] + 1e-7, rel
+        z = _host_logits(sd, h32)
+        sd["classifier.out_proj.bias"] = np.array([-z.mean()], dtype=np.float32)
+        e32 = Engine(sd, head="sigmoid1", precision="fp32")
+        ex = Engine(sd, head="sigmoid1", precision=precision)
+        hx = ex.encode(dev_ids, lens).cpu().numpy()
+        z32, zx = _host_logits(sd, h32) - z.mean(), _host_logits(sd, hx) - z.mean()
+        p32, px = _score(e32, ids), _score(ex, ids)
+        e32.close()
+        ex.close()
+        d = np.abs(hx - h32).max(-1) / h32.std(-1)
+        rowrel[case] = float(d[real].max())
+        vmax = float(np.abs(h32[real]).max())
+        res[case] = (float(z32.std()), float(np.abs(zx - z32).max()),
+                     float(np.abs(px - p32).max()), vmax)
+        print(f"{precision} {case}: logit std {z32.std():.3f} range [{z32.min():.3f}, "
+              f"{z32.max():.3f}], max |dlogit| {np.abs(zx - z32).max():.2e}, max |dp| "
+              f"{np.abs(px - p32).max():.2e}, per-row rel {rowrel[case]:.2e}, max |h| {vmax:.1f}")
+    for case, (zstd, dz, dp, vmax) in res.items():
+        assert zstd >= 0.5, (case, zstd)
+        assert dz <= logit_tol and dp <= prob_tol, (case, dz, dp)
+        if case == "outlier":
+            assert vmax >= 20.0, vmax
+    k = 4 if precision == "f32x3" else 8
+    assert rowrel["shifted"] <= k * rowrel["base"] and rowrel["outlier"] <= k * rowrel["base"], \
+        rowrel
 
 
 def test_bench_size_batch_properties(gpu):

@@ -126,6 +126,43 @@ def test_gemm_packed_matches_split_products(gpu, M, N, K, np_, epi, bn):
     assert (err <= tol).all(), float((err - tol).max())
 
 
+def test_gemm_packed_gelu_propagates_nan(gpu):
+    """The FFN1 GELU epilogue (gelu_exp2_pairs) passes a NaN pre-activation through as NaN and
+    an infinite one as non-finite — never as a finite value (an upstream overflow must not turn
+    into finite scores; its max(x, 0) is the IEEE maximum, not maxnum).  Every other element
+    keeps the float64 tolerance of test_gemm_packed_matches_split_products."""
+    lib = _lib()
+    M, N, K, np_ = 300, 512, 128, 2
+    g = torch.Generator().manual_seed(11)
+    A = torch.randn(M, K, generator=g) * 0.7
+    W = torch.randn(N, K, generator=g) * 0.05
+    bias = torch.randn(N, generator=g)
+    A[5, 17] = float("nan")  # row 5: every pre-activation NaN
+    bias[7] = float("inf")  # column 7: +inf pre-activations
+    Ah, Al = _split(A)
+    Wh, Wl = _split(W)
+    ref = Ah.double() @ Wh.double().T + Ah.double() @ Wl.double().T + Al.double() @ Wh.double().T
+    ref = torch.nn.functional.gelu(ref + bias.double())
+    scale = A.abs().double().nan_to_num(0) @ W.abs().double().T
+    C = torch.full((M, N), float("nan"), device="cuda")
+    Cp = torch.zeros((M, np_ * N), dtype=torch.bfloat16, device="cuda")
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert lib.ae_bench_gemm_packed(_p(_pack(Ah, Al, np_).cuda()), _p(_pack(Wh, Wl, np_).cuda()),
+                                    _p(bias.cuda()), _p(None), _p(C), _p(Cp), M, N, K, 1, np_,
+                                    512, 0, st) == 0
+    torch.cuda.synchronize()
+    planes = Cp.cpu().reshape(M, N // 32, 2, 32).double()
+    hi = planes[:, :, 0].reshape(M, N)
+    got = _unpack(Cp.cpu(), np_, N)
+    assert torch.isnan(hi[5]).all() and torch.isnan(got[5]).all()
+    assert not torch.isfinite(hi[:, 7]).any() and not torch.isfinite(got[:, 7]).any()
+    keep = torch.ones(M, N, dtype=torch.bool)
+    keep[5], keep[:, 7] = False, False
+    err = (got - ref).abs()[keep]
+    tol = (1e-5 * scale + 2e-5 * ref.abs() + 1e-6)[keep]
+    assert (err <= tol).all(), float((err - tol).max())
+
+
 def _attn_ref(qkv, cu, n, mask=None, L=0, q_rows=None):
     """float64 attention per (sequence, head): softmax(Q·K^T/8 (+ finfo.min where the bit-packed
     mask excludes a key)) · V over each sequence's keys; [T, 768]."""
@@ -318,9 +355,10 @@ def test_attention_pp_restructured_loops_bit_identical(gpu, case):
 def _fold_lib():
     lib = _lib()
     vp, i32, f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_float
-    lib.ae_launch_gemm_packed_fold.argtypes = [vp] * 5 + [f32, vp] + [i32] * 5 + [vp]
+    lib.ae_launch_gemm_packed_fold.argtypes = [vp] * 5 + [f32, vp] + [i32] * 5 + [vp, vp]
     lib.ae_launch_gemm_packed_fold.restype = ctypes.c_int
-    lib.ae_launch_gemm_packed_res_stats.argtypes = [vp] * 7 + [f32] + [vp] * 3 + [i32] * 4 + [vp]
+    lib.ae_launch_gemm_packed_res_stats.argtypes = [vp] * 7 + [f32] + [vp] * 3 + [i32] * 4 + \
+        [vp, vp]
     lib.ae_launch_gemm_packed_res_stats.restype = ctypes.c_int
     return lib
 
@@ -351,13 +389,16 @@ def _ln64(v, gamma, beta, eps=1e-5):
     return (v - mu) / torch.sqrt(var + eps) * gamma.double() + beta.double(), var
 
 
-@pytest.mark.parametrize("M,K,np_", [(300, 768, 2), (4097, 768, 2), (37, 3072, 2), (1000, 768, 1)])
-def test_gemm_packed_res_stats_matches_f64(gpu, M, K, np_):
+@pytest.mark.parametrize("M,K,np_,shift", [(300, 768, 2, 0), (4097, 768, 2, 1), (37, 3072, 2, 1),
+                                            (1000, 768, 1, 0), (1000, 768, 1, 1)])
+def test_gemm_packed_res_stats_matches_f64(gpu, M, K, np_, shift):
     """ae_launch_gemm_packed_res_stats (256 x 192 kernel): v = A·W^T + bias + r as f32 and packed
     planes plus the (mean, M2) of every row over its 4 192-column tiles, first with a plain
     residual (PK_EPI_RES_STATS: layer 0), then with the residual the previous pre-LayerNorm rows
     normalised on the fly from the statistics the first launch wrote (PK_EPI_RES_STATS_LN).
-    Both in place (R = C), as the engine runs them; against float64 of the split products."""
+    Both in place (R = C), as the engine runs them; against float64 of the split products.  With
+    shift, the planes hold v - kappa (the plane shift; kappa = bias + beta, as the engine passes)
+    while f32 v and its statistics stay those of v."""
     lib = _fold_lib()
     N = 768
     g = torch.Generator().manual_seed(7 * M + K)
@@ -380,10 +421,11 @@ def test_gemm_packed_res_stats_matches_f64(gpu, M, K, np_):
             r = R0.double()
         else:
             r, _ = _ln64(prev, gamma, beta)
+        kap = (bias + (beta if rst is not None else 0.5)) if shift else None
         rc = lib.ae_launch_gemm_packed_res_stats(
             _p(dA), _p(dW), _p(db), _p(v), _p(rst), _p(dg if rst is not None else None),
             _p(dbeta if rst is not None else None), 1e-5, _p(v), _p(vp), _p(out_st), M, N, K,
-            np_, st)
+            np_, _p(kap.cuda() if shift else None), st)
         assert rc == 0
         torch.cuda.synchronize()
         ref = _split_prod(A, W, np_) + bias.double() + r
@@ -395,7 +437,8 @@ def test_gemm_packed_res_stats_matches_f64(gpu, M, K, np_):
         assert ((got - ref).abs() <= tol).all(), (it, float(((got - ref).abs() - tol).max()))
         planes = _unpack(vp.cpu(), np_, N)
         rel = 2e-5 if np_ == 2 else 5e-3
-        assert ((planes - got).abs() <= rel * got.abs() + 1e-7).all(), it
+        want = got - kap.double() if shift else got
+        assert ((planes - want).abs() <= rel * want.abs() + 1e-7).all(), it
         # the tile statistics of the f32 output, against float64 of the same values
         ws = out_st.cpu().view(torch.float32).reshape(M, 4, 2).double()
         t = got.reshape(M, 4, 192)
@@ -406,21 +449,29 @@ def test_gemm_packed_res_stats_matches_f64(gpu, M, K, np_):
         prev = got
 
 
-@pytest.mark.parametrize("M,N,np_,gelu", [(300, 2304, 2, 0), (4100, 3072, 2, 1), (37, 3072, 2, 1),
-                                          (1000, 2304, 1, 0), (600, 3072, 1, 1)])
-def test_gemm_packed_fold_matches_f64(gpu, M, N, np_, gelu):
+@pytest.mark.parametrize("M,N,np_,gelu,shift", [
+    (300, 2304, 2, 0, 0), (4100, 3072, 2, 1, 0), (37, 3072, 2, 1, 0), (1000, 2304, 1, 0, 0),
+    (600, 3072, 1, 1, 0), (300, 2304, 2, 0, 1), (4100, 3072, 2, 1, 1), (600, 3072, 1, 1, 1)])
+def test_gemm_packed_fold_matches_f64(gpu, M, N, np_, gelu, shift):
     """ae_launch_gemm_packed_fold (256 x 256 kernel, PK_EPI_BIAS_FOLD / PK_EPI_GELU_FOLD): the
     QKV / FFN1 GEMM over PRE-LayerNorm rows v with the LayerNorm folded in,
         y = rstd · (v·W'^T - mean · s) + bias',  W' = W·diag(gamma), s = rowsums(W'),
         bias' = bias + W·beta                                    (GELU'd for FFN1)
     must equal LayerNorm(v)·W^T + bias in float64 — rows with a mean offset and varied scale, so
-    the mean · s cancellation is exercised.  Packed-plane output."""
+    the mean · s cancellation is exercised.  Packed-plane output.  With shift (the plane shift):
+    v carries per-column constants kappa (|kappa| ~ 3, outlier columns at 30-40), the A planes
+    hold v - kappa and the accumulators start at kc = kappa·W'^T — the split error then scales
+    with |v - kappa|, which the tolerance states."""
     lib = _fold_lib()
     K = 768
     g = torch.Generator().manual_seed(3 * M + N + gelu)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     v = torch.randn(M, K, generator=g) * (0.5 + 2.0 * torch.rand(M, 1, generator=g)) + \
         3.0 * torch.randn(M, 1, generator=g)
+    kap = 3.0 * torch.randn(K, generator=g)
+    kap[[77, 300, 588]] = torch.tensor([30.0, -40.0, 35.0])
+    if shift:
+        v = v + kap
     gamma = 1.0 + 0.1 * torch.randn(K, generator=g)
     beta = 0.1 * torch.randn(K, generator=g)
     W = torch.randn(N, K, generator=g) * 0.05
@@ -429,13 +480,15 @@ def test_gemm_packed_fold_matches_f64(gpu, M, N, np_, gelu):
     Wh, Wl = _split(Wf)
     s = (Wh.double() + (Wl.double() if np_ == 2 else 0.0)).sum(1).float()
     bf = (bias.double() + W.double() @ beta.double()).float()
-    dv = _pack(*_split(v), np_).cuda()
+    dv = _pack(*_split(v - kap if shift else v), np_).cuda()
     dW = _pack(Wh, Wl, np_).cuda()
     ds, dbf = s.cuda(), bf.cuda()
+    held = Wh.double() + (Wl.double() if np_ == 2 else 0.0)
+    dkc = (held @ kap.double()).float().cuda() if shift else None
     dst = _tile_stats(v).cuda()
     out = torch.zeros((M, np_ * N), dtype=torch.bfloat16, device="cuda")
     rc = lib.ae_launch_gemm_packed_fold(_p(dv), _p(dW), _p(dbf), _p(ds), _p(dst), 1e-5, _p(out),
-                                        M, N, K, gelu, np_, st)
+                                        M, N, K, gelu, np_, _p(dkc), st)
     assert rc == 0
     torch.cuda.synchronize()
     x, var = _ln64(v, gamma, beta)
@@ -443,8 +496,10 @@ def test_gemm_packed_fold_matches_f64(gpu, M, N, np_, gelu):
     if gelu:
         ref = 0.5 * ref * (1.0 + torch.erf(ref / np.sqrt(2.0)))
     got = _unpack(out.cpu(), np_, N)
-    # the split products' error on v (not on LN(v)), times rstd: |v| includes the mean offset
-    scale = (v.abs().double() @ Wf.abs().double().T) / torch.sqrt(var + 1e-5)
+    # the split products' error on the planes' rows (v, or v - kappa under the plane shift), times
+    # rstd: |v| includes the mean offset
+    va = (v - kap if shift else v).abs().double()
+    scale = (va @ Wf.abs().double().T) / torch.sqrt(var + 1e-5)
     rel = 1e-5 if np_ == 2 else 8e-3
     tol = rel * scale + (2e-5 if np_ == 2 else 1e-2) * ref.abs() + 2e-6
     assert torch.isfinite(got).all()

@@ -348,3 +348,49 @@ def test_cosine_substitutes_f32x3_match_fp32(gpu):
     assert excused <= compared, (compared, excused)
     e32.close()
     e3.close()
+
+
+@pytest.mark.parametrize("precision", ["fp32", "f32x3"])
+def test_encode_rows_matches_full_last_layer(gpu, precision):
+    """ae_encode_rows (the last layer for each sequence's own row window only: attention with W_k
+    absorbed into each query row and W_v applied to the p-weighted row sum, then O-projection /
+    FFN for those rows; get_substitutes.py:98-108 reads each candidate at its own span) against
+    ae_encode_ex's full last layer over every row, 12 layers: both call forms (attend-pad with
+    every column kept, and the masked form with literal pad ids inside rows, which the compaction
+    drops), ragged lens, windows at the row's start and end, and a window running past lens
+    (those columns stay untouched).  Within 2e-5 of the full path (fp32), 4e-5 (f32x3, whose full
+    last layer runs split-bf16 products where the window path's attention runs exact f32)."""
+    from apmc_amd.engine import Engine
+    from apmc_amd.weights import synthetic_state_dict
+    sd = synthetic_state_dict(seed=3, head="none", with_mlm=True)
+    eng = Engine(sd, head="none", with_mlm=True, precision=precision)
+    rng = np.random.default_rng(17)
+    n, L, nrows = 40, 320, 3
+    tol = 2e-5 if precision == "fp32" else 4e-5
+    for attend_pad in (True, False):
+        ids = rng.integers(4, 50264, size=(n, L)).astype(np.int32)
+        lens = rng.integers(nrows + 2, L + 1, size=n).astype(np.int32)
+        lens[:3], lens[3] = L, L - 10
+        for i in range(n):
+            ids[i, 0], ids[i, lens[i] - 1], ids[i, lens[i]:] = 0, 2, 1
+        if not attend_pad:  # literal pads inside rows: not attended, dropped by the compaction
+            for i in range(0, n, 3):
+                ids[i, rng.integers(1, lens[i] - 1, size=2)] = 1
+            lens_arg = (ids != 1).sum(1).astype(np.int32)
+        else:
+            lens_arg = lens
+        row0 = rng.integers(0, L - nrows + 1, size=n).astype(np.int32)
+        row0 = np.minimum(row0, np.maximum(lens - nrows, 0)).astype(np.int32)
+        row0[0], row0[1], row0[2] = 0, L - nrows, L - 2 - nrows  # start, end of a full row
+        row0[3] = lens[3] - 1  # past lens: the last column written, the rest untouched
+        dev = torch.from_numpy(ids).cuda()
+        full = eng.encode(dev, lens_arg, attend_pad=attend_pad).cpu().numpy()
+        win = eng.encode_rows(dev, lens_arg, row0, nrows, attend_pad=attend_pad).cpu().numpy()
+        want = np.stack([full[i, row0[i]:row0[i] + nrows] for i in range(n)])
+        err = np.abs(win - want).max()
+        print(f"{precision} attend_pad={attend_pad}: max |rows - full| {err:.2e}")
+        assert err <= tol, err
+        # a column past lens, or a dropped pad column, is left untouched (zeros, like encode_ex)
+        assert not np.abs(win[3, 1:]).any()
+        assert np.isfinite(win).all()
+    eng.close()

@@ -34,8 +34,9 @@ def main():
     lib = load_library(args.lib)
     vp, i32, f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_float
     lib.ae_launch_gemm_packed.argtypes = [vp] * 6 + [i32] * 5 + [vp]
-    lib.ae_launch_gemm_packed_fold.argtypes = [vp] * 5 + [f32, vp] + [i32] * 5 + [vp]
-    lib.ae_launch_gemm_packed_res_stats.argtypes = [vp] * 7 + [f32] + [vp] * 3 + [i32] * 4 + [vp]
+    lib.ae_launch_gemm_packed_fold.argtypes = [vp] * 5 + [f32, vp] + [i32] * 5 + [vp, vp]
+    lib.ae_launch_gemm_packed_res_stats.argtypes = [vp] * 7 + [f32] + [vp] * 3 + [i32] * 4 + \
+        [vp, vp]
     dev = torch.device("cuda:0")
     st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     M, H, F = args.m, 768, 3072
@@ -54,6 +55,9 @@ def main():
     bias = torch.randn(F, device=dev, generator=g) * 0.1
     s = torch.randn(F, device=dev, generator=g)
     gam, bet = torch.ones(H, device=dev), torch.zeros(H, device=dev)
+    # the plane shift as the engine runs it: kappa for the producers, kc for the consumers
+    kap = torch.randn(H, device=dev, generator=g) * 0.1
+    kc = torch.randn(F, device=dev, generator=g) * 0.1
     v = torch.randn(M, H, device=dev, generator=g)
     rv = torch.randn(M, H, device=dev, generator=g)
     stats = torch.zeros(M * 4, 2, device=dev)
@@ -64,13 +68,13 @@ def main():
     vp_ = torch.zeros(M, 2 * H, dtype=torch.bfloat16, device=dev)
     calls = {
         "qkv_plain": lambda: lib.ae_launch_gemm_packed(p(x), p(w["qkv"]), p(bias), None, None, p(outp), M, 3 * H, H, 4, 2, st),
-        "qkv_fold": lambda: lib.ae_launch_gemm_packed_fold(p(x), p(w["qkv"]), p(bias), p(s), p(stats), 1e-5, p(outp), M, 3 * H, H, 0, 2, st),
+        "qkv_fold": lambda: lib.ae_launch_gemm_packed_fold(p(x), p(w["qkv"]), p(bias), p(s), p(stats), 1e-5, p(outp), M, 3 * H, H, 0, 2, p(kc), st),
         "ffn1_plain": lambda: lib.ae_launch_gemm_packed(p(x), p(w["ffn1"]), p(bias), None, None, p(outp), M, F, H, 1, 2, st),
-        "ffn1_fold": lambda: lib.ae_launch_gemm_packed_fold(p(x), p(w["ffn1"]), p(bias), p(s), p(stats), 1e-5, p(outp), M, F, H, 1, 2, st),
+        "ffn1_fold": lambda: lib.ae_launch_gemm_packed_fold(p(x), p(w["ffn1"]), p(bias), p(s), p(stats), 1e-5, p(outp), M, F, H, 1, 2, p(kc), st),
         "oproj_plain": lambda: lib.ae_launch_gemm_packed(p(ctx), p(w["oproj"]), p(bias), p(rv), p(v), None, M, H, H, 2, 2, st),
-        "oproj_stats": lambda: lib.ae_launch_gemm_packed_res_stats(p(ctx), p(w["oproj"]), p(bias), p(rv), p(stats), p(gam), p(bet), 1e-5, p(v), p(vp_), p(ostats), M, H, H, 2, st),
+        "oproj_stats": lambda: lib.ae_launch_gemm_packed_res_stats(p(ctx), p(w["oproj"]), p(bias), p(rv), p(stats), p(gam), p(bet), 1e-5, p(v), p(vp_), p(ostats), M, H, H, 2, p(kap), st),
         "ffn2_plain": lambda: lib.ae_launch_gemm_packed(p(h), p(w["ffn2"]), p(bias), p(rv), p(v), None, M, H, F, 2, 2, st),
-        "ffn2_stats": lambda: lib.ae_launch_gemm_packed_res_stats(p(h), p(w["ffn2"]), p(bias), p(rv), p(stats), p(gam), p(bet), 1e-5, p(v), p(vp_), p(ostats), M, H, F, 2, st),
+        "ffn2_stats": lambda: lib.ae_launch_gemm_packed_res_stats(p(h), p(w["ffn2"]), p(bias), p(rv), p(stats), p(gam), p(bet), 1e-5, p(v), p(vp_), p(ostats), M, H, F, 2, p(kap), st),
     }
     ts = {k: [] for k in calls}
     for k, c in calls.items():
