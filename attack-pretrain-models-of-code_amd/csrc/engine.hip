@@ -70,6 +70,8 @@ long ae_cls_attention_part_floats(long, int, int);
 hipError_t ae_launch_cls_attention(const float*, const float*, const float*, const float*,
                                    const float*, const int*, int, int, int, const uint32_t*, int,
                                    float, float*, float*, float*, float*, int*, hipStream_t);
+hipError_t ae_launch_layernorm_stats(const float*, const uint64_t*, const float*, const float*,
+                                     float, int, float*, hipStream_t);
 hipError_t ae_launch_query_rows(const int*, const int*, const int*, int, int, int, int*,
                                 hipStream_t);
 hipError_t ae_launch_gather_rows(const float*, const int*, const int*, int, int, float*,
@@ -537,7 +539,9 @@ int layer_rows(ae_engine* e, int li, int64_t t0, int M, int s0, int ns, int max_
                                          M, H, F, np, w.kap_f, st));
   }
   if (int rc = done()) return rc;
-  if (last) HIPC(ae_launch_layernorm(v, w.ln2g, w.ln2b, eps, M, e->x + t0 * H, nullptr, 0, st));
+  // the last full layer's output x = LN2(v) for the CLS path / MLM head / encode outputs, from
+  // FFN2's tile statistics in the folded consumers' merge order (the same bits they see)
+  if (last) HIPC(ae_launch_layernorm_stats(v, sa, w.ln2g, w.ln2b, eps, M, e->x + t0 * H, st));
   return AE_OK;
 }
 

@@ -1241,6 +1241,43 @@ extern "C" hipError_t ae_launch_gemm_packed_fold(const unsigned short* A, const 
               : pp_launch<1, PK_EPI_BIAS_FOLD, 0>(a, w, bias, nullptr, nullptr, cp, M, N, K, PK_GROUP_M, st, fold);
 }
 
+// LayerNorm of M pre-LayerNorm rows v from their [M][4] tile statistics (row_norm's merge order)
+// with the expression the PK_EPI_RES_STATS_LN residual uses, so the last full layer's output x (the
+// CLS path, MLM head and encode outputs) carries the same bits as every folded consumer's view of
+// the same rows.  One wave per row.
+__global__ __launch_bounds__(256) void layernorm_stats_kernel(const float* __restrict__ v,
+                                                              const uint64_t* __restrict__ stats,
+                                                              const float* __restrict__ g,
+                                                              const float* __restrict__ b,
+                                                              float eps, int M,
+                                                              float* __restrict__ out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= M) return;
+  float mu, rs;
+  row_norm(stats + (size_t)row * 4, eps, mu, rs);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const int col = c * 256 + lane * 4;
+    const floatx4 x = *reinterpret_cast<const floatx4*>(v + (size_t)row * 768 + col);
+    const floatx4 gg = *reinterpret_cast<const floatx4*>(g + col);
+    const floatx4 bb = *reinterpret_cast<const floatx4*>(b + col);
+    floatx4 y;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) y[i] = (x[i] - mu) * rs * gg[i] + bb[i];
+    *reinterpret_cast<floatx4*>(out + (size_t)row * 768 + col) = y;
+  }
+}
+
+extern "C" hipError_t ae_launch_layernorm_stats(const float* v, const uint64_t* stats,
+                                                const float* g, const float* b, float eps, int M,
+                                                float* out, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  hipLaunchKernelGGL(layernorm_stats_kernel, dim3((M + 3) / 4), dim3(256), 0, st, v, stats, g, b,
+                     eps, M, out);
+  return hipGetLastError();
+}
+
 // v = A·W^T + bias + r over rows of N = 768 (the O-projection / FFN2), written as f32 C and packed
 // planes Cp of v - shift (shift null: of v; the plane shift, FoldArgs), with the (mean, M2) of every
 // row of v over each of its 4 192-column tiles into stats ([M][4] 8-B words).  r = R as it is when rstats is null, else r = LN(R) with R's own tile

@@ -407,7 +407,7 @@ def _mhm_record(index, code, task, res, label, queries, dt_min, recorder, last_c
 
 def run_mhm_attack(model, codes, subs, labels, args: AttackArgs, indices=None, tok=None,
                    n_candi=30, max_iter=None, prob_threshold=1, original=False, max_inflight=1,
-                   queue=None):
+                   queue=None, last_code=None):
     """mhm_attack.py:160-236 (MHM-NS; `original` = MHM with the random-token candidates) for
     every task: devign / authorship / clone (CodeBERT) and their gcb_* GraphCodeBERT copies
     (MHM_ATTACKERS; max_iter defaults to each driver's own, MHM_MAX_ITER).
@@ -418,7 +418,11 @@ def run_mhm_attack(model, codes, subs, labels, args: AttackArgs, indices=None, t
     `random.Random(args.seed + index)` — the same per-example seeding `rng="per_example"` gives
     the GA driver — and records stay in index order.  `queue` (batched form only) pulls the
     examples from a dist.DynamicQueue shared by all ranks instead of `indices`.  With
-    args.csv_store_path every attacked example gets its writemhm row (mhm_attack.py:229)."""
+    args.csv_store_path every attacked example gets its writemhm row (mhm_attack.py:229).
+    last_code: the eval list's LAST pair, which the GraphCodeBERT clone driver writes as every
+    row's Original Code (its leftover loop variable, mhm_attack.py:162 then :221); default
+    codes[-1], which is that pair only when `codes` is the whole eval list — a caller passing a
+    slice passes the whole list's last element."""
     tok = tok or Tokenizer()
     task = getattr(args, "task", "devign")
     if max_iter is None:
@@ -430,7 +434,8 @@ def run_mhm_attack(model, codes, subs, labels, args: AttackArgs, indices=None, t
     try:
         records, t0 = _run_mhm_loop(model, codes, subs, labels, args, attacker, tok, task, order,
                                     recorder, n_candi, max_iter, prob_threshold, original,
-                                    max_inflight, queue)
+                                    max_inflight, queue,
+                                    codes[-1] if last_code is None else last_code)
     finally:
         if recorder is not None:
             recorder.close()
@@ -443,7 +448,7 @@ def run_mhm_attack(model, codes, subs, labels, args: AttackArgs, indices=None, t
 
 
 def _run_mhm_loop(model, codes, subs, labels, args, attacker, tok, task, order, recorder, n_candi,
-                  max_iter, prob_threshold, original, max_inflight, queue):
+                  max_iter, prob_threshold, original, max_inflight, queue, last_code):
     records, t0 = [], time.time()
     if max_inflight > 1 or queue is not None:
         from .batching import run_requests
@@ -459,7 +464,7 @@ def _run_mhm_loop(model, codes, subs, labels, args, attacker, tok, task, order, 
             dt = (time.time() - ts) / 60
             writer.finish(index, lambda rec: _mhm_record(index, codes[index], task, value[1],
                                                          labels[index], queries, dt, rec,
-                                                         codes[-1]))
+                                                         last_code))
 
         run_requests(model, _source(order, queue, writer), start, on_done, max(2, max_inflight))
         records = writer.records()
@@ -482,5 +487,5 @@ def _run_mhm_loop(model, codes, subs, labels, args, attacker, tok, task, order, 
             res = {"error": f"KeyError: {e}"}
         records.append(_mhm_record(index, codes[index], task, res, labels[index],
                                    model.query - q0, (time.time() - ts) / 60, recorder,
-                                   codes[-1]))
+                                   last_code))
     return records, t0

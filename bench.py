@@ -79,10 +79,12 @@ def parse_args():
                     help="examples of the sequential MHM-NS comparison run")
     ap.add_argument("--aa-examples", type=int, default=132,
                     help="authorship programs of the config-5 leg (GA vs MHM-NS; 0 disables)")
-    ap.add_argument("--aa-gcb-examples", type=int, default=32,
-                    help="of them, attacked by GA on the GraphCodeBERT victim too (0 disables)")
+    ap.add_argument("--aa-gcb-examples", type=int, default=132,
+                    help="of them, attacked by GA and MHM-NS on the GraphCodeBERT victim too (0 "
+                         "disables; all 132 take ~80 s)")
     ap.add_argument("--clone-examples", type=int, default=32,
-                    help="config-4 leg: GraphCodeBERT BigCloneBench pairs attacked (0 = skip)")
+                    help="config-4 leg: GraphCodeBERT BigCloneBench pairs attacked (0 = skip; all "
+                         "500 take ~9 min: profiles/r6a_config4_full_500.jsonl)")
     ap.add_argument("--no-config1", action="store_true", help="skip the config-1 leg")
     ap.add_argument("--no-microbench", action="store_true",
                     help="skip the SURVEY §8(d) microbenchmarks (batch 1024, varlen, GCB 640)")
@@ -1031,11 +1033,12 @@ def main():
             v, sample = cpu_baseline(L, args.cpu_seconds, t)
             points.append({"cores": t, "value": round(v, 4), "sample": sample,
                            "path": "oracle/roberta_cpu.py fp32 eager"})
-        best = max(points, key=lambda q: q["value"])
-        try:  # the transformers forward the reference itself calls, at the best thread count
-            v, sample = cpu_baseline(L, args.cpu_seconds, best["cores"], impl="hf")
-            points.append({"cores": best["cores"], "value": round(v, 4), "sample": sample,
-                           "path": "transformers RobertaForSequenceClassification eager fp32"})
+        try:  # the transformers forward the reference itself calls, at every point of the sweep
+            for t in sweep:
+                log(f"CPU baseline, transformers ({t} threads)")
+                v, sample = cpu_baseline(L, args.cpu_seconds, t, impl="hf")
+                points.append({"cores": t, "value": round(v, 4), "sample": sample,
+                               "path": "transformers RobertaForSequenceClassification eager fp32"})
         except ImportError as e:
             log(f"transformers not importable: {e}")
         best = max(points, key=lambda q: q["value"])

