@@ -29,6 +29,10 @@
 // profiles/r4g_*; merging the chunks in the sequence's last-arriving chunk workgroup instead of a
 // combine kernel made the attention kernel 36 -> 163-204 us: one workgroup then reads all of a
 // sequence's records, r4i)
+// Round 6: the same kernels serve any fixed number qper of query rows per sequence (query qi of
+// sequence qi / qper; its chunk records after the sequence's earlier queries', rec_base): the
+// row windows of ae_encode_rows, where each config-3 candidate is read only at its own span
+// (get_substitutes.py:98-108) — the last layer then costs O(rows) instead of a full layer.
 // Masked (GraphCodeBERT) launches read row 0 of the sequence's bit-packed mask; the CLS row always
 // attends itself (special tokens see [:max_length], utils.py:555-557), so a fully masked CLS row
 // cannot occur — if it does the device error flag poisons the scores (alert_engine.h ae_score).
