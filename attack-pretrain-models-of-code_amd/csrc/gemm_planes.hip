@@ -121,6 +121,7 @@ __device__ __forceinline__ void wait_vm() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
   else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   else static_assert(N == 0, "unsupported vmcnt");
@@ -1060,6 +1061,334 @@ __global__ __launch_bounds__(512, 1) void gemm_pp192_kernel(
 
 namespace {
 int cu_count();
+// ------------------------------------------------------------------------------------------
+// Two-per-CU 128 x 192 packed GEMM (gemm_p2_kernel): the N = 768 GEMMs (O-projection, FFN2) with
+// the residual + statistics epilogue of the folded LayerNorm (PK_EPI_RES_STATS(_LN)), built so that
+// TWO workgroups share a CU and one's epilogue — HBM-bound: the residual rows in, v and its planes
+// out, 590 KB per 256 x 192 tile of gemm_pp192_kernel — runs under the other's MFMAs, which one
+// workgroup per CU cannot do.  4 waves (2 x 2 blocks of 64 x 96, gemm_pp192_kernel's wave block
+// and epilogue), 80 KiB of LDS: two 40-KiB stages of a 32-k K-tile (A 128 rows + W 192 rows) and
+// nothing else — the epilogue's side data (bias, gamma / beta, the plane shift, the residual rows'
+// statistics: 8 KiB) is moved by LDS-DMA into the tail of the stage that frees up first during the
+// last two K-tiles, and the staging regions fill the stages once the loop is done.  No ping-pong
+// between wave groups: per K-tile every wave waits for its own pieces, a barrier, its fragment
+// reads, a barrier (the stage is free), then its 36 MFMAs with K-tile kt+2's 10 DMA pieces in
+// their issue gaps; the co-resident workgroup fills the matrix pipe while this one waits.
+// V = 1: the fragment reads pipelined against the MFMAs — all 20 issued, the MFMAs of column block
+// 0 after the A and W(0) reads (the compiler's partial lgkmcnt), block 1 after W(1), then the
+// stage-free barrier and block 2 with K-tile kt+2's DMA pieces.
+template <int NP, int EPI, int V = 0>
+__global__ __launch_bounds__(256, 2) void gemm_p2_kernel(
+    const __bf16* __restrict__ A, const __bf16* __restrict__ W, const float* __restrict__ bias,
+    const float* R, float* C, int M, int N, int K, int group_m, StatArgs ln) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char pk_smem[];
+  static_assert(EPI == PK_EPI_RES_STATS || EPI == PK_EPI_RES_STATS_LN, "statistics epilogues only");
+  constexpr int BM = 128, BN = 192, ROWB = PK_ROWB;
+  constexpr int A_BYTES = BM * ROWB, STAGE = (BM + BN) * ROWB;  // 40 KiB per K-tile
+  constexpr int KB = 64 / NP, NS = KB / 16, T = NP == 2 ? 3 : 1;
+  constexpr int NPC = 10;  // DMA pieces per wave per K-tile: 4 of A (rows 32 w ..), 6 of W (48 w ..)
+
+  const int tiles_n = (N + BN - 1) / BN;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int per_group = group_m * tiles_n;
+  const int g = t / per_group, first_m = g * group_m;
+  const int gsize = min(tiles_m - first_m, group_m);
+  const int tm0 = first_m + (t - g * per_group) % gsize, tn0 = (t - g * per_group) / gsize;
+  const int m0 = tm0 * BM, n0 = tn0 * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int sm = wave >> 1, sn = wave & 1;  // sub-row (64 rows), sub-column (96 columns)
+  const int li = lane & 31, lh = lane >> 5;
+  const size_t lda = (size_t)NP * K;
+
+  const char* src[NPC];
+  uint32_t dst[NPC];
+#pragma unroll
+  for (int j = 0; j < NPC; ++j) {
+    const bool is_a = j < 4;
+    const int r0 = is_a ? 32 * wave + 8 * j : 48 * wave + 8 * (j - 4);
+    const int r = r0 + (lane >> 3);
+    const int cs = (lane & 7) ^ ((r >> 1) & 7);
+    if (is_a) {
+      const int gr = m0 + r < M ? m0 + r : M - 1;
+      src[j] = reinterpret_cast<const char*>(A + gr * lda) + 16 * cs;
+      dst[j] = r0 * ROWB;
+    } else {
+      const int gr = n0 + r < N ? n0 + r : N - 1;
+      src[j] = reinterpret_cast<const char*>(W + gr * lda) + 16 * cs;
+      dst[j] = A_BYTES + r0 * ROWB;
+    }
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)pk_smem;
+  const int nk = K / KB;
+  auto issue = [&](int j, int kt) {
+    dma16(src[j] + (size_t)kt * ROWB, lds0 + (kt & 1) * STAGE + dst[j]);
+  };
+  // the epilogue's side data: into the tail of the stage that frees up first at the end of the
+  // loop (K-tile nk - 2's; with one K-tile, the unused second stage)
+  const int side_stage = nk >= 2 ? ((nk - 2) & 1) : 1;
+  const uint32_t SIDE = side_stage * STAGE + STAGE - 8192;  // bias | gamma | beta | shift | rstats
+  constexpr bool rnorm = EPI == PK_EPI_RES_STATS_LN;
+  auto issue_side = [&]() {
+    if (wave == 0) {
+      dma16(bias + n0 + 4 * min(lane, 47), lds0 + SIDE);
+    } else if (wave == 1) {
+      if (rnorm) {
+        dma16(ln.gamma + n0 + 4 * min(lane, 47), lds0 + SIDE + 1024);
+        dma16(ln.beta + n0 + 4 * min(lane, 47), lds0 + SIDE + 2048);
+      }
+    } else if (wave == 2) {
+      if (ln.shift) dma16(ln.shift + n0 + 4 * min(lane, 47), lds0 + SIDE + 3072);
+    } else if (rnorm) {
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const int r0 = h * 32;  // first tile row of the piece; 2 lanes per row
+        dma16(ln.rstats + (size_t)min(m0 + r0 + (lane >> 1), M - 1) * 4 + 2 * (lane & 1),
+              lds0 + SIDE + 4096 + (uint32_t)(r0 * 32));
+      }
+    }
+  };
+
+  floatx16 acc[2][3];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  const int sw = (li >> 1) & 7;
+  const int a_row = (sm * 64 + li) * ROWB;
+  const int w_row = A_BYTES + (sn * 96 + li) * ROWB;
+  bf16x8 fa[2][NS][NP], fw[3][NS][NP];
+
+  if (nk > 0) {
+#pragma unroll
+    for (int j = 0; j < NPC; ++j) issue(j, 0);
+  }
+  if (nk > 1) {
+#pragma unroll
+    for (int j = 0; j < NPC; ++j) issue(j, 1);
+  } else {
+    issue_side();
+  }
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const unsigned char* st = pk_smem + (kt & 1) * STAGE;
+    // this wave's pieces of K-tile kt (K-tile kt + 1's may still be in flight), then everyone's
+    if (kt + 1 < nk) wait_vm<NPC>();
+    else wait_vm<0>();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int s2 = 0; s2 < NS; ++s2)
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+          fa[tt][s2][p] = *reinterpret_cast<const bf16x8*>(
+              st + a_row + tt * 32 * ROWB + 16 * ((4 * p + 2 * s2 + lh) ^ sw));
+#pragma unroll
+    for (int tn = 0; tn < 3; ++tn)
+#pragma unroll
+      for (int s2 = 0; s2 < NS; ++s2)
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+          fw[tn][s2][p] = *reinterpret_cast<const bf16x8*>(
+              st + w_row + tn * 32 * ROWB + 16 * ((4 * p + 2 * s2 + lh) ^ sw));
+    const bool dma = kt + 2 < nk;
+    constexpr int NM = NS * 2 * T;  // MFMAs per column block
+    auto mfma_block = [&](int tn, bool with_dma) {
+#pragma unroll
+      for (int i = 0; i < NM; ++i) {
+        const int s2 = i / (2 * T), tt = (i / T) % 2, term = i % T;
+        floatx16& c = acc[tt][tn];
+        const bf16x8& x = (T == 3 && term == 1) ? fw[tn][s2][NP - 1] : fw[tn][s2][0];
+        const bf16x8& y = (T == 3 && term == 0) ? fa[tt][s2][NP - 1] : fa[tt][s2][0];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, c, 0, 0, 0);
+        if (with_dma) {
+          // K-tile kt + 2's pieces in the MFMA issue gaps: 10 over the MFMAs that follow the
+          // stage-free barrier (V 0: all 3 x NM of them, V 1: block 2's NM)
+          constexpr int SPAN = V == 0 ? 3 * NM : NM;
+          constexpr int EVERY = SPAN / NPC > 0 ? SPAN / NPC : 1;
+          const int gi = (V == 0 ? tn * NM : 0) + i;
+          if (dma && gi % EVERY == EVERY - 1 && gi / EVERY < NPC) {
+            __builtin_amdgcn_sched_barrier(0);
+            issue(gi / EVERY, kt + 2);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+      if (with_dma && V == 1 && dma && NM / (NM / NPC > 0 ? NM / NPC : 1) < NPC) {
+        // fewer MFMAs than pieces: the rest after the block
+#pragma unroll
+        for (int j = NM / (NM / NPC > 0 ? NM / NPC : 1); j < NPC; ++j) issue(j, kt + 2);
+      }
+    };
+    if constexpr (V == 0) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();  // every wave holds its fragments: stage kt & 1 is free
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + 2 == nk) issue_side();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int tn = 0; tn < 3; ++tn) mfma_block(tn, true);
+      __builtin_amdgcn_s_setprio(0);
+    } else {
+      __builtin_amdgcn_s_setprio(1);
+      mfma_block(0, false);
+      mfma_block(1, false);
+      __builtin_amdgcn_s_setprio(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();  // every wave holds its fragments: stage kt & 1 is free
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + 2 == nk) issue_side();
+      __builtin_amdgcn_s_setprio(1);
+      mfma_block(2, true);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  // every wave is past its last fragment reads (the loop's second barrier); the side data landed
+  // with each issuer's final vmcnt(0) before the last K-tile's first barrier
+
+  // ---- v = (acc + bias) + residual as f32 and packed planes of v - shift, plus this tile's
+  // (mean, M2) of every row (gemm_pp192_kernel's epilogue for a 128-row tile; see there).
+  // acc[tm][tn] register 4 j + i of lane l = row sm*64 + tm*32 + (l & 31), column sn*96 + tn*32 +
+  // 8 j + 4 (l >> 5) + i of the tile.  R may alias C (no other workgroup touches this tile).
+  const int cb0 = n0 + sn * 96;
+  const int rb0 = m0 + sm * 64 + li;  // + 32 tm
+  constexpr int RS = 400;
+  // staging: waves 0-2 in the other stage, wave 3 at the head of the side stage; the row
+  // statistics exchange after it
+  unsigned char* reg = pk_smem + (wave < 3 ? (side_stage ^ 1) * STAGE + wave * 32 * RS
+                                           : side_stage * STAGE);
+  RowStat* lst = reinterpret_cast<RowStat*>(pk_smem + side_stage * STAGE + 32 * RS);
+  const int prow0 = m0 + sm * 64;
+  const float* const colt = reinterpret_cast<const float*>(pk_smem + SIDE);
+  float rmu[2] = {0.f, 0.f}, rrs[2] = {1.f, 1.f};
+  if constexpr (rnorm) {
+    const uint64_t* rst = reinterpret_cast<const uint64_t*>(pk_smem + SIDE + 4096);
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm) row_norm(rst + (rb0 - m0 + 32 * tm) * 4, ln.eps, rmu[tm], rrs[tm]);
+  }
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm) {
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+      const int idx = k * 64 + lane, lr = idx / 24, c = idx % 24;
+      const int row = prow0 + tm * 32 + lr;
+      const floatx4 f = row < M ? *reinterpret_cast<const floatx4*>(R + (size_t)row * N + cb0 + 4 * c)
+                                : floatx4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<floatx4*>(reg + lr * RS + c * 16) = f;
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int tn = 0; tn < 3; ++tn)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int tc = sn * 96 + tn * 32 + 8 * j + 4 * lh;  // column within the tile
+        const floatx4 bv = *reinterpret_cast<const floatx4*>(colt + tc);
+        floatx4 rv = *reinterpret_cast<const floatx4*>(reg + li * RS + (tn * 8 + 2 * j + lh) * 16);
+        if constexpr (rnorm) {
+          const floatx4 gg = *reinterpret_cast<const floatx4*>(colt + 256 + tc);
+          const floatx4 bb = *reinterpret_cast<const floatx4*>(colt + 512 + tc);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) rv[i] = (rv[i] - rmu[tm]) * rrs[tm] * gg[i] + bb[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc[tm][tn][4 * j + i] = (acc[tm][tn][4 * j + i] + bv[i]) + rv[i];
+          asm volatile("" : "+v"(acc[tm][tn][4 * j + i]));
+        }
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  float mean96[2], m2_96[2];
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm) {
+    float sum = 0.f;
+#pragma unroll
+    for (int tn = 0; tn < 3; ++tn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sum += acc[tm][tn][r];
+    sum += __shfl_xor(sum, 32, 64);
+    const float mu = sum * (1.f / 96.f);
+    float q = 0.f;
+#pragma unroll
+    for (int tn = 0; tn < 3; ++tn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float d = acc[tm][tn][r] - mu;
+        q += d * d;
+      }
+    q += __shfl_xor(q, 32, 64);
+    mean96[tm] = mu;
+    m2_96[tm] = q;
+  }
+  if (lh == 0) {
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm) lst[(wave * 2 + tm) * 32 + li] = RowStat{mean96[tm], m2_96[tm]};
+  }
+  __syncthreads();
+  if (sn == 0 && lh == 0) {
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm) {
+      const RowStat o = lst[((wave ^ 1) * 2 + tm) * 32 + li];
+      const float d = mean96[tm] - o.mean;
+      const RowStat t2{(mean96[tm] + o.mean) * 0.5f, (m2_96[tm] + o.m2) + 48.f * d * d};
+      if (rb0 + 32 * tm < M) ln.stats[(size_t)(rb0 + 32 * tm) * 4 + tn0] = __builtin_bit_cast(uint64_t, t2);
+    }
+  }
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm) {
+#pragma unroll
+    for (int tn = 0; tn < 3; ++tn)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        floatx4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = acc[tm][tn][4 * j + i];
+        *reinterpret_cast<floatx4*>(reg + li * RS + (tn * 8 + 2 * j + lh) * 16) = o;
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const int kk = k % 3, g2 = k / 3;
+      const int idx = kk * 64 + lane, lr = idx / 12 + 16 * g2, c8 = idx % 12;
+      const int row = prow0 + tm * 32 + lr;
+      const floatx4 o0 = *reinterpret_cast<const floatx4*>(reg + lr * RS + c8 * 32);
+      const floatx4 o1 = *reinterpret_cast<const floatx4*>(reg + lr * RS + c8 * 32 + 16);
+      if (row < M) {
+        const int col = cb0 + 8 * c8;
+        float* const vrow = C + (size_t)prow0 * N + (uint32_t)(lr + tm * 32) * (uint32_t)N;
+        *reinterpret_cast<floatx4*>(vrow + col) = o0;
+        *reinterpret_cast<floatx4*>(vrow + col + 4) = o1;
+        uint32_t h[4], l[4];
+        floatx4 p0 = o0, p1 = o1;  // the planes hold v - kappa (the plane shift, FoldArgs)
+        if (ln.shift) {
+          const float* const kap = colt + 768;  // SIDE + 3072
+          p0 -= *reinterpret_cast<const floatx4*>(kap + (col - n0));
+          p1 -= *reinterpret_cast<const floatx4*>(kap + (col - n0) + 4);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          split_pair(i < 2 ? gelu_f2{p0[2 * i], p0[2 * i + 1]} : gelu_f2{p1[2 * i - 4], p1[2 * i - 3]},
+                     h[i], l[i]);
+        unsigned short* dstp = reinterpret_cast<unsigned short*>(ln.xp) + (size_t)prow0 * NP * N +
+                               (uint32_t)(lr + tm * 32) * (uint32_t)(NP * N) +
+                               (uint32_t)((col >> 5) * 32 * NP + (col & 31));
+        *reinterpret_cast<uint4*>(dstp) = uint4{h[0], h[1], h[2], h[3]};
+        if (NP == 2) *reinterpret_cast<uint4*>(dstp + 32) = uint4{l[0], l[1], l[2], l[3]};
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
 // DIAG value of the persistent launch (exact results): one workgroup per CU looping over tiles
 constexpr int PP_PERSIST = 9;
 
@@ -1117,6 +1446,18 @@ hipError_t pp192_launch(const __bf16* A, const __bf16* W, const float* bias, con
   const int tiles_m = (M + 255) / 256;
   const int tiles = tiles_m * ((N + 191) / 192);
   hipLaunchKernelGGL((gemm_pp192_kernel<NP, EPI, NT>), dim3(tiles), dim3(512), lds, st, A, W, bias, R,
+                     C, M, N, K, group_m, ln);
+  return hipGetLastError();
+}
+
+template <int NP, int EPI, int V = 0>
+hipError_t p2_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R, float* C,
+                     int M, int N, int K, int group_m, hipStream_t st, StatArgs ln) {
+  constexpr int lds = 2 * (128 + 192) * PK_ROWB;  // 80 KiB: two workgroups per CU
+  if (hipError_t e = ensure_dynamic_lds((const void*)gemm_p2_kernel<NP, EPI, V>, lds); e != hipSuccess)
+    return e;
+  const int tiles = ((M + 127) / 128) * ((N + 191) / 192);
+  hipLaunchKernelGGL((gemm_p2_kernel<NP, EPI, V>), dim3(tiles), dim3(256), lds, st, A, W, bias, R,
                      C, M, N, K, group_m, ln);
   return hipGetLastError();
 }
@@ -1304,6 +1645,39 @@ extern "C" hipError_t ae_launch_gemm_packed_res_stats(
 #ifdef AE_TOOLS
 // ---- tools library only (lib/libalert_engine_tools.so, -DAE_TOOLS): timing experiments whose
 // variants give WRONG results on purpose; the product library exports none of this.
+
+// ae_launch_gemm_packed_res_stats with an explicit kernel: variant 0 = gemm_pp192_kernel (one
+// 256 x 192 workgroup per CU), 1 = gemm_p2_kernel (two 128 x 192 workgroups per CU, M-tiles
+// grouped by `group` (0: 8)).  Exact results in both.
+extern "C" hipError_t ae_bench_gemm_packed_res_stats(
+    const unsigned short* A, const unsigned short* W, const float* bias, const float* R,
+    const uint64_t* rstats, const float* gamma, const float* beta, float eps, float* C,
+    unsigned short* Cp, uint64_t* stats, int M, int N, int K, int np, const float* shift,
+    int variant, int group, hipStream_t st) {
+  if (variant == 0)
+    return ae_launch_gemm_packed_res_stats(A, W, bias, R, rstats, gamma, beta, eps, C, Cp, stats,
+                                           M, N, K, np, shift, st);
+  if (M <= 0) return hipSuccess;
+  if ((variant != 1 && variant != 2) || N != 768 || K % 64 != 0 || (np != 1 && np != 2) || !bias ||
+      !R || !C || !Cp || !stats || (rstats && (!gamma || !beta)))
+    return hipErrorInvalidValue;
+  const StatArgs ln{gamma, beta, eps, reinterpret_cast<__bf16*>(Cp), stats, rstats, shift};
+  auto a = reinterpret_cast<const __bf16*>(A);
+  auto w = reinterpret_cast<const __bf16*>(W);
+  const int gm = group > 0 ? group : 8;
+  if (variant == 2) {  // fragment reads pipelined against the MFMAs (V 1)
+    if (rstats)
+      return np == 2 ? p2_launch<2, PK_EPI_RES_STATS_LN, 1>(a, w, bias, R, C, M, N, K, gm, st, ln)
+                     : p2_launch<1, PK_EPI_RES_STATS_LN, 1>(a, w, bias, R, C, M, N, K, gm, st, ln);
+    return np == 2 ? p2_launch<2, PK_EPI_RES_STATS, 1>(a, w, bias, R, C, M, N, K, gm, st, ln)
+                   : p2_launch<1, PK_EPI_RES_STATS, 1>(a, w, bias, R, C, M, N, K, gm, st, ln);
+  }
+  if (rstats)
+    return np == 2 ? p2_launch<2, PK_EPI_RES_STATS_LN>(a, w, bias, R, C, M, N, K, gm, st, ln)
+                   : p2_launch<1, PK_EPI_RES_STATS_LN>(a, w, bias, R, C, M, N, K, gm, st, ln);
+  return np == 2 ? p2_launch<2, PK_EPI_RES_STATS>(a, w, bias, R, C, M, N, K, gm, st, ln)
+                 : p2_launch<1, PK_EPI_RES_STATS>(a, w, bias, R, C, M, N, K, gm, st, ln);
+}
 
 // Kernel experiments (tools/gemm_bench.py, tests): explicit tile width (0 = the production choice)
 // and a diagnostic variant (0 = the production kernel; see DIAG above — values 1-7 give WRONG

@@ -389,17 +389,25 @@ def _ln64(v, gamma, beta, eps=1e-5):
     return (v - mu) / torch.sqrt(var + eps) * gamma.double() + beta.double(), var
 
 
+@pytest.mark.parametrize("variant", [0, 1, 2])
 @pytest.mark.parametrize("M,K,np_,shift", [(300, 768, 2, 0), (4097, 768, 2, 1), (37, 3072, 2, 1),
-                                            (1000, 768, 1, 0), (1000, 768, 1, 1)])
-def test_gemm_packed_res_stats_matches_f64(gpu, M, K, np_, shift):
+                                            (1000, 768, 1, 0), (1000, 768, 1, 1), (200, 64, 1, 1),
+                                            (300, 64, 2, 0)])
+def test_gemm_packed_res_stats_matches_f64(gpu, M, K, np_, shift, variant):
     """ae_launch_gemm_packed_res_stats (256 x 192 kernel): v = A·W^T + bias + r as f32 and packed
     planes plus the (mean, M2) of every row over its 4 192-column tiles, first with a plain
     residual (PK_EPI_RES_STATS: layer 0), then with the residual the previous pre-LayerNorm rows
     normalised on the fly from the statistics the first launch wrote (PK_EPI_RES_STATS_LN).
     Both in place (R = C), as the engine runs them; against float64 of the split products.  With
     shift, the planes hold v - kappa (the plane shift; kappa = bias + beta, as the engine passes)
-    while f32 v and its statistics stay those of v."""
+    while f32 v and its statistics stay those of v.  variants 1 / 2: the two-per-CU 128 x 192 kernel
+    (gemm_p2_kernel, tools library; 2 = its fragment reads pipelined against the MFMAs); K = 64
+    its one- (np 1) and two-K-tile (np 2) paths."""
     lib = _fold_lib()
+    lib.ae_bench_gemm_packed_res_stats.argtypes = [ctypes.c_void_p] * 7 + [ctypes.c_float] + \
+        [ctypes.c_void_p] * 3 + [ctypes.c_int32] * 4 + [ctypes.c_void_p, ctypes.c_int32,
+                                                         ctypes.c_int32, ctypes.c_void_p]
+    lib.ae_bench_gemm_packed_res_stats.restype = ctypes.c_int
     N = 768
     g = torch.Generator().manual_seed(7 * M + K)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -422,10 +430,10 @@ def test_gemm_packed_res_stats_matches_f64(gpu, M, K, np_, shift):
         else:
             r, _ = _ln64(prev, gamma, beta)
         kap = (bias + (beta if rst is not None else 0.5)) if shift else None
-        rc = lib.ae_launch_gemm_packed_res_stats(
+        rc = lib.ae_bench_gemm_packed_res_stats(
             _p(dA), _p(dW), _p(db), _p(v), _p(rst), _p(dg if rst is not None else None),
             _p(dbeta if rst is not None else None), 1e-5, _p(v), _p(vp), _p(out_st), M, N, K,
-            np_, _p(kap.cuda() if shift else None), st)
+            np_, _p(kap.cuda() if shift else None), variant, 0, st)
         assert rc == 0
         torch.cuda.synchronize()
         ref = _split_prod(A, W, np_) + bias.double() + r

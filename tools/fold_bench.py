@@ -29,9 +29,13 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--lib", default=None)
+    ap.add_argument("--p2", action="store_true",
+                    help="also the two-per-CU 128 x 192 kernel of the statistics epilogues "
+                         "(tools library, ae_bench_gemm_packed_res_stats variant 1)")
+    ap.add_argument("--only", default=None, help="comma-separated launch names")
     args = ap.parse_args()
     from apmc_amd.engine import load_library
-    lib = load_library(args.lib)
+    lib = load_library(args.lib, tools=args.p2)
     vp, i32, f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_float
     lib.ae_launch_gemm_packed.argtypes = [vp] * 6 + [i32] * 5 + [vp]
     lib.ae_launch_gemm_packed_fold.argtypes = [vp] * 5 + [f32, vp] + [i32] * 5 + [vp, vp]
@@ -76,6 +80,19 @@ def main():
         "ffn2_plain": lambda: lib.ae_launch_gemm_packed(p(h), p(w["ffn2"]), p(bias), p(rv), p(v), None, M, H, F, 2, 2, st),
         "ffn2_stats": lambda: lib.ae_launch_gemm_packed_res_stats(p(h), p(w["ffn2"]), p(bias), p(rv), p(stats), p(gam), p(bet), 1e-5, p(v), p(vp_), p(ostats), M, H, F, 2, p(kap), st),
     }
+    if args.p2:
+        lib.ae_bench_gemm_packed_res_stats.argtypes = [vp] * 7 + [f32] + [vp] * 3 + [i32] * 4 + \
+            [vp, i32, i32, vp]
+        for nm, a_, w_, K_ in (("oproj", ctx, w["oproj"], H), ("ffn2", h, w["ffn2"], F)):
+            for var in (1, 2):
+                for grp in (8, 4, 16):
+                    calls[f"{nm}_stats_p2v{var}_g{grp}"] = (
+                        lambda a_=a_, w_=w_, K_=K_, grp=grp, var=var:
+                        lib.ae_bench_gemm_packed_res_stats(
+                            p(a_), p(w_), p(bias), p(rv), p(stats), p(gam), p(bet), 1e-5, p(v),
+                            p(vp_), p(ostats), M, H, K_, 2, p(kap), var, grp, st))
+    if args.only:
+        calls = {k: c for k, c in calls.items() if k in args.only.split(",")}
     ts = {k: [] for k in calls}
     for k, c in calls.items():
         assert c() == 0, k
