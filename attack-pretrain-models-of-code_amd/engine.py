@@ -78,7 +78,8 @@ def load_library(path: str | os.PathLike | None = None, tools: bool = False) -> 
     lib.ae_graph_mask.argtypes = [vp, vp, vp, vp, i32, i32, i32, vp, vp]
     lib.ae_encode.argtypes = [vp, vp, vp, i32, i32, vp, vp]
     lib.ae_encode_ex.argtypes = [vp, vp, vp, i32, i32, i32, i32, i32, vp, vp]
-    lib.ae_encode_rows.argtypes = [vp, vp, vp, i32, i32, i32, vp, i32, vp, vp]
+    if path is None or hasattr(lib, "ae_encode_rows"):  # an older library at an explicit path
+        lib.ae_encode_rows.argtypes = [vp, vp, vp, i32, i32, i32, vp, i32, vp, vp]  # (same-box A/B)
     lib.ae_mlm_topk.argtypes = [vp, vp, i32, i32, vp, vp, vp]
     lib.ae_mlm_nll.argtypes = [vp, vp, i32, i32, vp, vp]
     lib.ae_splice.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp]
@@ -90,7 +91,8 @@ def load_library(path: str | os.PathLike | None = None, tools: bool = False) -> 
     lib.ae_last_error.restype = ctypes.c_char_p
     lib.ae_version.restype = ctypes.c_char_p
     for name in EXPORTS:
-        if name not in ("ae_last_error", "ae_version", "ae_source_hash"):
+        if name not in ("ae_last_error", "ae_version", "ae_source_hash") and \
+                (path is None or hasattr(lib, name)):
             getattr(lib, name).restype = ctypes.c_int
     _LIBS[key] = lib
     return lib
