@@ -99,6 +99,15 @@ template <int NP>
 __device__ __forceinline__ int vpos(int r, int x) {
   return NP == 2 ? x ^ ((r & 3) << 2) : x ^ (((r >> 1) & 1) << 2);
 }
+template <int N>
+__device__ __forceinline__ void wait_vm_n() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else static_assert(N == 0, "unsupported vmcnt");
+}
 }  // namespace
 
 // PIPE 4: software-pipelined loop — the S MFMAs of key tile kt + 1 issue in the same scheduling
@@ -648,6 +657,393 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && !(HAS_MASK && NP == 2)) ? 3 : 2
   }
 }
 
+// PIPE 80: two 32-query blocks per wave (64 queries: block A = the 4-wave loops' wave 2w, block B
+// = wave 2w + 1), two waves per workgroup (the same 128-query blocks), four workgroups per CU, so
+// two waves per SIMD within 256 registers.  One wave's instruction stream interleaves the blocks:
+// S_A, then S_B under block A's row max / exp / split, then PV_A under block B's, then PV_B — the
+// K and V fragments each serve both blocks (half the LDS reads per MFMA), and every block's
+// arithmetic is PIPE 6's (same MFMA order, tile max, deferred rescale, exp / split and row sum),
+// so the context is bit-identical.  K and V in 2-slot rings (tile kt + 2 issued once every wave
+// has finished tile kt), 32 KiB per workgroup.  No mask path (masked launches run PIPE 66).
+template <int NP, bool PLANES, int NW, bool QLDS, int NS, int DIAG = 0, bool KH = false>
+__global__ __launch_bounds__(64 * NW, 2) void attn_pq_kernel(const unsigned short* __restrict__ qkvp,
+                                                          float* __restrict__ out,
+                                                          unsigned short* __restrict__ op,
+                                                          const int* __restrict__ cu,
+                                                          const int* __restrict__ q_rows) {
+  using P = PPL<NP>;
+  constexpr int TERMS = NP == 2 ? 3 : 1;
+  constexpr int QB = 64 * NW;                        // queries per workgroup
+  constexpr int DM = KT / P::ROWS_PER_DMA / NW;      // DMA instructions per wave per matrix tile
+  // QLDS: the Q lo-plane fragments in LDS (1 KiB per wave, block and 16-d step, lane-major) instead
+  // of 32 registers, past the K / V rings
+  constexpr bool QL = QLDS && TERMS == 3;
+  constexpr int QOFF = 2 * NS * P::TILE;  // NS K slots, then NS V slots
+  constexpr int RING_Q = QOFF + (QL ? NW * 8 * 1024 : 0);
+  constexpr int LDS_BYTES = RING_Q > NW * 32 * 66 * 4 ? RING_Q : NW * 32 * 66 * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
+  const int seq = blockIdx.z, head = blockIdx.y, qb = blockIdx.x;
+  const int start = cu[seq];
+  const int len = cu[seq + 1] - start;
+  const int nq = q_rows ? min(len, q_rows[0]) : len;
+  if (qb * QB >= nq) return;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 31, lh = lane >> 5;
+  constexpr size_t LDR = (size_t)NP * QKV_COLS;
+
+  // Q fragments of both blocks (pre-scaled; B operand: B[k = d][j = q])
+  bf16x8 qh[2][4], ql[2][QL ? 1 : 4];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int q = qb * QB + wave * 64 + b * 32 + li;
+    const int qr = q < nq ? q : nq - 1;
+    const unsigned short* qp = qkvp + (size_t)(start + qr) * LDR + (size_t)head * 64 * NP;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int d = 16 * s + 8 * lh;
+      const int off = (d >> 5) * 32 * NP + (d & 31);
+      qh[b][s] = *reinterpret_cast<const bf16x8*>(qp + off);
+      if constexpr (QL) {
+        *reinterpret_cast<bf16x8*>(lds + QOFF + ((wave * 2 + b) * 4 + s) * 1024 + lane * 16) =
+            *reinterpret_cast<const bf16x8*>(qp + off + 32);
+      } else if (TERMS == 3) {
+        ql[b][s] = *reinterpret_cast<const bf16x8*>(qp + off + 32);
+      }
+    }
+  }
+
+  const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
+  const int dr = lane / P::CR, dc = lane % P::CR;
+  // K_j in slot j & 1, V_j in slot 2 + (j & 1)
+  // per-lane byte offset of DMA instruction j's chunk from the tile's first token row (K: isv 0),
+  // recomputed per issue (outside the MFMA regions) rather than held in 2·DM registers
+  auto voff = [&](int isv, int j) {
+    const int r = (wave * DM + j) * P::ROWS_PER_DMA + dr;
+    return 2u * ((uint32_t)r * (uint32_t)LDR + ((1 + isv) * AE_HIDDEN + head * 64) * NP +
+                 (isv ? vpos<NP>(r, dc) : kpos<NP>(r, dc)) * 8);
+  };
+  const unsigned char* sbase = reinterpret_cast<const unsigned char*>(qkvp + (size_t)start * LDR);
+  auto issue = [&](int kt, int isv) {
+    const unsigned char* sb = sbase + (size_t)kt * KT * LDR * 2;
+    const uint32_t dst = lds0 + (uint32_t)((isv * NS + kt % NS) * P::TILE);
+    if ((kt + 1) * KT <= len) {
+#pragma unroll
+      for (int j = 0; j < DM; ++j) dma16s(voff(isv, j), sb, dst + (wave * DM + j) * 1024);
+    } else {  // key rows past the sequence re-read its last row (finite, masked to -inf)
+      const int last = len - 1 - kt * KT;
+#pragma unroll
+      for (int j = 0; j < DM; ++j) {
+        const int over = (wave * DM + j) * P::ROWS_PER_DMA + dr - last;
+        const uint32_t v = voff(isv, j) - (over > 0 ? (uint32_t)over * (uint32_t)(LDR * 2) : 0u);
+        dma16s(v, sb, dst + (wave * DM + j) * 1024);
+      }
+    }
+  };
+  auto barrier = []() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // wait until at most nt tiles (2·DM DMA instructions each) of this wave are in flight
+  auto wait_tiles = [](int nt) {
+    if (nt >= 2) wait_vm_n<4 * DM>();
+    else if (nt == 1) wait_vm_n<2 * DM>();
+    else wait_vm_n<0>();
+  };
+
+  floatx16 o[2][2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { o[b][0][r] = 0.f; o[b][1][r] = 0.f; }
+  float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
+
+  // O_b^T += V^T P_b^T for key step t, d tile dt (PIPE 6's order: t outer, dt inner)
+  auto pv_step = [&](const unsigned char* stv, int ln, int b, int t, int dt, const bf16x8 (&ph)[2],
+                     const bf16x8 (&pl)[2]) {
+    {
+      const int k0 = 16 * t + 4 * (ln >> 5);
+      const int kq = k0 + ((ln >> 2) & 3);
+      {
+        const int col = dt * 32 + 16 * ((ln >> 4) & 1) + 4 * (ln & 3);
+        const int cb = (col & 7) * 2;
+        const unsigned char* va = stv + kq * P::RB + cb;
+        const unsigned char* vb = stv + (kq + 8) * P::RB + cb;
+        bf16x8 vh, vl;
+        if (DIAG == 1) {
+          asm volatile("" : "=v"(vh), "=v"(vl));
+        } else {
+          const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)(va + vpos<NP>(kq, chunk_of<NP>(0, col)) * 16));
+          const bf16x4 c = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)(vb + vpos<NP>(kq + 8, chunk_of<NP>(0, col)) * 16));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { vh[e] = a[e]; vh[4 + e] = c[e]; }
+        }
+        if (TERMS == 3 && DIAG != 1) {
+          const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)(va + vpos<NP>(kq, chunk_of<NP>(1, col)) * 16));
+          const bf16x4 c = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)(vb + vpos<NP>(kq + 8, chunk_of<NP>(1, col)) * 16));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { vl[e] = a[e]; vl[4 + e] = c[e]; }
+        }
+        floatx16& oo = o[b][dt];
+        if (TERMS == 3) {
+          oo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl, ph[t], oo, 0, 0, 0);
+          oo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, pl[t], oo, 0, 0, 0);
+        }
+        oo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, ph[t], oo, 0, 0, 0);
+      }
+    }
+  };
+  // block b's tile max (absent keys -inf), deferred-rescale decision, P = exp2(S - m) split into
+  // bf16 hi / lo, and the row sum — PIPE 67's arithmetic; the O rescale is left to the caller
+  // block b's tile max (absent keys -inf) and the deferred-rescale decision (PIPE 67's
+  // arithmetic): the reference max m_new and alpha = exp2(m_run - m_new)
+  auto tile_max = [&](auto fc, int kt, int b, floatx16& s, float& m_new, float& alpha, bool& grow) {
+    float mt = -INFINITY;
+    if constexpr (decltype(fc)::value) {  // full tile (compile-time: no branch in the region)
+      float a[6];
+#pragma unroll
+      for (int r = 0; r < 5; ++r) a[r] = max_nc(s[3 * r], max_nc(s[3 * r + 1], s[3 * r + 2]));
+      a[5] = s[15];
+      mt = max_nc(max_nc(a[0], max_nc(a[1], a[2])), max_nc(a[3], max_nc(a[4], a[5])));
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const bool in = kt * KT + mfma32_row(r, lh) < len;
+        s[r] = in ? s[r] : -INFINITY;
+        mt = max_nc(mt, s[r]);
+      }
+    }
+    const auto sw = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(uint32_t, mt),
+                                                    __builtin_bit_cast(uint32_t, mt), false, false);
+    mt = max_nc(__builtin_bit_cast(float, (uint32_t)sw[0]), __builtin_bit_cast(float, (uint32_t)sw[1]));
+    grow = __any(mt > m_run[b] + 8.f);
+    // m_new = grow ? max(m_run, mt) : m_run as a bit select on the uniform grow mask: a select on
+    // a wave-uniform condition becomes a branch, which would end the scheduling region here
+    const uint32_t gm = 0u - (uint32_t)grow;
+    m_new = __builtin_bit_cast(float, (__builtin_bit_cast(uint32_t, max_nc(m_run[b], mt)) & gm) |
+                                          (__builtin_bit_cast(uint32_t, m_run[b]) & ~gm));
+    alpha = __builtin_amdgcn_exp2f(m_run[b] - m_new);
+  };
+  // P = exp2(S - m_new) for scores r0 .. r1 - 1, split into bf16 hi / lo, summed in r order
+  auto exp_split = [&](const floatx16& s, float m_new, int r0, int r1, bf16x8 (&ph)[2],
+                       bf16x8 (&pl)[2], float& psum) {
+    if constexpr (DIAG == 3) {  // timing diagnostic: S's bits as P, no exp / split
+      if (r0 == 0) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          ph[h] = __builtin_bit_cast(bf16x8, floatx4{s[8 * h], s[8 * h + 1], s[8 * h + 2], s[8 * h + 3]});
+          pl[h] = __builtin_bit_cast(bf16x8, floatx4{s[8 * h + 4], s[8 * h + 5], s[8 * h + 6], s[8 * h + 7]});
+        }
+        psum = s[0];
+      }
+      return;
+    }
+#pragma unroll
+    for (int r = r0; r < r1; ++r) {
+      const float p = __builtin_amdgcn_exp2f(s[r] - m_new);
+      psum = r == 0 ? p : psum + p;
+      const __bf16 h = (__bf16)p;
+      ph[r >> 3][r & 7] = h;
+      pl[r >> 3][r & 7] = (__bf16)(p - (float)h);
+    }
+  };
+  // the 16-d K fragments of step ks (lane li: key row li)
+  auto kread = [&](const unsigned char* stk, int ln, int ks, bf16x8& kh, bf16x8& kl) {
+    if constexpr (DIAG == 1) {  // timing diagnostic: opaque register values, no LDS read
+      asm volatile("" : "=v"(kh), "=v"(kl));
+      return;
+    }
+    const int kli = ln & 31;
+    const unsigned char* kr = stk + kli * P::RB;
+    const int d0 = 16 * ks + 8 * (ln >> 5);
+    kh = *reinterpret_cast<const bf16x8*>(kr + kpos<NP>(kli, chunk_of<NP>(0, d0)) * 16);
+    if (TERMS == 3) kl = *reinterpret_cast<const bf16x8*>(kr + kpos<NP>(kli, chunk_of<NP>(1, d0)) * 16);
+  };
+  auto s_step = [&](int b, int ks, const bf16x8& kh, const bf16x8& kl, floatx16& s) {
+    if (TERMS == 3) {
+      bf16x8 qlf;
+      if (DIAG == 1 && QL) asm volatile("" : "=v"(qlf));
+      else qlf = QL ? *reinterpret_cast<const bf16x8*>(lds + QOFF + ((wave * 2 + b) * 4 + ks) * 1024 + lane * 16)
+                            : ql[b][QL ? 0 : ks];
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl, qh[b][ks], ks == 0 ? floatx16{} : s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, qlf, s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, qh[b][ks], s, 0, 0, 0);
+    } else {
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, qh[b][ks], ks == 0 ? floatx16{} : s, 0, 0, 0);
+    }
+  };
+  // scores of block A's softmax chunk c (c = 1..3 after the tile max in chunk 0)
+  constexpr int CH[5] = {0, 0, 6, 11, 16};
+
+  const int nkt = (len + KT - 1) / KT;
+  // prologue: tiles 0 .. NS-1 (as many as exist); tile 0 waited for
+#pragma unroll
+  for (int j = 0; j < NS; ++j)
+    if (j < nkt) {
+      issue(j, 0);
+      issue(j, 1);
+    }
+  wait_tiles(min(nkt, NS) - 1);
+  barrier();
+  auto body = [&](auto rc, auto fc, int kt) {
+    constexpr int R = decltype(rc)::value;
+    const unsigned char* stk = lds + R * P::TILE;
+    const unsigned char* stv = lds + (NS + R) * P::TILE;
+    floatx16 sa, sb;
+    bf16x8 pha[2], pla[2], phb[2], plb[2];
+    bf16x8 kh[2], kl[2];
+    float ma, mb, aa, ab, psa = 0.f, psb = 0.f;
+    bool ga, gb;
+    // the lane index through an opaque copy: the swizzled LDS addresses are recomputed per tile
+    // (a few VALU) instead of held in loop-invariant registers the two blocks' state needs
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    // S_A (matrix pipe only; the other wave on the SIMD fills the VALU).  KH: the tile's K
+    // fragments read once into 32 registers for both blocks, else read again for S_B
+    bf16x8 kall[KH ? 4 : 1][2];
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (KH) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) kread(stk, ln, ks, kall[ks][0], kall[ks][1]);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) s_step(0, ks, kall[ks][0], kall[ks][1], sa);
+    } else {
+      kread(stk, ln, 0, kh[0], kl[0]);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        if (ks + 1 < 4) kread(stk, ln, ks + 1, kh[(ks + 1) & 1], kl[(ks + 1) & 1]);
+        s_step(0, ks, kh[ks & 1], kl[ks & 1], sa);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // S_B under block A's tile max (step 0) and exp / split (steps 1-3), fenced per step
+    if (!KH) kread(stk, ln, 0, kh[0], kl[0]);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      if (!KH && ks + 1 < 4) kread(stk, ln, ks + 1, kh[(ks + 1) & 1], kl[(ks + 1) & 1]);
+      if constexpr (KH) s_step(1, ks, kall[ks][0], kall[ks][1], sb);
+      else s_step(1, ks, kh[ks & 1], kl[ks & 1], sb);
+      if (ks == 0) tile_max(fc, kt, 0, sa, ma, aa, ga);
+      else exp_split(sa, ma, CH[ks], CH[ks + 1], pha, pla, psa);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // pin block A's P fragments before the rescale branch: without a use here the compiler sinks
+    // the whole exp / split past it, out of the region it shares with S_B's MFMAs
+    asm volatile("" ::"v"(pha[0]), "v"(pha[1]), "v"(pla[0]), "v"(pla[1]), "v"(psa));
+    l_run[0] = l_run[0] * aa + psa;
+    m_run[0] = ma;
+    if (ga) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { o[0][0][r] *= aa; o[0][1][r] *= aa; }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // PV_A under block B's tile max and exp / split, fenced per (key step, d tile)
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      pv_step(stv, ln, 0, st >> 1, st & 1, pha, pla);
+      if (st == 0) tile_max(fc, kt, 1, sb, mb, ab, gb);
+      else exp_split(sb, mb, CH[st], CH[st + 1], phb, plb, psb);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("" ::"v"(phb[0]), "v"(phb[1]), "v"(plb[0]), "v"(plb[1]), "v"(psb));
+    l_run[1] = l_run[1] * ab + psb;
+    m_run[1] = mb;
+    if (gb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { o[1][0][r] *= ab; o[1][1][r] *= ab; }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int st = 0; st < 4; ++st) pv_step(stv, ln, 1, st >> 1, st & 1, phb, plb);
+    // tile kt + 1 landed (tiles kt + 2 .. kt + NS - 1 stay in flight); every wave is done with
+    // slot R: tile kt + NS into it
+    if (DIAG != 2 && DIAG != 4) {
+      wait_tiles(min(nkt - 1, kt + NS - 1) - kt - 1);
+      barrier();
+    }
+    if (DIAG != 4 && kt + NS < nkt) {
+      issue(kt + NS, 0);
+      issue(kt + NS, 1);
+    }
+  };
+  // the last tile, when partial, runs the per-key select form of the tile max
+  const int nfull = len / KT;
+  using T0 = std::integral_constant<int, 0>;
+  using T1 = std::integral_constant<int, 1>;
+  using T2 = std::integral_constant<int, NS == 3 ? 2 : 0>;
+  using FULL = std::true_type;
+  using PART = std::false_type;
+  for (int kt = 0; kt < nkt; kt += NS) {
+    if (kt < nfull) body(T0(), FULL(), kt);
+    else body(T0(), PART(), kt);
+    if (kt + 1 >= nkt) break;
+    if (kt + 1 < nfull) body(T1(), FULL(), kt + 1);
+    else body(T1(), PART(), kt + 1);
+    if constexpr (NS == 3) {
+      if (kt + 2 >= nkt) break;
+      if (kt + 2 < nfull) body(T2(), FULL(), kt + 2);
+      else body(T2(), PART(), kt + 2);
+    }
+  }
+
+  // epilogue: each block's O through the wave's LDS rows (66 floats), then 16-B stores
+  constexpr int S6 = 66;
+  float* os6 = reinterpret_cast<float*>(lds) + wave * 32 * S6;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const float l_tot = l_run[b] + __shfl_xor(l_run[b], 32, 64);
+    const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int d = mfma32_row(r, lh);
+      os6[li * S6 + d] = o[b][0][r] * inv;
+      os6[li * S6 + 32 + d] = o[b][1][r] * inv;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own rows: no barrier
+    constexpr int CPR = PLANES ? 8 * NP : 16;
+    constexpr int RPI = 64 / CPR;
+    const int c = lane % CPR;
+#pragma unroll
+    for (int it = 0; it < 32 / RPI; ++it) {
+      const int rr = it * RPI + lane / CPR;
+      const int qq = qb * QB + wave * 64 + b * 32 + rr;
+      const float* src = os6 + rr * S6;
+      if (PLANES) {
+        const int d0 = 32 * (c / (4 * NP)) + 8 * (c % 4);
+        const bool lo_plane = NP == 2 && ((c >> 2) & 1);
+        uint32_t w[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const floatx2 v = *reinterpret_cast<const floatx2*>(src + d0 + 2 * e);
+          const __bf16 hx = (__bf16)v.x, hy = (__bf16)v.y;
+          bf16x2 pr;
+          if (lo_plane) pr = bf16x2{(__bf16)(v.x - (float)hx), (__bf16)(v.y - (float)hy)};
+          else pr = bf16x2{hx, hy};
+          w[e] = __builtin_bit_cast(uint32_t, pr);
+        }
+        if (qq < nq) {
+          unsigned short* dst = op + (size_t)(start + qq) * NP * AE_HIDDEN + head * 64 * NP + c * 8;
+          *reinterpret_cast<u32x4*>(dst) = u32x4{w[0], w[1], w[2], w[3]};
+        }
+      } else {
+        const floatx2 a = *reinterpret_cast<const floatx2*>(src + 4 * c);
+        const floatx2 e = *reinterpret_cast<const floatx2*>(src + 4 * c + 2);
+        if (qq < nq)
+          *reinterpret_cast<floatx4*>(out + (size_t)(start + qq) * AE_HIDDEN + head * AE_HEAD_DIM + 4 * c) =
+              floatx4{a.x, a.y, e.x, e.y};
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // block A's rows read before B's land
+  }
+}
+
 // qkvp: packed planes [T][np·2304] with Q pre-scaled by log2(e)/8; context to op (packed planes)
 // or out (f32 [T, 768]).  q_rows / max_q: the CLS-only launch of the last layer.
 namespace {
@@ -677,6 +1073,25 @@ hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op
 #undef APP_LAUNCH
   return hipGetLastError();
 }
+#ifdef AE_TOOLS
+// PIPE 80 (attn_pq_kernel): 4-wave workgroups of 256 queries, no mask
+template <int NSL, int DIAG = 0, bool KH = false>
+hipError_t apq_launch(const unsigned short* qkvp, float* out, unsigned short* op, const int* cu,
+                      const int* q_rows, int max_q, int n, int heads, int np, hipStream_t stream) {
+  if (n <= 0 || max_q <= 0) return hipSuccess;
+  if (np != 1 && np != 2) return hipErrorInvalidValue;
+  constexpr int NW = 4;
+  dim3 grid((max_q + 64 * NW - 1) / (64 * NW), heads, n), block(64 * NW);
+#define APQ(N, PL) hipLaunchKernelGGL((attn_pq_kernel<N, PL, NW, true, NSL, DIAG, KH>), grid, block, 0, stream, qkvp, out, op, cu, q_rows)
+  if (np == 2) {
+    if (op) APQ(2, true); else APQ(2, false);
+  } else {
+    if (op) APQ(1, true); else APQ(1, false);
+  }
+#undef APQ
+  return hipGetLastError();
+}
+#endif  // AE_TOOLS
 // production loop: PIPE 66 = PIPE 6 with saddr DMA and the permlane row max, at three
 // workgroups per CU (168 registers): packed-plane output (the engine's launch), B=64 x L=512, same
 // box, interleaved rounds: pp6 192.3 / pp66 172.2 us median, ragged 138.6 / 123.5
@@ -731,6 +1146,18 @@ extern "C" hipError_t ae_bench_attention_pp(const unsigned short* qkvp, float* o
     case 66: return app_launch<66>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
     case 67: return app_launch<67>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
     case 72: return app_launch<72>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
+    case 80: return mask ? app_launch<67>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream)
+                         : apq_launch<2>(qkvp, out, op, cu, q_rows, max_q, n, heads, np, stream);
+    case 81: return mask ? app_launch<67>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream)
+                         : apq_launch<3>(qkvp, out, op, cu, q_rows, max_q, n, heads, np, stream);
+    // timing diagnostics of 81 (results WRONG): 82 no LDS fragment reads, 83 no end-of-tile wait /
+    // barrier, 84 no exp / split, 85 no DMA after the prologue and no waits
+    case 82: return apq_launch<3, 1>(qkvp, out, op, cu, q_rows, max_q, n, heads, np, stream);
+    case 83: return apq_launch<3, 2>(qkvp, out, op, cu, q_rows, max_q, n, heads, np, stream);
+    case 84: return apq_launch<3, 3>(qkvp, out, op, cu, q_rows, max_q, n, heads, np, stream);
+    case 85: return apq_launch<3, 4>(qkvp, out, op, cu, q_rows, max_q, n, heads, np, stream);
+    case 86: return mask ? app_launch<67>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream)
+                         : apq_launch<3, 0, true>(qkvp, out, op, cu, q_rows, max_q, n, heads, np, stream);
     default: break;
   }
   return hipErrorInvalidValue;

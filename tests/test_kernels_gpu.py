@@ -246,7 +246,7 @@ def _qkv_planes(qkv, np_):
     return _pack(hi, lo, np_)
 
 
-@pytest.mark.parametrize("variant", [6, 66, 67, 72])
+@pytest.mark.parametrize("variant", [6, 66, 67, 72, 80, 81, 86])
 @pytest.mark.parametrize("np_", [2, 1])
 @pytest.mark.parametrize("case", ["ragged", "mask", "cls", "planes", "grow"])
 def test_attention_pp_matches_f64(gpu, np_, case, variant):
@@ -341,7 +341,7 @@ def test_attention_pp_restructured_loops_bit_identical(gpu, case):
     dq, dcu = _qkv_planes(qkv, 2).cuda(), cu.cuda()
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     outs = {}
-    for v in (6, 66, 67, 72):
+    for v in (6, 66, 67, 72, 80, 81, 86):
         op = torch.zeros((T, 2 * 768), dtype=torch.int16, device="cuda")
         assert lib.ae_bench_attention_pp(_p(dq), None, _p(op), _p(dcu), None, max(lens), n, 12,
                                          None, 0, 2, v, st) == 0
@@ -350,6 +350,9 @@ def test_attention_pp_restructured_loops_bit_identical(gpu, case):
     assert torch.equal(outs[66], outs[6])
     assert torch.equal(outs[67], outs[6])
     assert torch.equal(outs[72], outs[6])  # exp / split and the next S MFMAs hand-interleaved
+    assert torch.equal(outs[80], outs[6])  # two 32-query blocks per wave, 256-query workgroups
+    assert torch.equal(outs[81], outs[6])  # the same with 3-slot K / V rings
+    assert torch.equal(outs[86], outs[6])  # 81 with the K fragments read once for both blocks
 
 
 def _fold_lib():

@@ -393,4 +393,19 @@ def test_encode_rows_matches_full_last_layer(gpu, precision):
         # a column past lens, or a dropped pad column, is left untouched (zeros, like encode_ex)
         assert not np.abs(win[3, 1:]).any()
         assert np.isfinite(win).all()
+    # the whole sequence as the window (every row a query of the absorbed last layer), one row
+    ids = rng.integers(4, 50264, size=(3, 96)).astype(np.int32)
+    ids[:, 0], ids[:, -1] = 0, 2
+    lens = np.array([96, 96, 96], np.int32)
+    dev = torch.from_numpy(ids).cuda()
+    full = eng.encode(dev, lens, attend_pad=True).cpu().numpy()
+    win = eng.encode_rows(dev, lens, np.zeros(3, np.int32), 96, attend_pad=True).cpu().numpy()
+    print(f"{precision} whole-row window: max |rows - full| {np.abs(win - full).max():.2e}")
+    assert np.abs(win - full).max() <= tol
+    one = eng.encode_rows(dev[1:2], lens[1:2], np.array([40], np.int32), 1,
+                          attend_pad=True).cpu().numpy()
+    assert np.abs(one[0, 0] - full[1, 40]).max() <= tol
+    # argument validation before any device work: a window past L
+    with pytest.raises(RuntimeError, match="window"):
+        eng.encode_rows(dev, lens, np.array([0, 0, 95], np.int32), 2, attend_pad=True)
     eng.close()
