@@ -1,4 +1,4 @@
-# round 6: config 3 at its stated size in two calls: bash scripts/c5.sh START END
+# round 6: config 3 at its stated size in two calls: bash scripts/c6.sh START END
 set -o pipefail
 mkdir -p gpurun_out/c6
 timeout -k 10 1080 python -u tools/get_substitutes.py --eval_data_file data/devign/test_funcs.jsonl \
