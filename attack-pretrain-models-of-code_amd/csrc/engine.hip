@@ -33,6 +33,14 @@ hipError_t ae_launch_attention_pp(const unsigned short*, float*, unsigned short*
 hipError_t ae_bench_attention_pp(const unsigned short*, float*, unsigned short*, const int*,
                                  const int*, int, int, int, const uint32_t*, int, int, int,
                                  hipStream_t);
+hipError_t ae_bench_gemm_packed_fold(const unsigned short*, const unsigned short*, const float*,
+                                     const float*, const uint64_t*, float, unsigned short*, int,
+                                     int, int, int, int, const float*, int, int, hipStream_t);
+hipError_t ae_bench_gemm_packed_res_stats(const unsigned short*, const unsigned short*,
+                                          const float*, const float*, const uint64_t*,
+                                          const float*, const float*, float, float*,
+                                          unsigned short*, uint64_t*, int, int, int, int,
+                                          const float*, int, int, hipStream_t);
 #endif
 hipError_t ae_launch_gemm_packed(const unsigned short*, const unsigned short*, const float*,
                                  const float*, float*, unsigned short*, int, int, int, int, int,
@@ -173,6 +181,9 @@ struct ae_engine {
   // experiments (AE_ATTN_VARIANT, tools/engine_ab.py): an attention_pp loop variant other than the
   // production one for the unmasked launches (0 = production)
   int attn_variant = 0;
+  // experiments (AE_GEMM_P2, tools/engine_ab.py): bit 1 QKV, 2 FFN1, 4 O-projection, 8 FFN2 on
+  // the two-per-CU 128 x 192 kernel (gemm_p2_kernel) instead of the production launch
+  int gemm_p2 = 0;
   hipStream_t sts[kMaxParts] = {};  // sts[0] unused: part 0 runs on the caller's stream
   hipEvent_t ev_fork = nullptr, ev_lag[kMaxParts] = {}, ev_join[kMaxParts] = {};
   // profiling: event pairs are created when profiling is switched on (never inside the timed
@@ -504,6 +515,12 @@ int layer_rows(ae_engine* e, int li, int64_t t0, int M, int s0, int ns, int max_
   const bool prof = e->prof_kind == AE_KIND_GEMM_ANY;
   {
     Prof p(e, st, prof, 2.0 * M * 3 * H * H);
+#ifdef AE_TOOLS
+    if (prev && (e->gemm_p2 & 1))
+      HIPC(ae_bench_gemm_packed_fold(xp, w.wqkv_p, w.bqkv_f, w.sqkv, sa, eps, qkvp, M, 3 * H, H, 0,
+                                     np, w.kcqkv, 1, 0, st));
+    else
+#endif
     if (prev)
       HIPC(ae_launch_gemm_packed_fold(xp, w.wqkv_p, w.bqkv_f, w.sqkv, sa, eps, qkvp, M, 3 * H, H,
                                       0, np, w.kcqkv, st));
@@ -521,6 +538,14 @@ int layer_rows(ae_engine* e, int li, int64_t t0, int M, int s0, int ns, int max_
   if (int rc = done()) return rc;
   {
     Prof p(e, st, prof, 2.0 * M * H * H);
+#ifdef AE_TOOLS
+    if (e->gemm_p2 & 4)
+      HIPC(ae_bench_gemm_packed_res_stats(cp, w.wo_p, w.bo, prev ? v : e->x + t0 * H,
+                                          prev ? sa : nullptr, prev ? prev->ln2g : nullptr,
+                                          prev ? prev->ln2b : nullptr, eps, v, xp, sb, M, H, H, np,
+                                          w.kap_o, 1, 0, st));
+    else
+#endif
     HIPC(ae_launch_gemm_packed_res_stats(cp, w.wo_p, w.bo, prev ? v : e->x + t0 * H,
                                          prev ? sa : nullptr, prev ? prev->ln2g : nullptr,
                                          prev ? prev->ln2b : nullptr, eps, v, xp, sb, M, H, H, np,
@@ -529,12 +554,24 @@ int layer_rows(ae_engine* e, int li, int64_t t0, int M, int s0, int ns, int max_
   if (int rc = done()) return rc;
   {
     Prof p(e, st, prof || e->prof_kind == AE_KIND_GEMM_FFN1, 2.0 * M * F * H);
+#ifdef AE_TOOLS
+    if (e->gemm_p2 & 2)
+      HIPC(ae_bench_gemm_packed_fold(xp, w.w1_p, w.b1_f, w.s1, sb, eps, hp, M, F, H, 1, np, w.kc1,
+                                     1, 0, st));
+    else
+#endif
     HIPC(ae_launch_gemm_packed_fold(xp, w.w1_p, w.b1_f, w.s1, sb, eps, hp, M, F, H, 1, np, w.kc1,
                                     st));
   }
   if (int rc = done()) return rc;
   {
     Prof p(e, st, prof, 2.0 * M * H * F);
+#ifdef AE_TOOLS
+    if (e->gemm_p2 & 8)
+      HIPC(ae_bench_gemm_packed_res_stats(hp, w.w2_p, w.b2, v, sb, w.ln1g, w.ln1b, eps, v, xp, sa,
+                                          M, H, F, np, w.kap_f, 1, 0, st));
+    else
+#endif
     HIPC(ae_launch_gemm_packed_res_stats(hp, w.w2_p, w.b2, v, sb, w.ln1g, w.ln1b, eps, v, xp, sa,
                                          M, H, F, np, w.kap_f, st));
   }
@@ -914,6 +951,8 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
       }
       e->attn_variant = v == 67 ? 0 : v;
     }
+    const char* g2 = std::getenv("AE_GEMM_P2");  // experiments: bit mask, see ae_engine::gemm_p2
+    if (g2) e->gemm_p2 = std::atoi(g2) & 15;
     const char* parts = std::getenv("AE_SPLIT_PARTS");  // experiments: 2 (default) .. 4
     if (parts && parts[0] >= '2' && parts[0] <= '4') e->split_parts = parts[0] - '0';
 #endif

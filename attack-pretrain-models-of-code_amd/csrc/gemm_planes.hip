@@ -1080,9 +1080,11 @@ int cu_count();
 template <int NP, int EPI, int V = 0>
 __global__ __launch_bounds__(256, 2) void gemm_p2_kernel(
     const __bf16* __restrict__ A, const __bf16* __restrict__ W, const float* __restrict__ bias,
-    const float* R, float* C, int M, int N, int K, int group_m, StatArgs ln) {
+    const float* R, float* C, int M, int N, int K, int group_m, StatArgs ln, FoldArgs fold) {
   extern __shared__ __attribute__((aligned(16))) unsigned char pk_smem[];
-  static_assert(EPI == PK_EPI_RES_STATS || EPI == PK_EPI_RES_STATS_LN, "statistics epilogues only");
+  constexpr bool FOLD = EPI == PK_EPI_GELU_FOLD || EPI == PK_EPI_BIAS_FOLD;
+  static_assert(EPI == PK_EPI_RES_STATS || EPI == PK_EPI_RES_STATS_LN || FOLD,
+                "statistics or folded-LayerNorm epilogues only");
   constexpr int BM = 128, BN = 192, ROWB = PK_ROWB;
   constexpr int A_BYTES = BM * ROWB, STAGE = (BM + BN) * ROWB;  // 40 KiB per K-tile
   constexpr int KB = 64 / NP, NS = KB / 16, T = NP == 2 ? 3 : 1;
@@ -1132,6 +1134,23 @@ __global__ __launch_bounds__(256, 2) void gemm_p2_kernel(
   const uint32_t SIDE = side_stage * STAGE + STAGE - 8192;  // bias | gamma | beta | shift | rstats
   constexpr bool rnorm = EPI == PK_EPI_RES_STATS_LN;
   auto issue_side = [&]() {
+    if constexpr (FOLD) {  // bias' | s | kc | the tile rows' statistics (FoldArgs)
+      if (wave == 0) {
+        dma16(bias + n0 + 4 * min(lane, 47), lds0 + SIDE);
+      } else if (wave == 1) {
+        dma16(fold.s + n0 + 4 * min(lane, 47), lds0 + SIDE + 1024);
+      } else if (wave == 2) {
+        if (fold.kc) dma16(fold.kc + n0 + 4 * min(lane, 47), lds0 + SIDE + 2048);
+      } else {
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const int r0 = h * 32;
+          dma16(fold.stats + (size_t)min(m0 + r0 + (lane >> 1), M - 1) * 4 + 2 * (lane & 1),
+                lds0 + SIDE + 4096 + (uint32_t)(r0 * 32));
+        }
+      }
+      return;
+    }
     if (wave == 0) {
       dma16(bias + n0 + 4 * min(lane, 47), lds0 + SIDE);
     } else if (wave == 1) {
@@ -1254,6 +1273,73 @@ __global__ __launch_bounds__(256, 2) void gemm_p2_kernel(
   }
   // every wave is past its last fragment reads (the loop's second barrier); the side data landed
   // with each issuer's final vmcnt(0) before the last K-tile's first barrier
+  if constexpr (FOLD) {
+    // ---- folded LayerNorm (gemm_pp_kernel's PK_EPI_*_FOLD for a 128 x 192 tile): y = rstd ·
+    // ((acc + kc) − mean · s) + bias', GELU'd for FFN1, staged per 32-row half in the wave's LDS
+    // rows and stored as packed planes with 16-B lanes.  kc (the plane shift's accumulator start)
+    // is added here rather than preloaded: it lands with the epilogue's side data.
+    constexpr int RS = 400;
+    unsigned char* reg = pk_smem + (wave < 3 ? (side_stage ^ 1) * STAGE + wave * 32 * RS
+                                             : side_stage * STAGE);
+    const float* const colt = reinterpret_cast<const float*>(pk_smem + SIDE);
+    const uint64_t* const fst = reinterpret_cast<const uint64_t*>(pk_smem + SIDE + 4096);
+    const int cb0 = n0 + sn * 96, prow0 = m0 + sm * 64;
+    const bool has_kc = fold.kc != nullptr;
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm) {
+      float mu, rs;
+      row_norm(fst + (sm * 64 + tm * 32 + li) * 4, fold.eps, mu, rs);
+#pragma unroll
+      for (int tn = 0; tn < 3; ++tn) {
+        gelu_f2 y[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int tc = sn * 96 + tn * 32 + 8 * j + 4 * lh;  // column within the tile
+          const floatx4 bv = *reinterpret_cast<const floatx4*>(colt + tc);
+          const floatx4 sv = *reinterpret_cast<const floatx4*>(colt + 256 + tc);
+          floatx4 kv = {0.f, 0.f, 0.f, 0.f};
+          if (has_kc) kv = *reinterpret_cast<const floatx4*>(colt + 512 + tc);
+#pragma unroll
+          for (int i = 0; i < 4; i += 2) {
+            const gelu_f2 a = gelu_f2{acc[tm][tn][4 * j + i], acc[tm][tn][4 * j + i + 1]} +
+                              gelu_f2{kv[i], kv[i + 1]};
+            y[2 * j + i / 2] = __builtin_elementwise_fma(
+                __builtin_elementwise_fma(gelu_f2{sv[i], sv[i + 1]}, gelu_f2(-mu), a), gelu_f2(rs),
+                gelu_f2{bv[i], bv[i + 1]});
+          }
+        }
+        if constexpr (EPI == PK_EPI_GELU_FOLD) gelu_exp2_pairs(y);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          *reinterpret_cast<floatx4*>(reg + li * RS + (tn * 8 + 2 * j + lh) * 16) =
+              floatx4{y[2 * j].x, y[2 * j].y, y[2 * j + 1].x, y[2 * j + 1].y};
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own rows: no barrier
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const int kk = k % 3, g2 = k / 3;
+        const int idx = kk * 64 + lane, lr = idx / 12 + 16 * g2, c8 = idx % 12;
+        const int row = prow0 + tm * 32 + lr;
+        const floatx4 o0 = *reinterpret_cast<const floatx4*>(reg + lr * RS + c8 * 32);
+        const floatx4 o1 = *reinterpret_cast<const floatx4*>(reg + lr * RS + c8 * 32 + 16);
+        if (row < M) {
+          const int col = cb0 + 8 * c8;
+          uint32_t h[4], l[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            split_pair(i < 2 ? gelu_f2{o0[2 * i], o0[2 * i + 1]} : gelu_f2{o1[2 * i - 4], o1[2 * i - 3]},
+                       h[i], l[i]);
+          unsigned short* dstp = reinterpret_cast<unsigned short*>(ln.xp) + (size_t)prow0 * NP * N +
+                                 (uint32_t)(lr + tm * 32) * (uint32_t)(NP * N) +
+                                 (uint32_t)((col >> 5) * 32 * NP + (col & 31));
+          *reinterpret_cast<uint4*>(dstp) = uint4{h[0], h[1], h[2], h[3]};
+          if (NP == 2) *reinterpret_cast<uint4*>(dstp + 32) = uint4{l[0], l[1], l[2], l[3]};
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read back before the next half lands
+    }
+    return;
+  }
 
   // ---- v = (acc + bias) + residual as f32 and packed planes of v - shift, plus this tile's
   // (mean, M2) of every row (gemm_pp192_kernel's epilogue for a 128-row tile; see there).
@@ -1452,13 +1538,14 @@ hipError_t pp192_launch(const __bf16* A, const __bf16* W, const float* bias, con
 
 template <int NP, int EPI, int V = 0>
 hipError_t p2_launch(const __bf16* A, const __bf16* W, const float* bias, const float* R, float* C,
-                     int M, int N, int K, int group_m, hipStream_t st, StatArgs ln) {
+                     int M, int N, int K, int group_m, hipStream_t st, StatArgs ln,
+                     FoldArgs fold = FoldArgs{}) {
   constexpr int lds = 2 * (128 + 192) * PK_ROWB;  // 80 KiB: two workgroups per CU
   if (hipError_t e = ensure_dynamic_lds((const void*)gemm_p2_kernel<NP, EPI, V>, lds); e != hipSuccess)
     return e;
   const int tiles = ((M + 127) / 128) * ((N + 191) / 192);
   hipLaunchKernelGGL((gemm_p2_kernel<NP, EPI, V>), dim3(tiles), dim3(256), lds, st, A, W, bias, R,
-                     C, M, N, K, group_m, ln);
+                     C, M, N, K, group_m, ln, fold);
   return hipGetLastError();
 }
 
@@ -1677,6 +1764,35 @@ extern "C" hipError_t ae_bench_gemm_packed_res_stats(
                    : p2_launch<1, PK_EPI_RES_STATS_LN>(a, w, bias, R, C, M, N, K, gm, st, ln);
   return np == 2 ? p2_launch<2, PK_EPI_RES_STATS>(a, w, bias, R, C, M, N, K, gm, st, ln)
                  : p2_launch<1, PK_EPI_RES_STATS>(a, w, bias, R, C, M, N, K, gm, st, ln);
+}
+
+// ae_launch_gemm_packed_fold with an explicit kernel: variant 0 = gemm_pp_kernel (one 256 x 256
+// workgroup per CU, the production launch), 1 = gemm_p2_kernel (two 128 x 192 workgroups per CU,
+// M-tiles grouped by `group` (0: 8), kc added in the epilogue instead of preloaded: equal to the
+// production results up to f32 rounding).  N % 192 == 0.
+extern "C" hipError_t ae_bench_gemm_packed_fold(const unsigned short* A, const unsigned short* W,
+                                                const float* bias, const float* s,
+                                                const uint64_t* stats, float eps,
+                                                unsigned short* Cp, int M, int N, int K, int gelu,
+                                                int np, const float* kc, int variant, int group,
+                                                hipStream_t st) {
+  if (variant == 0)
+    return ae_launch_gemm_packed_fold(A, W, bias, s, stats, eps, Cp, M, N, K, gelu, np, kc, st);
+  if (M <= 0) return hipSuccess;
+  if (variant != 1 || N % 192 != 0 || K % 64 != 0 || (np != 1 && np != 2) || !bias || !s ||
+      !stats || !Cp)
+    return hipErrorInvalidValue;
+  StatArgs ln{};
+  ln.xp = reinterpret_cast<__bf16*>(Cp);
+  const FoldArgs fold{s, stats, eps, kc};
+  auto a = reinterpret_cast<const __bf16*>(A);
+  auto w = reinterpret_cast<const __bf16*>(W);
+  const int gm = group > 0 ? group : 8;
+  if (np == 2)
+    return gelu ? p2_launch<2, PK_EPI_GELU_FOLD>(a, w, bias, nullptr, nullptr, M, N, K, gm, st, ln, fold)
+                : p2_launch<2, PK_EPI_BIAS_FOLD>(a, w, bias, nullptr, nullptr, M, N, K, gm, st, ln, fold);
+  return gelu ? p2_launch<1, PK_EPI_GELU_FOLD>(a, w, bias, nullptr, nullptr, M, N, K, gm, st, ln, fold)
+              : p2_launch<1, PK_EPI_BIAS_FOLD>(a, w, bias, nullptr, nullptr, M, N, K, gm, st, ln, fold);
 }
 
 // Kernel experiments (tools/gemm_bench.py, tests): explicit tile width (0 = the production choice)

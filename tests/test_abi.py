@@ -52,8 +52,8 @@ def test_product_library_has_no_experiment_entry_points():
     assert b"AE_ATTN_VARIANT" not in LIB_PATH.read_bytes()
     assert b"AE_SPLIT_STREAMS" not in LIB_PATH.read_bytes()
     tools = _dynamic_symbols(TOOLS_LIB_PATH)
-    for s in ("ae_bench_gemm_packed", "ae_bench_attention_pp",
-              "ae_bench_attention_x3"):
+    for s in ("ae_bench_gemm_packed", "ae_bench_attention_pp", "ae_bench_attention_x3",
+              "ae_bench_gemm_packed_res_stats", "ae_bench_gemm_packed_fold"):
         assert s in tools, s
     assert set(declared_symbols()) <= tools
 

@@ -363,6 +363,8 @@ def _fold_lib():
     lib.ae_launch_gemm_packed_res_stats.argtypes = [vp] * 7 + [f32] + [vp] * 3 + [i32] * 4 + \
         [vp, vp]
     lib.ae_launch_gemm_packed_res_stats.restype = ctypes.c_int
+    lib.ae_bench_gemm_packed_fold.argtypes = [vp] * 5 + [f32, vp] + [i32] * 5 + [vp, i32, i32, vp]
+    lib.ae_bench_gemm_packed_fold.restype = ctypes.c_int
     return lib
 
 
@@ -460,10 +462,11 @@ def test_gemm_packed_res_stats_matches_f64(gpu, M, K, np_, shift, variant):
         prev = got
 
 
+@pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("M,N,np_,gelu,shift", [
     (300, 2304, 2, 0, 0), (4100, 3072, 2, 1, 0), (37, 3072, 2, 1, 0), (1000, 2304, 1, 0, 0),
     (600, 3072, 1, 1, 0), (300, 2304, 2, 0, 1), (4100, 3072, 2, 1, 1), (600, 3072, 1, 1, 1)])
-def test_gemm_packed_fold_matches_f64(gpu, M, N, np_, gelu, shift):
+def test_gemm_packed_fold_matches_f64(gpu, M, N, np_, gelu, shift, variant):
     """ae_launch_gemm_packed_fold (256 x 256 kernel, PK_EPI_BIAS_FOLD / PK_EPI_GELU_FOLD): the
     QKV / FFN1 GEMM over PRE-LayerNorm rows v with the LayerNorm folded in,
         y = rstd · (v·W'^T - mean · s) + bias',  W' = W·diag(gamma), s = rowsums(W'),
@@ -472,7 +475,8 @@ def test_gemm_packed_fold_matches_f64(gpu, M, N, np_, gelu, shift):
     the mean · s cancellation is exercised.  Packed-plane output.  With shift (the plane shift):
     v carries per-column constants kappa (|kappa| ~ 3, outlier columns at 30-40), the A planes
     hold v - kappa and the accumulators start at kc = kappa·W'^T — the split error then scales
-    with |v - kappa|, which the tolerance states."""
+    with |v - kappa|, which the tolerance states.  Variant 1: the two-per-CU 128 x 192 kernel
+    (tools library, ae_bench_gemm_packed_fold; kc added in its epilogue)."""
     lib = _fold_lib()
     K = 768
     g = torch.Generator().manual_seed(3 * M + N + gelu)
@@ -498,8 +502,12 @@ def test_gemm_packed_fold_matches_f64(gpu, M, N, np_, gelu, shift):
     dkc = (held @ kap.double()).float().cuda() if shift else None
     dst = _tile_stats(v).cuda()
     out = torch.zeros((M, np_ * N), dtype=torch.bfloat16, device="cuda")
-    rc = lib.ae_launch_gemm_packed_fold(_p(dv), _p(dW), _p(dbf), _p(ds), _p(dst), 1e-5, _p(out),
-                                        M, N, K, gelu, np_, _p(dkc), st)
+    if variant == 0:
+        rc = lib.ae_launch_gemm_packed_fold(_p(dv), _p(dW), _p(dbf), _p(ds), _p(dst), 1e-5,
+                                            _p(out), M, N, K, gelu, np_, _p(dkc), st)
+    else:
+        rc = lib.ae_bench_gemm_packed_fold(_p(dv), _p(dW), _p(dbf), _p(ds), _p(dst), 1e-5,
+                                           _p(out), M, N, K, gelu, np_, _p(dkc), variant, 0, st)
     assert rc == 0
     torch.cuda.synchronize()
     x, var = _ln64(v, gamma, beta)

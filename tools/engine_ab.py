@@ -1,6 +1,6 @@
 """Same-box A/B of engine configurations on the bench's scoring step (GPU): one engine per
 configuration (each built under its own AE_* environment — AE_ATTN_VARIANT, AE_SPLIT_STREAMS,
-AE_SPLIT_PARTS, AE_SPLIT_LAG), interleaved rounds of `--steps` steps each in one process, on a
+AE_SPLIT_PARTS, AE_SPLIT_LAG, AE_GEMM_P2), interleaved rounds of `--steps` steps each in one process, on a
 full-length and a ragged B=64 x L=512 batch, with the max |dp| of each against the first.
 
   python tools/engine_ab.py --configs "prod:;pp6:AE_ATTN_VARIANT=6" [--steps 10] [--rounds 7]
@@ -16,7 +16,7 @@ import time
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 KNOBS = ("AE_ATTN_VARIANT", "AE_SPLIT_STREAMS", "AE_SPLIT_PARTS", "AE_SPLIT_LAG",
-         "AE_CLS_ABSORB")
+         "AE_CLS_ABSORB", "AE_GEMM_P2")
 
 
 def main():

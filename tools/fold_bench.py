@@ -30,8 +30,9 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--lib", default=None)
     ap.add_argument("--p2", action="store_true",
-                    help="also the two-per-CU 128 x 192 kernel of the statistics epilogues "
-                         "(tools library, ae_bench_gemm_packed_res_stats variant 1)")
+                    help="also the two-per-CU 128 x 192 kernel (tools library): the statistics "
+                         "epilogues (ae_bench_gemm_packed_res_stats variants 1 / 2) and the folded "
+                         "QKV / FFN1 (ae_bench_gemm_packed_fold variant 1)")
     ap.add_argument("--only", default=None, help="comma-separated launch names")
     args = ap.parse_args()
     from apmc_amd.engine import load_library
@@ -91,6 +92,14 @@ def main():
                         lib.ae_bench_gemm_packed_res_stats(
                             p(a_), p(w_), p(bias), p(rv), p(stats), p(gam), p(bet), 1e-5, p(v),
                             p(vp_), p(ostats), M, H, K_, 2, p(kap), var, grp, st))
+    if args.p2:
+        lib.ae_bench_gemm_packed_fold.argtypes = [vp] * 5 + [f32, vp] + [i32] * 5 + [vp, i32, i32, vp]
+        for nm, gl, N_ in (("qkv", 0, 3 * H), ("ffn1", 1, F)):
+            for grp in (8, 4, 16):
+                calls[f"{nm}_fold_p2_g{grp}"] = (
+                    lambda gl=gl, N_=N_, grp=grp, nm=nm:
+                    lib.ae_bench_gemm_packed_fold(p(x), p(w[nm]), p(bias), p(s), p(stats), 1e-5,
+                                                  p(outp), M, N_, H, gl, 2, p(kc), 1, grp, st))
     if args.only:
         calls = {k: c for k, c in calls.items() if k in args.only.split(",")}
     ts = {k: [] for k in calls}
