@@ -959,7 +959,19 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
     if (e->split) {
       HIPC(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
       for (int p = 0; p < ae_engine::kMaxParts; ++p) {
-        if (p > 0) HIPC(hipStreamCreateWithFlags(&e->sts[p], hipStreamNonBlocking));
+        if (p > 0) {
+          int prio = 0;
+#ifdef AE_TOOLS
+          // experiments (AE_SPLIT_PRIO): the lagging parts' streams at the lowest ("lo") or the
+          // highest ("hi") stream priority instead of the default
+          if (const char* sp2 = std::getenv("AE_SPLIT_PRIO")) {
+            int least = 0, greatest = 0;
+            HIPC(hipDeviceGetStreamPriorityRange(&least, &greatest));
+            prio = sp2[0] == 'h' ? greatest : sp2[0] == 'l' ? least : 0;
+          }
+#endif
+          HIPC(hipStreamCreateWithPriority(&e->sts[p], hipStreamNonBlocking, prio));
+        }
         HIPC(hipEventCreateWithFlags(&e->ev_lag[p], hipEventDisableTiming));
         HIPC(hipEventCreateWithFlags(&e->ev_join[p], hipEventDisableTiming));
       }

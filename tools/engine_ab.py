@@ -16,7 +16,7 @@ import time
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 KNOBS = ("AE_ATTN_VARIANT", "AE_SPLIT_STREAMS", "AE_SPLIT_PARTS", "AE_SPLIT_LAG",
-         "AE_CLS_ABSORB", "AE_GEMM_P2")
+         "AE_CLS_ABSORB", "AE_GEMM_P2", "AE_SPLIT_PRIO")
 
 
 def main():
