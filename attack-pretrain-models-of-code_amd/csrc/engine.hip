@@ -960,17 +960,20 @@ int ae_create(const ae_config* cfg, const ae_weight_view* weights, int32_t n_wei
       HIPC(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
       for (int p = 0; p < ae_engine::kMaxParts; ++p) {
         if (p > 0) {
-          int prio = 0;
+          const char* sp2 = nullptr;
 #ifdef AE_TOOLS
           // experiments (AE_SPLIT_PRIO): the lagging parts' streams at the lowest ("lo") or the
           // highest ("hi") stream priority instead of the default
-          if (const char* sp2 = std::getenv("AE_SPLIT_PRIO")) {
+          sp2 = std::getenv("AE_SPLIT_PRIO");
+#endif
+          if (sp2) {
             int least = 0, greatest = 0;
             HIPC(hipDeviceGetStreamPriorityRange(&least, &greatest));
-            prio = sp2[0] == 'h' ? greatest : sp2[0] == 'l' ? least : 0;
+            HIPC(hipStreamCreateWithPriority(&e->sts[p], hipStreamNonBlocking,
+                                             sp2[0] == 'h' ? greatest : least));
+          } else {
+            HIPC(hipStreamCreateWithFlags(&e->sts[p], hipStreamNonBlocking));
           }
-#endif
-          HIPC(hipStreamCreateWithPriority(&e->sts[p], hipStreamNonBlocking, prio));
         }
         HIPC(hipEventCreateWithFlags(&e->ev_lag[p], hipEventDisableTiming));
         HIPC(hipEventCreateWithFlags(&e->ev_join[p], hipEventDisableTiming));
