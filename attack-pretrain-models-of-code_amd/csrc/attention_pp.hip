@@ -129,11 +129,11 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && !(HAS_MASK && NP == 2)) ? 3 : 2
   // PIPE 66: PIPE 6 with saddr DMA (per-lane offsets computed once, tiles advanced on the scalar
   // unit) and the cross-half row max by v_permlane32_swap instead of an LDS permute.
   // PIPE 67: 66 with the tile max as a 3-level tree of v_max3 (depth 3 instead of a chain of 8).
-  static_assert(PIPE == 4 || PIPE == 6 || PIPE == 66 || PIPE == 67 || PIPE == 72,
-                "loop variants 4, 6, 66, 67, 72");
+  static_assert(PIPE == 4 || PIPE == 6 || PIPE == 66 || PIPE == 67 || PIPE == 72 || PIPE == 74,
+                "loop variants 4, 6, 66, 67, 72, 74");
   constexpr int PB = PIPE >= 60 ? 6 : PIPE;
   constexpr bool FAST = PIPE >= 60;
-  constexpr bool TREE = PIPE == 67 || PIPE == 72;
+  constexpr bool TREE = PIPE == 67 || PIPE == 72 || PIPE == 74;
   static_assert(!(HAS_MASK && PB == 6 && !FAST),
                 "PIPE 6 has no mask path (its loop keeps no ordinary global load, so its mask "
                 "launches run PIPE 4); PIPE 66 moves the mask words by LDS-DMA");
@@ -465,14 +465,25 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && !(HAS_MASK && NP == 2)) ? 3 : 2
           uint32_t mb = 0xffffffffu;
           if constexpr (HAS_MASK)
             mb = *reinterpret_cast<const uint32_t*>(lds + MASK_OFF + (R % 3) * 1024 + wave * 256 + 4 * li);
+          // PIPE 74 (masked launches): a full tile whose mask words are all ones for every query
+          // of the wave (GraphCodeBERT's code rows over code keys) takes the tree max with no
+          // per-key select — the same scores, so the same bits
+          if (PIPE == 74 && (kt + 1) * KT <= len && __all(mb == 0xffffffffu)) {
+            float a[6];
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int kk = mfma32_row(r, lh);
-            // absent keys -inf; keys the mask excludes the most negative finite float (HF's
-            // additive finfo.min mask), as tile_max
-            const bool in = kt * KT + kk < len;
-            s_cur[r] = !in ? -INFINITY : (((mb >> kk) & 1u) ? s_cur[r] : -FLT_MAX);
-            mt = max_nc(mt, s_cur[r]);
+            for (int r = 0; r < 5; ++r) a[r] = max_nc(s_cur[3 * r], max_nc(s_cur[3 * r + 1], s_cur[3 * r + 2]));
+            a[5] = s_cur[15];
+            mt = max_nc(max_nc(a[0], max_nc(a[1], a[2])), max_nc(a[3], max_nc(a[4], a[5])));
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int kk = mfma32_row(r, lh);
+              // absent keys -inf; keys the mask excludes the most negative finite float (HF's
+              // additive finfo.min mask), as tile_max
+              const bool in = kt * KT + kk < len;
+              s_cur[r] = !in ? -INFINITY : (((mb >> kk) & 1u) ? s_cur[r] : -FLT_MAX);
+              mt = max_nc(mt, s_cur[r]);
+            }
           }
         }
         if constexpr (FAST) {
@@ -1055,7 +1066,7 @@ hipError_t app_launch(const unsigned short* qkvp, float* out, unsigned short* op
   if (np != 1 && np != 2) return hipErrorInvalidValue;
   dim3 grid((max_q + QPB - 1) / QPB, heads, n), block(256);
 #define APP_LAUNCH(N, M, PL)                                                                 \
-  hipLaunchKernelGGL((attn_pp_kernel<N, M, PL, M ? (PIPE == 72 ? 72 : PIPE >= 60 ? 66 : 4) : PIPE>), grid, block, 0, \
+  hipLaunchKernelGGL((attn_pp_kernel<N, M, PL, M ? (PIPE == 72 ? 72 : PIPE == 74 ? 74 : PIPE >= 60 ? 66 : 4) : (PIPE == 74 ? 67 : PIPE)>), grid, block, 0, \
                      stream, qkvp, out, op, cu,                                                 \
                      q_rows, mask, mask_L)
 #define APP_MP(N)                                                      \
@@ -1117,7 +1128,12 @@ hipError_t apq_launch(const unsigned short* qkvp, float* out, unsigned short* op
 // wave attends some key) — measured 347 vs 324 us on GraphCodeBERT-shaped masks and 352 vs 325
 // on random ones at B=64 x L=640 (the if / else around the tile's work costs 38 registers and
 // the schedule more than the skipped tiles return; tools/attn_bench.py --mask --mask-gcb): removed.
-constexpr int APP_PIPE = 67;
+// Round 6: PIPE 74 = 67 for unmasked launches; masked launches run 66 with a fast path for full
+// tiles whose mask words are all ones across the wave (the tree max, no per-key select) —
+// bit-identical to 66 (test_attention_pp_masked_fast_path_bit_identical) and 3-5 % faster on
+// GraphCodeBERT-shaped masks at B = 64 x L = 640 (302-306 vs 314-318 us; ragged 161.9 vs 174.0),
+// neutral on random masks (226.4 vs 226.9), profiles/r6v_*, r6w_*.
+constexpr int APP_PIPE = 74;
 }  // namespace
 
 extern "C" hipError_t ae_launch_attention_pp(const unsigned short* qkvp, float* out,
@@ -1146,6 +1162,7 @@ extern "C" hipError_t ae_bench_attention_pp(const unsigned short* qkvp, float* o
     case 66: return app_launch<66>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
     case 67: return app_launch<67>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
     case 72: return app_launch<72>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
+    case 74: return app_launch<74>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream);
     case 80: return mask ? app_launch<67>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream)
                          : apq_launch<2>(qkvp, out, op, cu, q_rows, max_q, n, heads, np, stream);
     case 81: return mask ? app_launch<67>(qkvp, out, op, cu, q_rows, max_q, n, heads, mask, mask_L, np, stream)

@@ -246,7 +246,7 @@ def _qkv_planes(qkv, np_):
     return _pack(hi, lo, np_)
 
 
-@pytest.mark.parametrize("variant", [6, 66, 67, 72, 80, 81, 86])
+@pytest.mark.parametrize("variant", [6, 66, 67, 72, 74, 80, 81, 86])
 @pytest.mark.parametrize("np_", [2, 1])
 @pytest.mark.parametrize("case", ["ragged", "mask", "cls", "planes", "grow"])
 def test_attention_pp_matches_f64(gpu, np_, case, variant):
@@ -353,6 +353,46 @@ def test_attention_pp_restructured_loops_bit_identical(gpu, case):
     assert torch.equal(outs[80], outs[6])  # two 32-query blocks per wave, 256-query workgroups
     assert torch.equal(outs[81], outs[6])  # the same with 3-slot K / V rings
     assert torch.equal(outs[86], outs[6])  # 81 with the K fragments read once for both blocks
+
+
+def test_attention_pp_masked_fast_path_bit_identical(gpu):
+    """Variant 74: a masked launch's full tile whose mask words are all ones for every query of
+    the wave takes the unmasked tree max (no per-key select) — GraphCodeBERT's code rows over code
+    keys.  The scores are the same, so the context must equal variant 66's (the production masked
+    loop) bit for bit, on a GraphCodeBERT-shaped mask (dense code block, sparse node rows, a node
+    row with no key at all) and ragged lengths."""
+    lib = _lib()
+    vp, i32 = ctypes.c_void_p, ctypes.c_int32
+    lib.ae_bench_attention_pp.argtypes = [vp] * 5 + [i32] * 3 + [vp, i32, i32, i32, vp]
+    lib.ae_bench_attention_pp.restype = ctypes.c_int
+    g = torch.Generator().manual_seed(21)
+    L = 320
+    lens = [320, 250, 97, 33]
+    n = len(lens)
+    cu = torch.zeros(n + 1, dtype=torch.int32)
+    cu[1:] = torch.cumsum(torch.tensor(lens), 0)
+    T = int(cu[-1])
+    dense = torch.zeros(n, L, L, dtype=torch.bool)
+    for i, ln in enumerate(lens):
+        ncode = max(1, ln - ln // 5)
+        dense[i, :ncode, :ncode] = True
+        for q in range(ncode, ln - 1):  # node rows: a few code keys and one node key
+            a = int(torch.randint(0, ncode, (1,), generator=g))
+            dense[i, q, a:a + 3] = True
+            dense[i, q, ncode + int(torch.randint(0, ln - ncode, (1,), generator=g))] = True
+    words = (dense.view(n, L, L // 32, 32).long() << torch.arange(32)).sum(-1)
+    dmask = (words - (words >= 2 ** 31).long() * 2 ** 32).to(torch.int32).cuda()
+    qkv = torch.randn(T, 3 * 768, generator=g)
+    dq, dcu = _qkv_planes(qkv, 2).cuda(), cu.cuda()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    outs = {}
+    for v in (66, 74):
+        op = torch.zeros((T, 2 * 768), dtype=torch.int16, device="cuda")
+        assert lib.ae_bench_attention_pp(_p(dq), None, _p(op), _p(dcu), None, max(lens), n, 12,
+                                         _p(dmask), L, 2, v, st) == 0
+        outs[v] = op
+    torch.cuda.synchronize()
+    assert torch.equal(outs[74], outs[66])
 
 
 def _fold_lib():
