@@ -475,13 +475,18 @@ __global__ __launch_bounds__(256, (PIPE >= 60 && !(HAS_MASK && NP == 2)) ? 3 : 2
             a[5] = s_cur[15];
             mt = max_nc(max_nc(a[0], max_nc(a[1], a[2])), max_nc(a[3], max_nc(a[4], a[5])));
           } else {
+            // the lane half's 4-key offset taken out once per tile, so every per-key bit position
+            // and bound below is a compile-time constant (no 16 per-lane shift amounts held
+            // across the loop)
+            const uint32_t mbh = mb >> (4 * lh);
+            const int lim = len - kt * KT - 4 * lh;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              const int kk = mfma32_row(r, lh);
+              const int k0 = mfma32_row(r, 0);
               // absent keys -inf; keys the mask excludes the most negative finite float (HF's
               // additive finfo.min mask), as tile_max
-              const bool in = kt * KT + kk < len;
-              s_cur[r] = !in ? -INFINITY : (((mb >> kk) & 1u) ? s_cur[r] : -FLT_MAX);
+              const bool in = k0 < lim;
+              s_cur[r] = !in ? -INFINITY : (((mbh >> k0) & 1u) ? s_cur[r] : -FLT_MAX);
               mt = max_nc(mt, s_cur[r]);
             }
           }
